@@ -1,0 +1,137 @@
+/*
+ * sezkp_stark.h — C ABI of the MI355X-native STARK v1 prover hot path.
+ *
+ * Drop-in boundary for logannye/streaming-zero-knowledge-proofs:
+ *   - top level: replaces `impl ProvingBackend for StarkV1`
+ *     (crates/sezkp-core/src/backend.rs:41-61, crates/sezkp-stark/src/lib.rs:126-190);
+ *   - version symbols: crates/sezkp-ffi/src/lib.rs:65-79 (ABI bumped 1 -> 2);
+ *   - kernel level: the hot loops of crates/sezkp-ffts (ntt.rs:79-177,
+ *     coset.rs:85-102), crates/sezkp-stark/src/v1/{lde.rs:42-97,
+ *     fri_stream.rs:37-121, merkle.rs:46-160, prover.rs:200-239}.
+ * Plain pointers and sizes only; no exceptions or aborts cross this boundary:
+ * every entry point returns 0 on success or a negative SEZKP_E_* code and
+ * writes a NUL-terminated message into `err` (when err_len > 0).
+ * Outputs of type sezkp_buf are library-allocated; release with sezkp_buf_free.
+ * Thread safety: calls on distinct sezkp_ctx objects may run concurrently.
+ */
+#ifndef SEZKP_STARK_H
+#define SEZKP_STARK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SEZKP_ABI_VERSION 2u
+
+#define SEZKP_OK 0
+#define SEZKP_E_INVALID (-1)   /* malformed input (shape, non power-of-two n, ...) */
+#define SEZKP_E_DEVICE (-2)    /* HIP runtime / kernel failure */
+#define SEZKP_E_NOMEM (-3)
+#define SEZKP_E_DECODE (-4)    /* CBOR/bincode decode failure */
+#define SEZKP_E_VERIFY (-5)    /* proof rejected */
+
+#define SEZKP_FLAG_STREAMING 1u /* meta gains "mode":"streaming" (StarkV1::prove_streaming, lib.rs:170-190) */
+
+/* crates/sezkp-ffi/src/lib.rs:65-79 */
+uint32_t sezkp_abi_version(void);
+const char* sezkp_version(void);
+
+typedef struct sezkp_buf {
+    uint8_t* data;
+    size_t len;
+} sezkp_buf;
+void sezkp_buf_free(sezkp_buf* b);
+
+/* Struct-of-arrays view of &[BlockSummary] (crates/sezkp-core/src/types.rs:116-151).
+ * Every block has exactly `tau` windows / head offsets; every step has exactly
+ * `tau` tape ops (tape-op arrays are step-major: [step*tau + r]). */
+typedef struct sezkp_block_view {
+    uint32_t n_blocks;
+    uint32_t tau;
+    const uint16_t* version;     /* [n_blocks] */
+    const uint32_t* block_id;    /* [n_blocks] */
+    const uint64_t* step_lo;     /* [n_blocks] */
+    const uint64_t* step_hi;     /* [n_blocks] */
+    const uint16_t* ctrl_in;     /* [n_blocks] */
+    const uint16_t* ctrl_out;    /* [n_blocks] */
+    const int64_t* in_head_in;   /* [n_blocks] */
+    const int64_t* in_head_out;  /* [n_blocks] */
+    const int64_t* win_left;     /* [n_blocks*tau] */
+    const int64_t* win_right;    /* [n_blocks*tau] */
+    const uint32_t* off_in;      /* [n_blocks*tau] head_in_offsets */
+    const uint32_t* off_out;     /* [n_blocks*tau] head_out_offsets */
+    const uint64_t* step_start;  /* [n_blocks+1] prefix offsets into the step arrays */
+    const int8_t* input_mv;      /* [total_steps] */
+    const int8_t* mv;            /* [total_steps*tau] */
+    const uint8_t* has_write;    /* [total_steps*tau] */
+    const uint16_t* wsym;        /* [total_steps*tau] (symbol when has_write) */
+} sezkp_block_view;
+
+/* ---------------------------------------------------------------- top level
+ * StarkV1::prove / prove_streaming (lib.rs:129-141, 170-190): proof_bytes is
+ * bincode(ProofV1) (proof.rs:80-98), meta_json the artifact meta. */
+int32_t sezkp_stark_v1_prove(const sezkp_block_view* blocks, const uint8_t manifest_root[32], uint32_t flags,
+                             sezkp_buf* proof_bytes, sezkp_buf* meta_json, char* err, size_t err_len);
+/* Same, returning the whole ProofArtifact as CBOR (io.rs:176-183). */
+int32_t sezkp_stark_v1_prove_artifact_cbor(const sezkp_block_view* blocks, const uint8_t manifest_root[32],
+                                           uint32_t flags, sezkp_buf* artifact_cbor, char* err, size_t err_len);
+/* StarkV1::verify (lib.rs:144-162 -> v1/verify.rs:60-196) on the host CPU. */
+int32_t sezkp_stark_v1_verify(const uint8_t* proof_bytes, size_t len, const sezkp_block_view* blocks,
+                              const uint8_t manifest_root[32], char* err, size_t err_len);
+
+/* ------------------------------------------------ resident-input context
+ * One context = one device + one stream + a workspace sized on upload.
+ * upload() builds the device trace image (HBM) from the block view;
+ * prove() then runs the whole prover with inputs resident in HBM. */
+typedef struct sezkp_ctx sezkp_ctx;
+sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len);
+void sezkp_ctx_destroy(sezkp_ctx* ctx);
+int32_t sezkp_ctx_upload(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len);
+int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, sezkp_buf* proof_bytes,
+                        char* err, size_t err_len);
+/* Per-stage device times (ms) of the last prove, measured with HIP events on
+ * the context's stream. Order: expand, col_commit, col_outer, compose, intt,
+ * lde_ntt, deep, layer0_tree, fri_fold_trees, fri_paths, col_openings, total.
+ * Returns the number of stages written. */
+int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max);
+/* Device hipStream_t of the context (as void*), for external timing. */
+void* sezkp_ctx_stream(const sezkp_ctx* ctx);
+
+/* ------------------------------------------------ kernel-level entry points
+ * Device pointers (u64 canonical Goldilocks, natural order), 32-byte digests,
+ * stream = hipStream_t (NULL = default stream). Asynchronous on `stream`. */
+/* In-place NTT (dir=+1 forward, -1 inverse incl. n^-1), natural -> natural:
+ * ntt.rs:79-155. `scratch` must hold 2^log_n elements. */
+int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir, void* stream);
+/* Coset LDE + DEEP (lde.rs:42-97): evals[2^log_n] (base-domain values) ->
+ * out[2^(log_n+log_blowup)] = y_i / (shift*w^i - z), shift fixed to 3.
+ * `evals` is overwritten. */
+int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_blowup, uint64_t z, uint64_t* out,
+                                void* stream);
+/* FRI fold (prover.rs:208-230): out[i] = in[i] + beta*in[i+n], i < n. Also
+ * hashes the folded leaves into a Merkle tree whose root lands in root32. */
+int32_t sezkp_fri_fold_commit(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, uint8_t* root32,
+                              void* stream);
+/* BLAKE3 leaves of 8-byte LE field values (merkle.rs:150-160) -> Merkle root
+ * (merkle.rs:46-71), n a power of two. */
+int32_t sezkp_merkle_root_u64(const uint64_t* vals, uint64_t n, uint8_t* root32, void* stream);
+
+/* ------------------------------------------------ host helpers (CPU)
+ * Manifest leaf_hash + merkle_root (crates/sezkp-merkle/src/lib.rs:85-157). */
+int32_t sezkp_manifest_root(const sezkp_block_view* blocks, uint8_t out[32]);
+/* Decode a CBOR Vec<BlockSummary> (io.rs:57-65). The returned handle owns the
+ * arrays a view points to; free with sezkp_blocks_free. */
+typedef struct sezkp_blocks sezkp_blocks;
+int32_t sezkp_blocks_decode_cbor(const uint8_t* data, size_t len, sezkp_blocks** out, char* err, size_t err_len);
+const sezkp_block_view* sezkp_blocks_view(const sezkp_blocks* b);
+void sezkp_blocks_free(sezkp_blocks* b);
+/* BLAKE3 hash with extendable output (host). */
+void sezkp_blake3(const uint8_t* data, size_t len, uint8_t* out, size_t out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SEZKP_STARK_H */

@@ -34,6 +34,8 @@ class _OrcBlocks(C.Structure):
 
 def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
+    global _lib
+    _lib = None
 
 
 _lib = None
@@ -55,6 +57,7 @@ def lib():
         L.orc_ntt_inverse.argtypes = [C.c_void_p, C.c_size_t]
         L.orc_coset_lde.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_void_p]
         L.orc_det_vec.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.orc_lde_deep.argtypes = [C.c_void_p, C.c_size_t, C.c_uint, C.c_uint64, C.c_void_p]
         L.orc_blake3.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t]
         L.orc_tr_new.restype = C.c_void_p
         L.orc_tr_new.argtypes = [C.c_char_p]
@@ -161,6 +164,13 @@ def coset_lde(coeffs: np.ndarray, k_log2: int, shift: int) -> np.ndarray:
 def det_vec(n: int, seed: int) -> np.ndarray:
     out = np.zeros(n, dtype=np.uint64)
     lib().orc_det_vec(out.ctypes.data, n, seed)
+    return out
+
+
+def lde_deep(base: np.ndarray, blow_log2: int, z: int) -> np.ndarray:
+    b = np.ascontiguousarray(base, dtype=np.uint64)
+    out = np.zeros(b.size << blow_log2, dtype=np.uint64)
+    lib().orc_lde_deep(b.ctypes.data, b.size, blow_log2, z, out.ctypes.data)
     return out
 
 

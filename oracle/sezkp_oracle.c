@@ -827,6 +827,13 @@ static uint64_t *lde_deep(const uint64_t *base_vals, size_t n, unsigned blow_log
     return y;
 }
 
+/* lde.rs:42-97 as a standalone entry (blowup 2^blow_log2, shift 3) */
+void orc_lde_deep(const uint64_t *base_vals, size_t n, unsigned blow_log2, uint64_t z, uint64_t *out) {
+    uint64_t *y = lde_deep(base_vals, n, blow_log2, 3, z);
+    memcpy(out, y, (n << blow_log2) * sizeof(uint64_t));
+    free(y);
+}
+
 /* ========================================================================
  * prove_v1 — prover.rs:61-462
  * ====================================================================== */

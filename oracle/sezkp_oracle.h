@@ -62,6 +62,7 @@ void orc_ntt_forward(uint64_t *a, size_t n);
 void orc_ntt_inverse(uint64_t *a, size_t n);
 void orc_coset_lde(const uint64_t *coeffs, size_t m, uint32_t k_log2, uint64_t shift, uint64_t *out);
 void orc_det_vec(uint64_t *out, size_t n, uint64_t seed); /* benches/ntt.rs:21-34 */
+void orc_lde_deep(const uint64_t *base_vals, size_t n, unsigned blow_log2, uint64_t z, uint64_t *out); /* lde.rs:42-97 */
 
 /* ---- BLAKE3 (spec restatement of crates.io blake3 1.8.2) ---- */
 void orc_blake3(const uint8_t *in, size_t len, uint8_t *out, size_t out_len);

@@ -1,0 +1,248 @@
+// cli.cpp — `sezkp-cli` drop-in for the STARK path on MI355X:
+//   prove  --backend stark --blocks B --manifest M --out P [--stream] [--assume-committed]
+//   verify --backend stark --blocks B --manifest M --proof P [--assume-committed]
+//   commit --blocks B --out M
+// Semantics follow crates/sezkp-cli/src/main.rs:429-578 (manifest precheck,
+// .json/.cbor block files only for prove/verify, write_proof_auto by extension)
+// and crates/sezkp-merkle/src/lib.rs:259-337 (commit / precheck).
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/sezkp_stark.h"
+#include "codec.h"
+#include "host_crypto.h"
+
+using namespace sezkp;
+
+namespace {
+
+std::string ext_lower(const std::string& p) {
+  size_t d = p.find_last_of('.');
+  size_t s = p.find_last_of('/');
+  if (d == std::string::npos || (s != std::string::npos && d < s)) return "";
+  std::string e = p.substr(d + 1);
+  for (auto& c : e) c = (char)tolower((unsigned char)c);
+  return e;
+}
+std::string hex(const uint8_t* p, size_t n) {
+  static const char* H = "0123456789abcdef";
+  std::string s;
+  for (size_t i = 0; i < n; i++) { s += H[p[i] >> 4]; s += H[p[i] & 15]; }
+  return s;
+}
+bool read_file(const std::string& path, std::vector<uint8_t>& out, std::string& err) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) { err = "open " + path; return false; }
+  out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+  return true;
+}
+bool write_file(const std::string& path, const std::vector<uint8_t>& data, std::string& err) {
+  std::ofstream f(path, std::ios::binary);
+  if (!f) { err = "create " + path; return false; }
+  f.write((const char*)data.data(), (std::streamsize)data.size());
+  return (bool)f;
+}
+
+bool load_blocks(const std::string& path, BlockStore& bs, std::string& err) {  // io.rs:78-88
+  const std::string e = ext_lower(path);
+  std::vector<uint8_t> raw;
+  if (e != "json" && e != "cbor") {
+    err = e.empty() ? "path has no extension (expected .json or .cbor)"
+                    : "unsupported blocks extension: " + e + " (supported: .json, .cbor)";
+    return false;
+  }
+  if (!read_file(path, raw, err)) return false;
+  if (e == "cbor") return decode_blocks_cbor(raw.data(), raw.size(), bs, err);
+  return decode_blocks_json((const char*)raw.data(), raw.size(), bs, err);
+}
+bool load_manifest(const std::string& path, uint8_t root[32], uint32_t* n_leaves, std::string& err) {
+  const std::string e = ext_lower(path);
+  std::vector<uint8_t> raw;
+  if (e != "json" && e != "cbor") {
+    err = e.empty() ? "path has no extension (expected .json or .cbor)" : "unsupported manifest extension: " + e;
+    return false;
+  }
+  if (!read_file(path, raw, err)) return false;
+  if (e == "cbor") return decode_manifest_cbor(raw.data(), raw.size(), root, n_leaves, err);
+  return decode_manifest_json((const char*)raw.data(), raw.size(), root, n_leaves, err);
+}
+
+// serde_json::to_writer_pretty layout of a ProofArtifact
+std::string pretty_artifact(const Artifact& a) {
+  std::ostringstream o;
+  auto arr = [&](const std::vector<uint8_t>& v) {
+    if (v.empty()) { o << "[]"; return; }
+    o << "[\n";
+    for (size_t i = 0; i < v.size(); i++) o << "    " << (unsigned)v[i] << (i + 1 < v.size() ? ",\n" : "\n");
+    o << "  ]";
+  };
+  o << "{\n  \"backend\": \"" << a.backend << "\",\n  \"manifest_root\": ";
+  arr(a.manifest_root);
+  o << ",\n  \"proof_bytes\": ";
+  arr(a.proof_bytes);
+  o << ",\n  \"meta\": " << a.meta_json << "\n}";
+  return o.str();
+}
+
+struct Args {
+  std::string cmd, backend = "stark", blocks, manifest, out, proof;
+  bool stream = false, assume = false;
+};
+
+int precheck(const Args& a, const BlockStore& bs) {  // verify_block_file_against_manifest
+  uint8_t mroot[32], got[32];
+  uint32_t nl = 0;
+  std::string err;
+  if (!load_manifest(a.manifest, mroot, &nl, err)) {
+    fprintf(stderr, "Error: blocks/manifest mismatch: %s\n", err.c_str());
+    return 1;
+  }
+  manifest_root(bs.view, got);
+  if (memcmp(got, mroot, 32) != 0) {
+    fprintf(stderr, "Error: blocks/manifest mismatch: root mismatch: manifest=%s, recomputed=%s\n",
+            hex(mroot, 32).c_str(), hex(got, 32).c_str());
+    return 1;
+  }
+  if (nl != bs.view.n_blocks) {
+    fprintf(stderr, "Error: blocks/manifest mismatch: leaf count mismatch: manifest=%u, recomputed=%u\n", nl,
+            bs.view.n_blocks);
+    return 1;
+  }
+  return 0;
+}
+
+int cmd_prove(const Args& a) {
+  std::string err;
+  BlockStore bs;
+  if (!load_blocks(a.blocks, bs, err)) { fprintf(stderr, "Error: reading blocks: %s\n", err.c_str()); return 1; }
+  if (!a.assume && precheck(a, bs)) return 1;
+  uint8_t mroot[32];
+  if (!load_manifest(a.manifest, mroot, nullptr, err)) { fprintf(stderr, "Error: reading manifest: %s\n", err.c_str()); return 1; }
+  sezkp_buf art{};
+  char msg[512] = {0};
+  const int32_t rc = sezkp_stark_v1_prove_artifact_cbor(&bs.view, mroot, a.stream ? SEZKP_FLAG_STREAMING : 0, &art,
+                                                        msg, sizeof msg);
+  if (rc) { fprintf(stderr, "Error: stark-v1 proof failed: %s\n", msg); return 1; }
+  std::vector<uint8_t> cbor(art.data, art.data + art.len);
+  sezkp_buf_free(&art);
+  Artifact dec;
+  decode_artifact_cbor(cbor.data(), cbor.size(), dec, err);
+  std::vector<uint8_t> outb = cbor;
+  if (ext_lower(a.out) != "cbor") {  // write_proof_auto: JSON unless .cbor (io.rs:199-205)
+    const bool streaming = a.stream;
+    uint64_t domain_n = 0;
+    for (int i = 7; i >= 0; i--) domain_n = (domain_n << 8) | dec.proof_bytes[i];
+    std::vector<MetaEntry> meta = {{"proto", true, "stark-v1", 0}, {"domain_n", false, "", domain_n},
+                                   {"tau", false, "", bs.view.tau}};
+    if (streaming) meta.push_back({"mode", true, "streaming", 0});
+    // serde_json pretty nests the meta object one level deeper
+    std::string mj = meta_to_json(meta);
+    std::string nested = "{\n";
+    {
+      std::vector<MetaEntry> m = meta;
+      std::sort(m.begin(), m.end(), [](const MetaEntry& x, const MetaEntry& y) { return x.key < y.key; });
+      for (size_t i = 0; i < m.size(); i++)
+        nested += "    \"" + m[i].key + "\": " + (m[i].is_str ? "\"" + m[i].s + "\"" : std::to_string(m[i].u)) +
+                  (i + 1 < m.size() ? ",\n" : "\n");
+      nested += "  }";
+    }
+    (void)mj;
+    dec.meta_json = nested;
+    std::string js = pretty_artifact(dec);
+    outb.assign(js.begin(), js.end());
+  }
+  if (!write_file(a.out, outb, err)) { fprintf(stderr, "Error: writing proof to %s: %s\n", a.out.c_str(), err.c_str()); return 1; }
+  printf("Proved with Stark, wrote %s (%zu bytes)\n", a.out.c_str(), dec.proof_bytes.size());
+  return 0;
+}
+
+int cmd_verify(const Args& a) {
+  std::string err;
+  BlockStore bs;
+  if (!load_blocks(a.blocks, bs, err)) { fprintf(stderr, "Error: reading blocks: %s\n", err.c_str()); return 1; }
+  if (!a.assume && precheck(a, bs)) return 1;
+  uint8_t mroot[32];
+  if (!load_manifest(a.manifest, mroot, nullptr, err)) { fprintf(stderr, "Error: reading manifest: %s\n", err.c_str()); return 1; }
+  std::vector<uint8_t> raw;
+  if (!read_file(a.proof, raw, err)) { fprintf(stderr, "Error: reading proof artifact: %s\n", err.c_str()); return 1; }
+  if (ext_lower(a.proof) != "cbor") { fprintf(stderr, "Error: only .cbor proof artifacts are supported for verify\n"); return 1; }
+  Artifact art;
+  if (!decode_artifact_cbor(raw.data(), raw.size(), art, err)) { fprintf(stderr, "Error: %s\n", err.c_str()); return 1; }
+  if (art.backend != "stark") { fprintf(stderr, "Error: stark-v1 verification failed: backend kind mismatch: expected STARK\n"); return 1; }
+  if (art.manifest_root.size() != 32 || memcmp(art.manifest_root.data(), mroot, 32)) {
+    fprintf(stderr, "Error: stark-v1 verification failed: manifest root mismatch\n");
+    return 1;
+  }
+  char msg[512] = {0};
+  if (sezkp_stark_v1_verify(art.proof_bytes.data(), art.proof_bytes.size(), &bs.view, mroot, msg, sizeof msg)) {
+    fprintf(stderr, "Error: stark-v1 verification failed: %s\n", msg);
+    return 1;
+  }
+  printf("OK: proof verified\n");
+  return 0;
+}
+
+int cmd_commit(const Args& a) {
+  std::string err;
+  BlockStore bs;
+  if (!load_blocks(a.blocks, bs, err)) { fprintf(stderr, "Error: read blocks %s: %s\n", a.blocks.c_str(), err.c_str()); return 1; }
+  uint8_t root[32];
+  manifest_root(bs.view, root);
+  std::vector<uint8_t> out;
+  if (ext_lower(a.out) == "cbor") out = encode_manifest_cbor(root, bs.view.n_blocks);
+  else {
+    std::string s = "{\n  \"version\": 1,\n  \"root\": [\n";
+    for (int i = 0; i < 32; i++) s += "    " + std::to_string(root[i]) + (i < 31 ? ",\n" : "\n");
+    s += "  ],\n  \"n_leaves\": " + std::to_string(bs.view.n_blocks) + "\n}";
+    out.assign(s.begin(), s.end());
+  }
+  if (!write_file(a.out, out, err)) { fprintf(stderr, "Error: %s\n", err.c_str()); return 1; }
+  printf("Committed %u leaves, root=%s, wrote manifest %s\n", bs.view.n_blocks, hex(root, 32).c_str(), a.out.c_str());
+  return 0;
+}
+
+void usage() {
+  fprintf(stderr,
+          "usage: sezkp-cli prove  --backend stark --blocks B --manifest M --out P [--stream] [--assume-committed]\n"
+          "       sezkp-cli verify --backend stark --blocks B --manifest M --proof P [--assume-committed]\n"
+          "       sezkp-cli commit --blocks B --out M\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) { usage(); return 2; }
+  Args a;
+  a.cmd = argv[1];
+  for (int i = 2; i < argc; i++) {
+    std::string s = argv[i];
+    auto val = [&](std::string& dst) {
+      if (i + 1 >= argc) { usage(); exit(2); }
+      dst = argv[++i];
+    };
+    if (s == "--backend" || s == "-b") val(a.backend);
+    else if (s == "--blocks") val(a.blocks);
+    else if (s == "--manifest") val(a.manifest);
+    else if (s == "--out" || s == "-o") val(a.out);
+    else if (s == "--proof") val(a.proof);
+    else if (s == "--stream") a.stream = true;
+    else if (s == "--assume-committed") a.assume = true;
+    else { fprintf(stderr, "unknown argument %s\n", s.c_str()); usage(); return 2; }
+  }
+  for (auto& c : a.backend) c = (char)tolower((unsigned char)c);
+  if (a.cmd == "commit") return cmd_commit(a);
+  if (a.backend != "stark") {
+    fprintf(stderr, "Error: only --backend stark is implemented by the MI355X build\n");
+    return 2;
+  }
+  if (a.cmd == "prove") return cmd_prove(a);
+  if (a.cmd == "verify") return cmd_verify(a);
+  usage();
+  return 2;
+}

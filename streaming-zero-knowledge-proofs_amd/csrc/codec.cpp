@@ -1,0 +1,537 @@
+// codec.cpp — CBOR/JSON decode of Vec<BlockSummary> and manifests, CBOR
+// encode of ProofArtifact, manifest commitment. Pull parsers decode straight
+// into the struct-of-arrays store (no DOM), so multi-GB block files stream.
+#include "codec.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "host_crypto.h"
+
+namespace sezkp {
+
+void BlockStore::bind() {
+  view.n_blocks = (uint32_t)version.size();
+  view.tau = tau;
+  view.version = version.data();
+  view.block_id = block_id.data();
+  view.step_lo = step_lo.data();
+  view.step_hi = step_hi.data();
+  view.ctrl_in = ctrl_in.data();
+  view.ctrl_out = ctrl_out.data();
+  view.in_head_in = in_head_in.data();
+  view.in_head_out = in_head_out.data();
+  view.win_left = win_left.data();
+  view.win_right = win_right.data();
+  view.off_in = off_in.data();
+  view.off_out = off_out.data();
+  view.step_start = step_start.data();
+  view.input_mv = input_mv.data();
+  view.mv = mv.data();
+  view.has_write = has_write.data();
+  view.wsym = wsym.data();
+}
+
+namespace {
+
+struct DecodeError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// ------------------------------------------------------------- CBOR pull
+class Cbor {
+ public:
+  Cbor(const uint8_t* p, size_t n) : p_(p), e_(p + n) {}
+  bool done() const { return p_ == e_; }
+  // container start: returns count, or -1 for indefinite length
+  int64_t begin_array() { return container(4); }
+  int64_t begin_map() { return container(5); }
+  bool more(int64_t& remaining) {  // iterate a container
+    if (remaining >= 0) return remaining-- > 0;
+    need(1);
+    if (*p_ == 0xff) { p_++; return false; }
+    return true;
+  }
+  std::string key() {
+    int mj; uint64_t v; bool ind;
+    head(mj, v, ind);
+    if (mj != 3 || ind) throw DecodeError("expected text key");
+    need(v);
+    std::string s((const char*)p_, (size_t)v);
+    p_ += v;
+    return s;
+  }
+  bool null() {
+    need(1);
+    if (*p_ == 0xf6 || *p_ == 0xf7) { p_++; return true; }
+    return false;
+  }
+  int64_t sint() {
+    int mj; uint64_t v; bool ind;
+    head(mj, v, ind);
+    if (mj == 0) { if (v > (uint64_t)INT64_MAX) throw DecodeError("int overflow"); return (int64_t)v; }
+    if (mj == 1) { if (v > (uint64_t)INT64_MAX) throw DecodeError("int overflow"); return -1 - (int64_t)v; }
+    throw DecodeError("expected integer");
+  }
+  uint64_t uint() {
+    int mj; uint64_t v; bool ind;
+    head(mj, v, ind);
+    if (mj != 0) throw DecodeError("expected unsigned integer");
+    return v;
+  }
+  std::string text() { return key(); }
+  void skip() {
+    int mj; uint64_t v; bool ind;
+    head(mj, v, ind);
+    switch (mj) {
+      case 0: case 1: case 7: return;
+      case 2: case 3:
+        if (ind) { while (!brk()) skip(); return; }
+        need(v); p_ += v; return;
+      case 4: case 5: {
+        const int per = mj == 5 ? 2 : 1;
+        if (ind) { while (!brk()) for (int i = 0; i < per; i++) skip(); return; }
+        for (uint64_t i = 0; i < v * per; i++) skip();
+        return;
+      }
+      case 6: skip(); return;
+    }
+  }
+
+ private:
+  void need(uint64_t k) { if ((uint64_t)(e_ - p_) < k) throw DecodeError("truncated CBOR"); }
+  bool brk() { need(1); if (*p_ == 0xff) { p_++; return true; } return false; }
+  void head(int& mj, uint64_t& v, bool& ind) {
+    need(1);
+    uint8_t b = *p_++;
+    mj = b >> 5;
+    int ai = b & 31;
+    ind = false;
+    if (ai < 24) { v = ai; return; }
+    int nb = ai == 24 ? 1 : ai == 25 ? 2 : ai == 26 ? 4 : ai == 27 ? 8 : 0;
+    if (ai == 31) { ind = true; v = 0; return; }
+    if (!nb) throw DecodeError("bad CBOR head");
+    need(nb);
+    v = 0;
+    for (int i = 0; i < nb; i++) v = (v << 8) | *p_++;
+  }
+  int64_t container(int want) {
+    int mj; uint64_t v; bool ind;
+    head(mj, v, ind);
+    if (mj != want) throw DecodeError(want == 4 ? "expected array" : "expected map");
+    return ind ? -1 : (int64_t)v;
+  }
+  const uint8_t* p_;
+  const uint8_t* e_;
+};
+
+// ------------------------------------------------------------- JSON pull
+class Json {
+ public:
+  Json(const char* p, size_t n) : p_(p), e_(p + n) {}
+  bool done() { ws(); return p_ == e_; }
+  int64_t begin_array() { ws(); expect('['); first_ = true; return -1; }
+  int64_t begin_map() { ws(); expect('{'); first_ = true; return -1; }
+  bool more(int64_t&) {
+    ws();
+    if (p_ < e_ && (*p_ == ']' || *p_ == '}')) { p_++; first_ = false; return false; }
+    if (!first_) { expect(','); ws(); }
+    first_ = false;
+    return true;
+  }
+  std::string key() {
+    std::string k = str();
+    ws();
+    expect(':');
+    first_ = false;
+    return k;
+  }
+  bool null() {
+    ws();
+    if (e_ - p_ >= 4 && !memcmp(p_, "null", 4)) { p_ += 4; return true; }
+    return false;
+  }
+  int64_t sint() {
+    ws();
+    bool neg = false;
+    if (p_ < e_ && *p_ == '-') { neg = true; p_++; }
+    uint64_t v = digits();
+    if (v > (uint64_t)INT64_MAX + (neg ? 1 : 0)) throw DecodeError("int overflow");
+    return neg ? (int64_t)(0 - v) : (int64_t)v;
+  }
+  uint64_t uint() { ws(); return digits(); }
+  std::string text() { return str(); }
+  void skip() {
+    ws();
+    if (p_ >= e_) throw DecodeError("truncated JSON");
+    char c = *p_;
+    if (c == '"') { str(); return; }
+    if (c == '[' || c == '{') {
+      int64_t r = c == '[' ? begin_array() : begin_map();
+      while (more(r)) { if (c == '{') key(); skip(); }
+      return;
+    }
+    while (p_ < e_ && *p_ != ',' && *p_ != ']' && *p_ != '}' && !isspace((unsigned char)*p_)) p_++;
+  }
+
+ private:
+  void ws() { while (p_ < e_ && isspace((unsigned char)*p_)) p_++; }
+  void expect(char c) {
+    ws();
+    if (p_ >= e_ || *p_ != c) throw DecodeError(std::string("JSON: expected '") + c + "'");
+    p_++;
+  }
+  uint64_t digits() {
+    if (p_ >= e_ || !isdigit((unsigned char)*p_)) throw DecodeError("JSON: expected number");
+    uint64_t v = 0;
+    while (p_ < e_ && isdigit((unsigned char)*p_)) {
+      uint64_t d = *p_++ - '0';
+      if (v > (UINT64_MAX - d) / 10) throw DecodeError("JSON: number overflow");
+      v = v * 10 + d;
+    }
+    if (p_ < e_ && (*p_ == '.' || *p_ == 'e' || *p_ == 'E')) throw DecodeError("JSON: non-integer number");
+    return v;
+  }
+  std::string str() {
+    ws();
+    expect('"');
+    std::string s;
+    while (p_ < e_ && *p_ != '"') {
+      if (*p_ == '\\') { p_++; if (p_ >= e_) break; }
+      s.push_back(*p_++);
+    }
+    expect('"');
+    return s;
+  }
+  const char* p_;
+  const char* e_;
+  bool first_ = false;
+};
+
+template <class P>
+void decode_tape_op(P& d, BlockStore& s) {
+  int64_t r = d.begin_map();
+  bool has = false;
+  uint64_t sym = 0;
+  int64_t mv = 0;
+  while (d.more(r)) {
+    std::string k = d.key();
+    if (k == "write") {
+      if (!d.null()) { has = true; sym = d.uint(); if (sym > 0xffff) throw DecodeError("write symbol > u16"); }
+    } else if (k == "mv") {
+      mv = d.sint();
+      if (mv < -128 || mv > 127) throw DecodeError("mv out of i8 range");
+    } else {
+      d.skip();
+    }
+  }
+  s.mv.push_back((int8_t)mv);
+  s.has_write.push_back(has ? 1 : 0);
+  s.wsym.push_back(has ? (uint16_t)sym : 0);
+}
+
+struct BlockShape {
+  std::vector<uint32_t> nwin, nin, nout;
+  std::vector<uint32_t> ntape;  // per step
+};
+
+template <class P>
+void decode_block(P& d, BlockStore& s, BlockShape& sh) {
+  int64_t r = d.begin_map();
+  uint32_t nwin = 0, nin = 0, nout = 0;
+  const uint64_t steps_before = s.input_mv.size();
+  s.version.push_back(0); s.block_id.push_back(0); s.step_lo.push_back(0); s.step_hi.push_back(0);
+  s.ctrl_in.push_back(0); s.ctrl_out.push_back(0); s.in_head_in.push_back(0); s.in_head_out.push_back(0);
+  while (d.more(r)) {
+    std::string k = d.key();
+    if (k == "version") s.version.back() = (uint16_t)d.uint();
+    else if (k == "block_id") s.block_id.back() = (uint32_t)d.uint();
+    else if (k == "step_lo") s.step_lo.back() = d.uint();
+    else if (k == "step_hi") s.step_hi.back() = d.uint();
+    else if (k == "ctrl_in") s.ctrl_in.back() = (uint16_t)d.uint();
+    else if (k == "ctrl_out") s.ctrl_out.back() = (uint16_t)d.uint();
+    else if (k == "in_head_in") s.in_head_in.back() = d.sint();
+    else if (k == "in_head_out") s.in_head_out.back() = d.sint();
+    else if (k == "windows") {
+      int64_t a = d.begin_array();
+      while (d.more(a)) {
+        int64_t m = d.begin_map();
+        int64_t left = 0, right = 0;
+        while (d.more(m)) {
+          std::string wk = d.key();
+          if (wk == "left") left = d.sint();
+          else if (wk == "right") right = d.sint();
+          else d.skip();
+        }
+        s.win_left.push_back(left);
+        s.win_right.push_back(right);
+        nwin++;
+      }
+    } else if (k == "head_in_offsets" || k == "head_out_offsets") {
+      const bool in = k == "head_in_offsets";
+      int64_t a = d.begin_array();
+      while (d.more(a)) {
+        uint64_t x = d.uint();
+        if (x > 0xffffffffULL) throw DecodeError("offset > u32");
+        (in ? s.off_in : s.off_out).push_back((uint32_t)x);
+        (in ? nin : nout)++;
+      }
+    } else if (k == "movement_log") {
+      int64_t m = d.begin_map();
+      while (d.more(m)) {
+        std::string mk = d.key();
+        if (mk != "steps") { d.skip(); continue; }
+        int64_t a = d.begin_array();
+        while (d.more(a)) {
+          int64_t sm = d.begin_map();
+          int64_t imv = 0;
+          uint32_t ntape = 0;
+          while (d.more(sm)) {
+            std::string sk = d.key();
+            if (sk == "input_mv") {
+              imv = d.sint();
+              if (imv < -128 || imv > 127) throw DecodeError("input_mv out of i8 range");
+            } else if (sk == "tapes") {
+              int64_t ta = d.begin_array();
+              while (d.more(ta)) { decode_tape_op(d, s); ntape++; }
+            } else {
+              d.skip();
+            }
+          }
+          s.input_mv.push_back((int8_t)imv);
+          sh.ntape.push_back(ntape);
+        }
+      }
+    } else {
+      d.skip();  // pre_tags / post_tags / unknown fields
+    }
+  }
+  sh.nwin.push_back(nwin);
+  sh.nin.push_back(nin);
+  sh.nout.push_back(nout);
+  s.step_start.push_back(s.step_start.back() + (s.input_mv.size() - steps_before));
+}
+
+template <class P>
+void decode_blocks(P& d, BlockStore& s) {
+  s.step_start.assign(1, 0);
+  BlockShape sh;
+  int64_t r = d.begin_array();
+  while (d.more(r)) decode_block(d, s, sh);
+  if (!d.done()) throw DecodeError("trailing bytes after block array");
+  // The prover reads tau = blocks[0].windows.len() and indexes every per-block
+  // vector and every step's tapes by r < tau (openings.rs:195, columns.rs:258).
+  s.tau = sh.nwin.empty() ? 0 : sh.nwin[0];
+  for (size_t k = 0; k < sh.nwin.size(); k++)
+    if (sh.nwin[k] != s.tau || sh.nin[k] != s.tau || sh.nout[k] != s.tau)
+      throw DecodeError("block " + std::to_string(k) + ": windows/head offsets length != tau");
+  for (uint32_t t : sh.ntape)
+    if (t != s.tau) throw DecodeError("step with tapes.len() != tau");
+  s.bind();
+}
+
+template <class P>
+void decode_manifest(P& d, uint8_t root[32], uint32_t* n_leaves) {
+  int64_t r = d.begin_map();
+  bool got = false;
+  while (d.more(r)) {
+    std::string k = d.key();
+    if (k == "root") {
+      int64_t a = d.begin_array();
+      int i = 0;
+      while (d.more(a)) {
+        uint64_t x = d.uint();
+        if (i >= 32 || x > 255) throw DecodeError("manifest root must be 32 bytes");
+        root[i++] = (uint8_t)x;
+      }
+      if (i != 32) throw DecodeError("manifest root must be 32 bytes");
+      got = true;
+    } else if (k == "n_leaves") {
+      uint64_t x = d.uint();
+      if (n_leaves) *n_leaves = (uint32_t)x;
+    } else {
+      d.skip();
+    }
+  }
+  if (!got) throw DecodeError("manifest without root");
+}
+
+// ------------------------------------------------------------- CBOR out
+void cb_head(std::vector<uint8_t>& o, int major, uint64_t v) {
+  const uint8_t m = (uint8_t)(major << 5);
+  if (v < 24) { o.push_back(m | (uint8_t)v); return; }
+  int nb = v < 256 ? 1 : v < 65536 ? 2 : v < (1ULL << 32) ? 4 : 8;
+  o.push_back(m | (uint8_t)(nb == 1 ? 24 : nb == 2 ? 25 : nb == 4 ? 26 : 27));
+  for (int i = nb - 1; i >= 0; i--) o.push_back((uint8_t)(v >> (8 * i)));
+}
+void cb_text(std::vector<uint8_t>& o, const std::string& s) {
+  cb_head(o, 3, s.size());
+  o.insert(o.end(), s.begin(), s.end());
+}
+void cb_byte_array(std::vector<uint8_t>& o, const uint8_t* p, size_t n) {  // serde Vec<u8>/[u8;N] -> array of uints
+  cb_head(o, 4, n);
+  for (size_t i = 0; i < n; i++) {
+    if (p[i] < 24) o.push_back(p[i]);
+    else { o.push_back(0x18); o.push_back(p[i]); }
+  }
+}
+void sort_meta(std::vector<MetaEntry>& meta) {
+  std::sort(meta.begin(), meta.end(), [](const MetaEntry& a, const MetaEntry& b) { return a.key < b.key; });
+}
+
+}  // namespace
+
+bool decode_blocks_cbor(const uint8_t* data, size_t len, BlockStore& out, std::string& err) {
+  try {
+    Cbor d(data, len);
+    decode_blocks(d, out);
+    return true;
+  } catch (const std::exception& e) {
+    err = std::string("deserialize CBOR block summaries: ") + e.what();
+    return false;
+  }
+}
+bool decode_blocks_json(const char* data, size_t len, BlockStore& out, std::string& err) {
+  try {
+    Json d(data, len);
+    decode_blocks(d, out);
+    return true;
+  } catch (const std::exception& e) {
+    err = std::string("deserialize JSON block summaries: ") + e.what();
+    return false;
+  }
+}
+bool decode_manifest_cbor(const uint8_t* data, size_t len, uint8_t root[32], uint32_t* n_leaves, std::string& err) {
+  try {
+    Cbor d(data, len);
+    decode_manifest(d, root, n_leaves);
+    return true;
+  } catch (const std::exception& e) {
+    err = std::string("deserialize CBOR manifest: ") + e.what();
+    return false;
+  }
+}
+bool decode_manifest_json(const char* data, size_t len, uint8_t root[32], uint32_t* n_leaves, std::string& err) {
+  try {
+    Json d(data, len);
+    decode_manifest(d, root, n_leaves);
+    return true;
+  } catch (const std::exception& e) {
+    err = std::string("deserialize JSON manifest: ") + e.what();
+    return false;
+  }
+}
+
+bool decode_artifact_cbor(const uint8_t* data, size_t len, Artifact& out, std::string& err) {
+  try {
+    Cbor d(data, len);
+    int64_t r = d.begin_map();
+    while (d.more(r)) {
+      std::string k = d.key();
+      if (k == "backend") out.backend = d.text();
+      else if (k == "manifest_root" || k == "proof_bytes") {
+        auto& v = k == "proof_bytes" ? out.proof_bytes : out.manifest_root;
+        int64_t a = d.begin_array();
+        while (d.more(a)) {
+          uint64_t x = d.uint();
+          if (x > 255) throw DecodeError("byte > 255");
+          v.push_back((uint8_t)x);
+        }
+      } else d.skip();
+    }
+    return true;
+  } catch (const std::exception& e) {
+    err = std::string("deserialize CBOR proof artifact: ") + e.what();
+    return false;
+  }
+}
+
+std::vector<uint8_t> encode_artifact_cbor(const std::string& backend, const uint8_t manifest_root[32],
+                                          const std::vector<uint8_t>& proof, std::vector<MetaEntry> meta) {
+  std::vector<uint8_t> o;
+  o.reserve(proof.size() * 2 + 256);
+  cb_head(o, 5, 4);
+  cb_text(o, "backend");
+  cb_text(o, backend);
+  cb_text(o, "manifest_root");
+  cb_byte_array(o, manifest_root, 32);
+  cb_text(o, "proof_bytes");
+  cb_byte_array(o, proof.data(), proof.size());
+  cb_text(o, "meta");
+  sort_meta(meta);
+  cb_head(o, 5, meta.size());
+  for (auto& m : meta) {
+    cb_text(o, m.key);
+    if (m.is_str) cb_text(o, m.s);
+    else cb_head(o, 0, m.u);
+  }
+  return o;
+}
+
+std::string meta_to_json(std::vector<MetaEntry> meta) {
+  sort_meta(meta);
+  std::string s = "{";
+  for (size_t i = 0; i < meta.size(); i++) {
+    if (i) s += ",";
+    s += "\"" + meta[i].key + "\":";
+    s += meta[i].is_str ? "\"" + meta[i].s + "\"" : std::to_string(meta[i].u);
+  }
+  return s + "}";
+}
+
+std::vector<uint8_t> encode_manifest_cbor(const uint8_t root[32], uint32_t n_leaves) {
+  std::vector<uint8_t> o;
+  cb_head(o, 5, 3);
+  cb_text(o, "version");
+  cb_head(o, 0, 1);
+  cb_text(o, "root");
+  cb_byte_array(o, root, 32);
+  cb_text(o, "n_leaves");
+  cb_head(o, 0, n_leaves);
+  return o;
+}
+
+// ----------------------------------------------------------------- manifest
+void manifest_leaf_hash(const sezkp_block_view& v, uint32_t k, uint8_t out[32]) {
+  BinWriter w;  // raw little-endian fields (sezkp-merkle/src/lib.rs:85-117)
+  const uint32_t tau = v.tau;
+  auto u16 = [&](uint16_t x) { w.raw(&x, 2); };
+  auto u32 = [&](uint32_t x) { w.raw(&x, 4); };
+  u16(v.version[k]);
+  u32(v.block_id[k]);
+  w.u64(v.step_lo[k]);
+  w.u64(v.step_hi[k]);
+  u16(v.ctrl_in[k]);
+  u16(v.ctrl_out[k]);
+  w.u64((uint64_t)v.in_head_in[k]);
+  w.u64((uint64_t)v.in_head_out[k]);
+  w.u64(tau);
+  for (uint32_t r = 0; r < tau; r++) {
+    w.u64((uint64_t)v.win_left[(size_t)k * tau + r]);
+    w.u64((uint64_t)v.win_right[(size_t)k * tau + r]);
+  }
+  for (uint32_t r = 0; r < tau; r++) u32(v.off_in[(size_t)k * tau + r]);
+  for (uint32_t r = 0; r < tau; r++) u32(v.off_out[(size_t)k * tau + r]);
+  w.u64(v.step_start[k + 1] - v.step_start[k]);
+  blake3_oneshot(w.b.data(), w.b.size(), out);
+}
+
+void manifest_root(const sezkp_block_view& v, uint8_t out[32]) {  // lib.rs:140-157, odd promotion
+  if (v.n_blocks == 0) { memset(out, 0, 32); return; }
+  std::vector<uint8_t> lv(32ull * v.n_blocks);
+  for (uint32_t k = 0; k < v.n_blocks; k++) manifest_leaf_hash(v, k, lv.data() + 32ull * k);
+  size_t n = v.n_blocks;
+  while (n > 1) {
+    size_t m = 0;
+    for (size_t i = 0; i < n; i += 2, m++) {
+      if (i + 1 < n) blake3_oneshot(lv.data() + 32 * i, 64, lv.data() + 32 * m);
+      else memmove(lv.data() + 32 * m, lv.data() + 32 * i, 32);
+    }
+    n = m;
+  }
+  memcpy(out, lv.data(), 32);
+}
+
+}  // namespace sezkp

@@ -1,0 +1,123 @@
+// dev_common.h — CDNA4 (gfx950) device primitives for the STARK v1 hot path:
+// Goldilocks arithmetic and single-block BLAKE3 compressions.
+//
+// Field: p = 2^64 - 2^32 + 1 (crates/sezkp-ffts/src/lib.rs:229). Every value
+// leaving a helper is canonical (< p), which is what the reference hashes and
+// serialises (to_le_bytes of the canonical u64, lib.rs:123).
+//
+// BLAKE3: all hot-path messages fit one 64-byte block (8-byte field leaves,
+// 64-byte parent l||r, <= 44-byte labelled column leaves), so one compression
+// with flags CHUNK_START|CHUNK_END|ROOT, counter 0, cv = IV is the whole hash
+// (crates/sezkp-stark/src/v1/merkle.rs:58-61,132-160; fri_stream.rs:37-50).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sezkp {
+
+constexpr uint64_t GL_P = 0xffffffff00000001ULL;
+constexpr uint64_t GL_EPS = 0xffffffffULL;  // 2^64 mod p
+
+// ------------------------------------------------------------------ Goldilocks
+__device__ __forceinline__ uint64_t gl_add(uint64_t a, uint64_t b) {
+  uint64_t s = a + b;
+  // carry out of 2^64 -> add eps; then one conditional subtract of p.
+  uint64_t c = (s < a) ? GL_EPS : 0;
+  s += c;
+  return (s >= GL_P) ? s - GL_P : s;
+}
+__device__ __forceinline__ uint64_t gl_sub(uint64_t a, uint64_t b) {
+  uint64_t d = a - b;
+  return (a < b) ? d + GL_P : d;
+}
+// x = hi*2^64 + lo  ->  x mod p   (2^64 = eps, 2^96 = -1)
+__device__ __forceinline__ uint64_t gl_reduce128(uint64_t lo, uint64_t hi) {
+  uint64_t hi_hi = hi >> 32;
+  uint64_t hi_lo = hi & GL_EPS;
+  uint64_t t0 = lo - hi_hi;
+  if (lo < hi_hi) t0 -= GL_EPS;           // borrow: + p mod 2^64
+  uint64_t t1 = hi_lo * GL_EPS;           // < 2^64
+  uint64_t r = t0 + t1;
+  if (r < t1) r += GL_EPS;                // carry
+  return (r >= GL_P) ? r - GL_P : r;
+}
+__device__ __forceinline__ uint64_t gl_mul(uint64_t a, uint64_t b) {
+  return gl_reduce128(a * b, __umul64hi(a, b));
+}
+__device__ __forceinline__ uint64_t gl_sqr(uint64_t a) { return gl_mul(a, a); }
+__device__ __forceinline__ uint64_t gl_from_i64(int64_t x) {
+  return x >= 0 ? (uint64_t)x : GL_P - (uint64_t)(-x);   // |x| < 2^63 << p
+}
+// a^(p-2) via the 2^32-1 addition chain (72 mul/sqr)
+__device__ __forceinline__ uint64_t gl_pow2k(uint64_t x, int k) {
+  for (int i = 0; i < k; i++) x = gl_sqr(x);
+  return x;
+}
+// tK = a^(2^K - 1);  p-2 = (2^32-2)*2^32 + (2^32-1)
+__device__ inline uint64_t gl_inv(uint64_t a) {
+  uint64_t t2 = gl_mul(gl_sqr(a), a);
+  uint64_t t4 = gl_mul(gl_pow2k(t2, 2), t2);
+  uint64_t t8 = gl_mul(gl_pow2k(t4, 4), t4);
+  uint64_t t16 = gl_mul(gl_pow2k(t8, 8), t8);
+  uint64_t t24 = gl_mul(gl_pow2k(t16, 8), t8);
+  uint64_t t28 = gl_mul(gl_pow2k(t24, 4), t4);
+  uint64_t t30 = gl_mul(gl_pow2k(t28, 2), t2);
+  uint64_t t31 = gl_mul(gl_sqr(t30), a);
+  uint64_t t32 = gl_mul(gl_sqr(t31), a);
+  uint64_t hi = gl_pow2k(gl_sqr(t31), 32);        // a^((2^32-2) * 2^32)
+  return gl_mul(hi, t32);
+}
+
+// ------------------------------------------------------------------ BLAKE3
+#define B3_IV0 0x6A09E667u
+#define B3_IV1 0xBB67AE85u
+#define B3_IV2 0x3C6EF372u
+#define B3_IV3 0xA54FF53Au
+#define B3_IV4 0x510E527Fu
+#define B3_IV5 0x9B05688Cu
+#define B3_IV6 0x1F83D9ABu
+#define B3_IV7 0x5BE0CD19u
+#define B3_ROOT_FLAGS 11u  // CHUNK_START | CHUNK_END | ROOT
+
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+#define B3_G(a, b, c, d, x, y)          \
+  a = a + b + (x); d = rotr32(d ^ a, 16); \
+  c = c + d;       b = rotr32(b ^ c, 12); \
+  a = a + b + (y); d = rotr32(d ^ a, 8);  \
+  c = c + d;       b = rotr32(b ^ c, 7);
+#include "b3_schedule.inc"
+
+// One-block root hash: out = first 32 bytes of BLAKE3(message of block_len bytes).
+__device__ __forceinline__ void b3_hash_block(const uint32_t (&m)[16], uint32_t block_len, uint32_t (&out)[8]) {
+  uint32_t v0 = B3_IV0, v1 = B3_IV1, v2 = B3_IV2, v3 = B3_IV3, v4 = B3_IV4, v5 = B3_IV5, v6 = B3_IV6, v7 = B3_IV7;
+  uint32_t v8 = B3_IV0, v9 = B3_IV1, v10 = B3_IV2, v11 = B3_IV3, v12 = 0, v13 = 0, v14 = block_len, v15 = B3_ROOT_FLAGS;
+  B3_ROUNDS(m)
+  out[0] = v0 ^ v8; out[1] = v1 ^ v9; out[2] = v2 ^ v10; out[3] = v3 ^ v11;
+  out[4] = v4 ^ v12; out[5] = v5 ^ v13; out[6] = v6 ^ v14; out[7] = v7 ^ v15;
+}
+// leaf = BLAKE3(8 LE bytes of v)  (merkle.rs:150-160, fri_stream.rs:37-41)
+__device__ __forceinline__ void b3_leaf_u64(uint64_t v, uint32_t (&out)[8]) {
+  uint32_t m[16] = {(uint32_t)v, (uint32_t)(v >> 32), 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  b3_hash_block(m, 8, out);
+}
+// parent = BLAKE3(l || r), a plain 64-byte message (merkle.rs:58-61)
+__device__ __forceinline__ void b3_parent(const uint32_t (&l)[8], const uint32_t (&r)[8], uint32_t (&out)[8]) {
+  uint32_t m[16] = {l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]};
+  b3_hash_block(m, 64, out);
+}
+
+// ------------------------------------------------------------ node helpers
+__device__ __forceinline__ void node_load(const uint32_t* __restrict__ p, uint32_t (&h)[8]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  h[0] = a.x; h[1] = a.y; h[2] = a.z; h[3] = a.w; h[4] = b.x; h[5] = b.y; h[6] = b.z; h[7] = b.w;
+}
+__device__ __forceinline__ void node_store(uint32_t* __restrict__ p, const uint32_t (&h)[8]) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  q[1] = make_uint4(h[4], h[5], h[6], h[7]);
+}
+
+}  // namespace sezkp

@@ -1,0 +1,364 @@
+// merkle.hip — DEEP division, FRI fold, BLAKE3 Merkle layers and path
+// extraction for CDNA4 (gfx950).
+//
+// Reference semantics:
+//  * DEEP: out_i = y_i * (3*w_N^i - z)^-1          (crates/sezkp-stark/src/v1/lde.rs:76-93)
+//  * fold: y'_i = y_i + beta * y_{i+len/2}          (prover.rs:200-239)
+//  * leaves BLAKE3(8 LE bytes), parents BLAKE3(l||r), odd promotion never
+//    triggers because every FRI layer is a power of two (merkle.rs:46-71,150-160)
+//  * paths: siblings bottom->top (merkle.rs:80-108; equal to
+//    fri_stream.rs:357-409 on power-of-two layers)
+//
+// Layout: a workgroup of 256 lanes owns a 1024-leaf subtree. Each lane hashes 4
+// consecutive leaves and folds them to one level-2 node in registers (all 64
+// lanes busy), the remaining 8 levels reduce through an 8 KB struct-of-words
+// LDS image read with ds_read_b64 pairs (conflict-free). Levels >= lstore are
+// written to HBM for path extraction; lower levels are recomputed on demand.
+#include "dev_common.h"
+#include "sezkp_internal.h"
+
+namespace sezkp {
+
+constexpr int MK_THREADS = 256;
+
+__device__ __forceinline__ void store_level(const TreeDev& T, int l, uint64_t idx, const uint32_t (&h)[8]) {
+  if (l >= T.lstore && l <= T.logLen) node_store(T.nodes + 8 * (tree_level_off(T.logLen, T.lstore, l) + idx), h);
+  if (l == T.logLen) node_store(T.root, h);
+}
+
+// LDS image: words-major [8][256]; nodes 2i and 2i+1 of word w are one b64.
+__device__ __forceinline__ void lds_put(uint32_t (*lds)[MK_THREADS], int i, const uint32_t (&h)[8]) {
+#pragma unroll
+  for (int w = 0; w < 8; w++) lds[w][i] = h[w];
+}
+__device__ __forceinline__ void lds_pair(uint32_t (*lds)[MK_THREADS], int i, uint32_t (&l)[8], uint32_t (&r)[8]) {
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    uint2 p = *reinterpret_cast<const uint2*>(&lds[w][2 * i]);
+    l[w] = p.x;
+    r[w] = p.y;
+  }
+}
+
+// Reduce `cnt` level-`lvl` nodes in LDS to one; WG-local node i at level l has
+// global index wg * (cnt_at_l) + i.
+__device__ __forceinline__ void wg_reduce(uint32_t (*lds)[MK_THREADS], int cnt, int lvl, uint64_t wg, const TreeDev& T) {
+  const int tid = threadIdx.x;
+  while (cnt > 1) {
+    const int half = cnt >> 1;
+    uint32_t h[8];
+    const bool act = tid < half;
+    if (act) {
+      uint32_t l[8], r[8];
+      lds_pair(lds, tid, l, r);
+      b3_parent(l, r, h);
+    }
+    __syncthreads();
+    lvl++;
+    cnt = half;
+    if (act) {
+      lds_put(lds, tid, h);
+      store_level(T, lvl, wg * (uint64_t)cnt + tid, h);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- DEEP
+// 16 consecutive elements per lane, one Montgomery batch inversion per
+// workgroup (4096 elements): wave prefix/suffix product scans + one Fermat
+// inversion in lane 0 of wave 0.
+constexpr int DEEP_PER = 16;
+__global__ void __launch_bounds__(MK_THREADS) k_deep(uint64_t* __restrict__ y, int logN, uint64_t z, NttTables T) {
+  __shared__ uint64_t wtot[MK_THREADS / 64];
+  __shared__ uint64_t s_inv;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t i0 = ((uint64_t)blockIdx.x * MK_THREADS + tid) * DEEP_PER;
+  const uint64_t N = 1ULL << logN;
+  const bool act = i0 < N;
+  uint64_t d[DEEP_PER], a[DEEP_PER];
+  uint64_t P = 1;
+  if (act) {
+    // x_i = 3 * w_N^i ; first from the two-level table, then incremental
+    const uint64_t e = i0 << (T.K - logN);
+    uint64_t x = gl_mul(gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]), 3);
+    uint64_t wN;
+    {
+      const uint64_t e1 = 1ULL << (T.K - logN);
+      wN = gl_mul(T.hi[e1 >> T.S], T.lo[e1 & ((1ULL << T.S) - 1)]);
+    }
+#pragma unroll
+    for (int j = 0; j < DEEP_PER; j++) {
+      d[j] = gl_sub(x, z);
+      P = gl_mul(P, d[j]);
+      a[j] = P;
+      x = gl_mul(x, wN);
+    }
+  }
+  // wave inclusive prefix S and exclusive suffix Q of the lane products
+  uint64_t S = P, Tq = P;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t u = __shfl_up(S, o, 64);
+    if (lane >= o) S = gl_mul(S, u);
+    uint64_t v = __shfl_down(Tq, o, 64);
+    if (lane + o < 64) Tq = gl_mul(Tq, v);
+  }
+  uint64_t Q = __shfl_down(Tq, 1, 64);
+  if (lane == 63) Q = 1;
+  uint64_t Sprev = __shfl_up(S, 1, 64);
+  if (lane == 0) Sprev = 1;
+  if (lane == 63) wtot[wave] = S;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t t = 1;
+#pragma unroll
+    for (int w = 0; w < MK_THREADS / 64; w++) t = gl_mul(t, wtot[w]);
+    s_inv = gl_inv(t);
+  }
+  __syncthreads();
+  uint64_t invW = s_inv;  // inverse of this wave's total = inv(all) * prod(other waves)
+#pragma unroll
+  for (int w = 0; w < MK_THREADS / 64; w++)
+    if (w != wave) invW = gl_mul(invW, wtot[w]);
+  // inv(S_lane) = invW * Q ; inv(P_lane) = inv(S_lane) * S_{lane-1}
+  uint64_t inv_run = gl_mul(gl_mul(invW, Q), Sprev);
+  if (!act) return;
+#pragma unroll
+  for (int j = DEEP_PER - 1; j >= 0; j--) {
+    uint64_t inv_dj = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
+    inv_run = gl_mul(inv_run, d[j]);
+    y[i0 + j] = gl_mul(y[i0 + j], inv_dj);
+  }
+}
+
+// ------------------------------------------------------- leaf + subtree
+// fold == 0: leaves are in[i];  fold == 1: leaves y'_i = in[i] + beta*in[i+len],
+// written to out (the next FRI layer). One WG = 1024 leaves (or the whole layer).
+__global__ void __launch_bounds__(MK_THREADS) k_leaf_subtree(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                             int logLen, int fold, uint64_t beta, TreeDev T) {
+  __shared__ uint32_t lds[8][MK_THREADS];
+  const int tid = threadIdx.x;
+  const uint64_t len = 1ULL << logLen;
+  const uint64_t wg = blockIdx.x;
+  const int sub_log = logLen < 10 ? logLen : 10;
+  const int logper = logLen < 2 ? logLen : 2;
+  const int nact = 1 << (sub_log - logper);
+  const uint64_t base = wg << sub_log;
+  if (tid < nact) {
+    const uint64_t i0 = base + ((uint64_t)tid << logper);
+    uint64_t v[4] = {0, 0, 0, 0};
+    if (logper == 2) {
+      const ulonglong2* p = reinterpret_cast<const ulonglong2*>(in + i0);
+      ulonglong2 a0 = p[0], a1 = p[1];
+      v[0] = a0.x; v[1] = a0.y; v[2] = a1.x; v[3] = a1.y;
+      if (fold) {
+        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(in + i0 + len);
+        ulonglong2 b0 = q[0], b1 = q[1];
+        v[0] = gl_add(v[0], gl_mul(beta, b0.x));
+        v[1] = gl_add(v[1], gl_mul(beta, b0.y));
+        v[2] = gl_add(v[2], gl_mul(beta, b1.x));
+        v[3] = gl_add(v[3], gl_mul(beta, b1.y));
+        ulonglong2* o = reinterpret_cast<ulonglong2*>(out + i0);
+        o[0] = make_ulonglong2(v[0], v[1]);
+        o[1] = make_ulonglong2(v[2], v[3]);
+      }
+    } else {
+      for (int j = 0; j < (1 << logper); j++) {
+        v[j] = in[i0 + j];
+        if (fold) {
+          v[j] = gl_add(v[j], gl_mul(beta, in[i0 + j + len]));
+          out[i0 + j] = v[j];
+        }
+      }
+    }
+    uint32_t h[8];
+    if (logper == 2) {
+      uint32_t l0[8], l1[8], p0[8], p1[8];
+      b3_leaf_u64(v[0], l0);
+      b3_leaf_u64(v[1], l1);
+      if (T.lstore == 0) { store_level(T, 0, i0, l0); store_level(T, 0, i0 + 1, l1); }
+      b3_parent(l0, l1, p0);
+      b3_leaf_u64(v[2], l0);
+      b3_leaf_u64(v[3], l1);
+      if (T.lstore == 0) { store_level(T, 0, i0 + 2, l0); store_level(T, 0, i0 + 3, l1); }
+      b3_parent(l0, l1, p1);
+      if (T.lstore <= 1) { store_level(T, 1, i0 >> 1, p0); store_level(T, 1, (i0 >> 1) + 1, p1); }
+      b3_parent(p0, p1, h);
+      store_level(T, 2, i0 >> 2, h);
+    } else if (logper == 1) {
+      uint32_t l0[8], l1[8];
+      b3_leaf_u64(v[0], l0);
+      b3_leaf_u64(v[1], l1);
+      if (T.lstore == 0) { store_level(T, 0, i0, l0); store_level(T, 0, i0 + 1, l1); }
+      b3_parent(l0, l1, h);
+      store_level(T, 1, i0 >> 1, h);
+    } else {
+      b3_leaf_u64(v[0], h);
+      store_level(T, 0, i0, h);
+    }
+    lds_put(lds, tid, h);
+  }
+  __syncthreads();
+  wg_reduce(lds, nact, logper, wg, T);
+}
+
+// ------------------------------------------------------------ upper levels
+// Input: stored level `from` (count 2^(logLen-from)); one WG reduces up to
+// 1024 nodes (4 per lane, 2 levels in registers) and stores every level.
+// grid.y indexes trees of identical shape spaced tree_stride nodes apart.
+__global__ void __launch_bounds__(MK_THREADS) k_tree_upper(TreeDev T0, uint64_t tree_stride, uint64_t root_stride,
+                                                           int from) {
+  __shared__ uint32_t lds[8][MK_THREADS];
+  TreeDev T = T0;
+  T.nodes += 8 * tree_stride * blockIdx.y;
+  T.root += root_stride * blockIdx.y;
+  const int tid = threadIdx.x;
+  const uint64_t wg = blockIdx.x;
+  const int cnt_log = T.logLen - from;
+  const int sub_log = cnt_log < 10 ? cnt_log : 10;
+  const int logper = cnt_log < 2 ? cnt_log : 2;
+  const int nact = 1 << (sub_log - logper);
+  const uint32_t* src = T.nodes + 8 * tree_level_off(T.logLen, T.lstore, from);
+  if (tid < nact) {
+    const uint64_t g = (wg << (sub_log - logper)) + tid;  // node index at level from+logper
+    uint32_t h[8];
+    if (logper == 2) {
+      uint32_t a[8], b[8], p0[8], p1[8];
+      node_load(src + 8 * (4 * g + 0), a);
+      node_load(src + 8 * (4 * g + 1), b);
+      b3_parent(a, b, p0);
+      node_load(src + 8 * (4 * g + 2), a);
+      node_load(src + 8 * (4 * g + 3), b);
+      b3_parent(a, b, p1);
+      store_level(T, from + 1, 2 * g, p0);
+      store_level(T, from + 1, 2 * g + 1, p1);
+      b3_parent(p0, p1, h);
+      store_level(T, from + 2, g, h);
+    } else if (logper == 1) {
+      uint32_t a[8], b[8];
+      node_load(src + 8 * (2 * g), a);
+      node_load(src + 8 * (2 * g + 1), b);
+      b3_parent(a, b, h);
+      store_level(T, from + 1, g, h);
+    } else {
+      node_load(src + 8 * g, h);
+      if (from == T.logLen) node_store(T.root, h);
+    }
+    lds_put(lds, tid, h);
+  }
+  __syncthreads();
+  wg_reduce(lds, nact, from + logper, wg, T);
+}
+
+// ---------------------------------------------------------- path extraction
+// One 64-lane workgroup per (layer, index): recompute the 64-leaf group that
+// holds the index (levels < lstore), then read stored siblings above.
+__global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict__ layers, const uint32_t* __restrict__ req,
+                                                  uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[8][64];
+  const int lane = threadIdx.x;
+  const uint32_t q = blockIdx.x;
+  const uint32_t r = req[2 * q];
+  const uint64_t idx = req[2 * q + 1];
+  const FriLayerDev Ly = layers[r];
+  const TreeDev& T = Ly.tree;
+  const int L = T.logLen;
+  const int glog = L < T.lstore ? L : T.lstore;
+  const uint64_t g = 1ULL << glog;
+  const uint64_t base = idx & ~(g - 1);
+  uint32_t* o = out + (uint64_t)q * PATH_REC_WORDS;
+  if (lane == 0) {
+    uint64_t v = Ly.vals[idx];
+    o[0] = (uint32_t)v;
+    o[1] = (uint32_t)(v >> 32);
+    o[2] = 0;
+    o[3] = 0;
+  }
+  if (lane < (int)g) {
+    uint32_t h[8];
+    b3_leaf_u64(Ly.vals[base + lane], h);
+    for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
+  }
+  __syncthreads();
+  int cnt = (int)g;
+  for (int lvl = 0; lvl < glog; lvl++) {
+    const int sib = (int)(((idx - base) >> lvl) ^ 1);
+    if (lane < 8) o[4 + 8 * lvl + lane] = lds[lane][sib];
+    const int half = cnt >> 1;
+    uint32_t h[8];
+    if (lane < half) {
+      uint32_t a[8], b[8];
+      for (int w = 0; w < 8; w++) { a[w] = lds[w][2 * lane]; b[w] = lds[w][2 * lane + 1]; }
+      b3_parent(a, b, h);
+    }
+    __syncthreads();
+    if (lane < half)
+      for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
+    __syncthreads();
+    cnt = half;
+  }
+  for (int lvl = glog; lvl < L; lvl++) {
+    const uint64_t sib = (idx >> lvl) ^ 1;
+    if (lane < 8) o[4 + 8 * lvl + lane] = T.nodes[8 * (tree_level_off(L, T.lstore, lvl) + sib) + lane];
+  }
+}
+
+// ------------------------------------------------------------------ host
+hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw) {
+  const uint64_t N = 1ULL << logN;
+  const uint64_t per_wg = (uint64_t)MK_THREADS * DEEP_PER;
+  const unsigned grid = (unsigned)((N + per_wg - 1) / per_wg);
+  hipLaunchKernelGGL(k_deep, dim3(grid), dim3(MK_THREADS), 0, st, y, logN, z, tw);
+  return hipGetLastError();
+}
+
+hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold,
+                               uint64_t beta, TreeDev tree) {
+  const int sub_log = logLen < 10 ? logLen : 10;
+  const unsigned grid = (unsigned)(1ULL << (logLen - sub_log));
+  hipLaunchKernelGGL(k_leaf_subtree, dim3(grid), dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, tree);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  int from = sub_log;
+  while (from < logLen) {
+    const int cnt_log = logLen - from;
+    const int step = cnt_log < 10 ? cnt_log : 10;
+    hipLaunchKernelGGL(k_tree_upper, dim3((unsigned)(1ULL << (cnt_log - step)), 1), dim3(MK_THREADS), 0, st, tree,
+                       (uint64_t)0, (uint64_t)0, from);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    from += step;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_tree_upper(hipStream_t st, TreeDev* trees, int ntrees, uint64_t tree_stride_nodes,
+                             uint64_t root_stride_words, int from_level) {
+  const TreeDev T = trees[0];
+  int from = from_level;
+  if (from == T.logLen) {  // single node: it is the root
+    hipLaunchKernelGGL(k_tree_upper, dim3(1, ntrees), dim3(MK_THREADS), 0, st, T, tree_stride_nodes,
+                       root_stride_words, from);
+    return hipGetLastError();
+  }
+  while (from < T.logLen) {
+    const int cnt_log = T.logLen - from;
+    const int step = cnt_log < 10 ? cnt_log : 10;
+    hipLaunchKernelGGL(k_tree_upper, dim3((unsigned)(1ULL << (cnt_log - step)), ntrees), dim3(MK_THREADS), 0, st, T,
+                       tree_stride_nodes, root_stride_words, from);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    from += step;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
+                            uint32_t* d_out) {
+  if (nreq == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fri_paths, dim3(nreq), dim3(64), 0, st, d_layers, d_req, d_out);
+  return hipGetLastError();
+}
+
+}  // namespace sezkp

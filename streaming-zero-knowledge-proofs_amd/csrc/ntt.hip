@@ -1,0 +1,226 @@
+// ntt.hip — Goldilocks NTT passes for CDNA4 (gfx950).
+//
+// Mathematically the reference's transforms (crates/sezkp-ffts/src/ntt.rs:79-155):
+// forward y_k = sum_j a_j w_N^{jk}, inverse = (1/n) sum_k y_k w_N^{-jk}, with
+// w_{2^s} = 7^((p-1)>>s) (lib.rs:237-242). Field arithmetic is exact, so any
+// factorisation produces the reference's bits.
+//
+// Structure: a transform of 2^logN points is a sequence of LDS passes. A pass
+// owns m consecutive radix-2 stages whose smallest half-size is L = 2^sL; it
+// treats every group {base + low + t*L : t < 2^m} (low < L) as one 2^m-point
+// sub-transform done in LDS with internal twiddles w_{2^m}, plus ONE element-
+// wise twiddle w_{2^m L}^{low * bitrev_m(t)} (post-multiply for DIF, pre-
+// multiply for DIT; the four-step identity). Tiles are C <= 16 groups with
+// consecutive `low` (128-B row segments) or, when L < C, one contiguous run.
+//   DIF: natural -> bit-reversed order.   DIT: bit-reversed -> natural order.
+// Twiddles: w_{2^K}^e = tw_hi[e >> S] * tw_lo[e & (2^S-1)] (two small tables,
+// L2-resident), inverse uses e -> 2^K - e.
+#include "dev_common.h"
+#include "sezkp_internal.h"
+
+namespace sezkp {
+
+constexpr int NTT_THREADS = 256;
+constexpr int NTT_CMAX = 16;
+constexpr int NTT_PADC = NTT_CMAX + 1;   // LDS row stride (u64) -> conflict-free b64 access
+constexpr int NTT_MMAX = 8;              // <= 256 rows per tile
+
+__device__ __forceinline__ uint64_t tw_pow(const NttTables& T, uint64_t e, bool inverse) {
+  uint64_t mask = (T.K >= 64) ? ~0ULL : ((1ULL << T.K) - 1);
+  if (inverse) e = (0 - e) & mask;
+  return gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]);
+}
+__device__ __forceinline__ uint64_t pow3(const NttTables& T, uint64_t e) {
+  return gl_mul(T.p3_hi[e >> T.S], T.p3_lo[e & ((1ULL << T.S) - 1)]);
+}
+
+template <bool DIF>
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(NttPassArgs P) {
+  __shared__ uint64_t sh[(1 << NTT_MMAX) * NTT_PADC];
+  __shared__ uint64_t W[(1 << NTT_MMAX) / 2];
+  const int m = P.m, R = 1 << m, sL = P.sL;
+  const uint64_t L = 1ULL << sL;
+  const int logC = P.logC, C = 1 << logC;
+  const int tid = threadIdx.x;
+  const uint64_t tile = blockIdx.x;
+  const NttTables& T = P.tw;
+
+  for (int x = tid; x < R / 2; x += NTT_THREADS) W[x] = tw_pow(T, (uint64_t)x << (T.K - m), P.inverse);
+
+  const int nel = R << logC;
+  const bool wide = L >= (uint64_t)C;  // tile = C consecutive `low` columns
+  uint64_t blk_base = 0, low0 = 0;
+  if (wide) {
+    uint64_t tiles_per_blk = L >> logC;
+    blk_base = (tile / tiles_per_blk) * ((uint64_t)R << sL);
+    low0 = (tile % tiles_per_blk) << logC;
+  }
+  const int tw_shift = T.K - m - sL;  // exponent scale into w_{2^K}
+  // ---- load (+ DIT pre-twiddle)
+  for (int q = tid; q < nel; q += NTT_THREADS) {
+    int t, c;
+    uint64_t low, pos;
+    if (wide) {
+      t = q >> logC; c = q & (C - 1); low = low0 + c;
+      pos = blk_base + low + ((uint64_t)t << sL);
+    } else {
+      low = q & (L - 1);
+      t = (q >> sL) & (R - 1);
+      c = ((q >> (sL + m)) << sL) | (int)low;
+      pos = tile * (uint64_t)nel + q;
+    }
+    uint64_t v;
+    if (P.src) {  // LDE replicated load: B[8k+s] = A[k] * n^-1 * 3^bitrev(k)
+      uint64_t k = pos >> 3;
+      uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;
+      v = gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk));
+    } else {
+      v = P.a[pos];
+    }
+    if (!DIF && low != 0) {
+      uint32_t bt = __brev((uint32_t)t) >> (32 - m);
+      v = gl_mul(v, tw_pow(T, (low * bt) << tw_shift, P.inverse));
+    }
+    sh[t * NTT_PADC + c] = v;
+  }
+  __syncthreads();
+  // ---- internal radix-2 stages over t
+  const int nbf = (R / 2) << logC;
+  for (int it = 0; it < m - P.skip; it++) {
+    const int s = DIF ? (m - 1 - it) : (it + P.skip);
+    const int h = 1 << s;
+    for (int b = tid; b < nbf; b += NTT_THREADS) {
+      const int c = b & (C - 1), u = b >> logC;
+      const int j = u & (h - 1);
+      const int t0 = ((u >> s) << (s + 1)) | j, t1 = t0 + h;
+      const uint64_t w = W[j << (m - 1 - s)];
+      uint64_t x = sh[t0 * NTT_PADC + c], y = sh[t1 * NTT_PADC + c];
+      if (DIF) {
+        sh[t0 * NTT_PADC + c] = gl_add(x, y);
+        sh[t1 * NTT_PADC + c] = gl_mul(gl_sub(x, y), w);
+      } else {
+        y = gl_mul(y, w);
+        sh[t0 * NTT_PADC + c] = gl_add(x, y);
+        sh[t1 * NTT_PADC + c] = gl_sub(x, y);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- (DIF post-twiddle +) store
+  for (int q = tid; q < nel; q += NTT_THREADS) {
+    int t, c;
+    uint64_t low, pos;
+    if (wide) {
+      t = q >> logC; c = q & (C - 1); low = low0 + c;
+      pos = blk_base + low + ((uint64_t)t << sL);
+    } else {
+      low = q & (L - 1);
+      t = (q >> sL) & (R - 1);
+      c = ((q >> (sL + m)) << sL) | (int)low;
+      pos = tile * (uint64_t)nel + q;
+    }
+    uint64_t v = sh[t * NTT_PADC + c];
+    if (DIF && low != 0) {
+      uint32_t bt = __brev((uint32_t)t) >> (32 - m);
+      v = gl_mul(v, tw_pow(T, (low * bt) << tw_shift, P.inverse));
+    }
+    P.a[pos] = v;
+  }
+}
+
+// Out-of-place bit-reversal permutation (optionally scaled), tiled so both the
+// read and the write are 16-element (128-B) row segments:
+// p = x*2^(a+b) + y*2^a + z  ->  rev(z)*2^(a+b) + rev(y)*2^a + rev(x), a = 4.
+__global__ void __launch_bounds__(256) k_bitrev_permute(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                         int logN, uint64_t scale, int do_scale) {
+  __shared__ uint64_t sh[16 * 17];
+  const int a = 4, b = logN - 2 * a;
+  const uint32_t y = blockIdx.x;   // middle bits
+  const int tid = threadIdx.x;
+  const int x = tid >> 4, z = tid & 15;
+  uint32_t ry = b ? (__brev(y) >> (32 - b)) : 0;
+  uint64_t src = ((uint64_t)x << (a + b)) | ((uint64_t)y << a) | z;
+  uint64_t v = in[src];
+  if (do_scale) v = gl_mul(v, scale);
+  sh[x * 17 + z] = v;
+  __syncthreads();
+  // thread (x', z') writes out[rev(z')... ] : destination row = rev(z), column = rev(x)
+  const int rz = tid >> 4, rx = tid & 15;        // destination coordinates (already reversed)
+  const int zz = __brev((uint32_t)rz) >> 28, xx = __brev((uint32_t)rx) >> 28;
+  uint64_t dst = ((uint64_t)rz << (a + b)) | ((uint64_t)ry << a) | rx;
+  out[dst] = sh[xx * 17 + zz];
+}
+
+// Small transforms (logN < 8) fall back to a plain in-LDS pass per call.
+__global__ void k_bitrev_permute_small(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int logN,
+                                       uint64_t scale, int do_scale) {
+  uint64_t N = 1ULL << logN;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t r = logN ? (__brev((uint32_t)i) >> (32 - logN)) : 0;
+    uint64_t v = in[i];
+    out[r] = do_scale ? gl_mul(v, scale) : v;
+  }
+}
+
+// ------------------------------------------------------------------ host side
+static void plan_passes(int logN, int first_min, int* ms, int* np) {
+  int passes = (logN + NTT_MMAX - 1) / NTT_MMAX;
+  if (passes < 1) passes = 1;
+  int base = logN / passes, rem = logN % passes;
+  for (int i = 0; i < passes; i++) ms[i] = base + (i < rem ? 1 : 0);
+  (void)first_min;
+  *np = passes;
+}
+
+hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T) {
+  if (logN == 0) return hipSuccess;
+  int ms[8], np;
+  plan_passes(logN, 1, ms, &np);
+  int sL = logN;
+  for (int i = 0; i < np; i++) {
+    NttPassArgs P{};
+    P.a = a; P.src = nullptr; P.tw = T; P.m = ms[i]; sL -= ms[i]; P.sL = sL;
+    P.inverse = inverse ? 1 : 0; P.skip = 0;
+    int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
+    uint64_t tiles = (1ULL << logN) >> (P.m + logC);
+    hipLaunchKernelGGL(k_ntt_pass<true>, dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
+  }
+  return hipGetLastError();
+}
+
+// DIT from bit-reversed input. If src != nullptr, the first pass loads the
+// replicated, scaled coefficients (LDE) and skips the 3 stages replication
+// makes trivial (blowup 8).
+hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
+                   const uint64_t* src, int log_src, uint64_t inv_n) {
+  if (logN == 0) return hipSuccess;
+  int ms[8], np;
+  plan_passes(logN, src ? 3 : 1, ms, &np);
+  // DIT order: smallest strides first; ensure the first pass holds >= 3 stages for the LDE skip
+  if (src && ms[0] < 3) return hipErrorInvalidValue;
+  int sL = 0;
+  for (int i = 0; i < np; i++) {
+    NttPassArgs P{};
+    P.a = a; P.tw = T; P.m = ms[i]; P.sL = sL; P.inverse = inverse ? 1 : 0;
+    P.src = (i == 0) ? src : nullptr;
+    P.log_src = log_src; P.inv_n = inv_n;
+    P.skip = (i == 0 && src) ? (logN - log_src) : 0;
+    int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
+    uint64_t tiles = (1ULL << logN) >> (P.m + logC);
+    hipLaunchKernelGGL(k_ntt_pass<false>, dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
+    sL += ms[i];
+  }
+  return hipGetLastError();
+}
+
+hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale, bool do_scale) {
+  if (logN >= 8) {
+    hipLaunchKernelGGL(k_bitrev_permute, dim3(1u << (logN - 8)), dim3(256), 0, st, in, out, logN, scale,
+                       do_scale ? 1 : 0);
+  } else {
+    hipLaunchKernelGGL(k_bitrev_permute_small, dim3(1), dim3(256), 0, st, in, out, logN, scale, do_scale ? 1 : 0);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace sezkp

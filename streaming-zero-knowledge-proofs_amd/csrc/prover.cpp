@@ -1,0 +1,763 @@
+// prover.cpp — host orchestration of the MI355X STARK v1 prover and the C ABI
+// (include/sezkp_stark.h). Restates the schedule of
+// crates/sezkp-stark/src/v1/prover.rs:61-462 in compute-once form: every hot
+// loop runs as a HIP kernel on the context's stream; the host keeps the
+// Fiat-Shamir transcript and assembles the bincode ProofV1 (proof.rs:80-98).
+//
+// Host<->device synchronisation points (each a few hundred bytes):
+//   col roots -> [alphas, masks, z] -> layer-0 root -> [betas] -> FRI roots ->
+//   [query indices] -> paths/openings.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/sezkp_stark.h"
+#include "codec.h"
+#include "host_crypto.h"
+#include "sezkp_internal.h"
+
+using namespace sezkp;
+
+namespace {
+
+constexpr int NUM_QUERIES = 30;  // params.rs:31
+constexpr int BLOWUP_LOG2 = 3;   // params.rs:28
+enum Stage { ST_EXPAND, ST_COMMIT, ST_OUTER, ST_COMPOSE, ST_INTT, ST_LDE, ST_DEEP, ST_L0TREE, ST_FRI, ST_PATHS,
+             ST_OPEN, ST_NSTAGE };
+
+struct Err {
+  int32_t code;
+  std::string msg;
+};
+#define HIP_OR_THROW(x)                                                                               \
+  do {                                                                                                \
+    hipError_t e_ = (x);                                                                              \
+    if (e_ != hipSuccess) throw Err{SEZKP_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+void set_err(char* err, size_t len, const std::string& m) {
+  if (err && len) {
+    snprintf(err, len, "%s", m.c_str());
+  }
+}
+
+// --------------------------------------------------------------- twiddles
+// w_{2^32}^e = hi[e>>16] * lo[e&0xffff]  and 3^e likewise (host-built once per device)
+struct DevTables {
+  uint64_t* d = nullptr;
+  NttTables T{};
+};
+std::mutex g_tab_mu;
+std::map<int, DevTables> g_tabs;
+
+const NttTables& tables_for_device(int dev) {
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  auto it = g_tabs.find(dev);
+  if (it != g_tabs.end()) return it->second.T;
+  const int K = 32, S = 16;
+  const size_t nl = 1u << S, nh = 1u << (K - S);
+  std::vector<uint64_t> h(2 * (nl + nh));
+  uint64_t* lo = h.data();
+  uint64_t* hi = lo + nl;
+  uint64_t* p3lo = hi + nh;
+  uint64_t* p3hi = p3lo + nl;
+  const uint64_t w = hgl_root_2exp(K);
+  const uint64_t wS = hgl_pow(w, nl);
+  const uint64_t t3S = hgl_pow(3, nl);
+  uint64_t a = 1, b = 1, c = 1, d = 1;
+  for (size_t i = 0; i < nl; i++) { lo[i] = a; a = hgl_mul(a, w); p3lo[i] = c; c = hgl_mul(c, 3); }
+  for (size_t i = 0; i < nh; i++) { hi[i] = b; b = hgl_mul(b, wS); p3hi[i] = d; d = hgl_mul(d, t3S); }
+  DevTables t;
+  HIP_OR_THROW(hipSetDevice(dev));
+  HIP_OR_THROW(hipMalloc(&t.d, h.size() * 8));
+  HIP_OR_THROW(hipMemcpy(t.d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  t.T.lo = t.d;
+  t.T.hi = t.d + nl;
+  t.T.p3_lo = t.d + nl + nh;
+  t.T.p3_hi = t.d + 2 * nl + nh;
+  t.T.K = K;
+  t.T.S = S;
+  return g_tabs.emplace(dev, t).first->second.T;
+}
+
+const char* KIND_NAME[7] = {"mv", "wflag", "wsym", "head", "winlen", "in_off", "out_off"};
+
+std::string label_of(int c, uint32_t tau) {  // all_labels (openings.rs:89-116)
+  if (c == 0) return "input_mv";
+  if (c == 1) return "is_first";
+  if (c == 2) return "is_last";
+  return std::string(KIND_NAME[(c - 3) / tau]) + "_" + std::to_string((c - 3) % tau);
+}
+
+ColTemplate make_template(int c, uint32_t tau, const std::string& label) {
+  ColTemplate t{};
+  uint8_t b[64] = {0};
+  memcpy(b, "col_leaf", 8);
+  const uint32_t L = (uint32_t)label.size();
+  for (int i = 0; i < 4; i++) b[8 + i] = (uint8_t)(L >> (8 * i));
+  memcpy(b + 12, label.data(), L);
+  for (int i = 0; i < 16; i++)
+    t.words[i] = (uint32_t)b[4 * i] | (uint32_t)b[4 * i + 1] << 8 | (uint32_t)b[4 * i + 2] << 16 |
+                 (uint32_t)b[4 * i + 3] << 24;
+  t.off = 12 + L;
+  t.block_len = 20 + L;
+  if (c < 3) { t.kind = c; t.tape = 0; }
+  else { t.kind = 3 + (c - 3) / tau; t.tape = (c - 3) % tau; }
+  return t;
+}
+
+uint64_t rd64(const uint8_t* p) {
+  uint64_t x = 0;
+  for (int i = 7; i >= 0; i--) x = (x << 8) | p[i];
+  return x;
+}
+int ilog2(uint64_t x) {
+  int l = 0;
+  while ((1ULL << l) < x) l++;
+  return l;
+}
+
+}  // namespace
+
+// ======================================================================== ctx
+struct sezkp_ctx {
+  int device = 0;
+  hipStream_t st = nullptr;
+  NttTables tw{};
+  std::vector<void*> dev_allocs;
+  std::vector<void*> host_allocs;
+  // shape
+  bool loaded = false;
+  uint64_t n = 0, N = 0;
+  int logn = 0, logN = 0, ncols = 0, logChunks = 0;
+  uint32_t tau = 0, nblk = 0;
+  TraceDev T{};
+  std::vector<std::string> labels;
+  ColTemplate* d_tmpl = nullptr;
+  uint32_t* d_outer = nullptr;
+  uint64_t outer_stride = 0;
+  uint32_t* d_colroots = nullptr;
+  uint64_t* d_base = nullptr;
+  uint64_t* d_lde = nullptr;
+  uint64_t* d_fri = nullptr;
+  std::vector<TreeDev> trees;
+  uint32_t* d_roots = nullptr;
+  FriLayerDev* d_layers = nullptr;
+  uint32_t* d_req = nullptr;
+  uint32_t* d_fri_out = nullptr;
+  uint32_t* d_open_out = nullptr;
+  uint32_t* h_req = nullptr;
+  uint32_t* h_fri_out = nullptr;
+  uint32_t* h_open_out = nullptr;
+  uint32_t* h_small = nullptr;  // col roots / fri roots staging
+  size_t max_fri_req = 0, max_open_req = 0;
+  hipEvent_t ev[ST_NSTAGE + 1]{};
+  double stage_ms[ST_NSTAGE + 1]{};
+  bool have_times = false;
+
+  template <class Tp>
+  Tp* dalloc(size_t count) {
+    void* p = nullptr;
+    HIP_OR_THROW(hipMalloc(&p, count * sizeof(Tp) + 64));
+    dev_allocs.push_back(p);
+    return static_cast<Tp*>(p);
+  }
+  template <class Tp>
+  Tp* halloc(size_t count) {
+    void* p = nullptr;
+    HIP_OR_THROW(hipHostMalloc(&p, count * sizeof(Tp) + 64, hipHostMallocDefault));
+    host_allocs.push_back(p);
+    return static_cast<Tp*>(p);
+  }
+  void free_all() {
+    for (void* p : dev_allocs) (void)hipFree(p);
+    for (void* p : host_allocs) (void)hipHostFree(p);
+    dev_allocs.clear();
+    host_allocs.clear();
+    loaded = false;
+  }
+  ~sezkp_ctx() {
+    if (st) (void)hipStreamSynchronize(st);
+    free_all();
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (st) (void)hipStreamDestroy(st);
+  }
+
+  void upload(const sezkp_block_view& v);
+  std::vector<uint8_t> prove(const uint8_t root[32]);
+};
+
+void sezkp_ctx::upload(const sezkp_block_view& v) {
+  HIP_OR_THROW(hipSetDevice(device));
+  HIP_OR_THROW(hipStreamSynchronize(st));
+  free_all();
+  tau = v.tau;
+  nblk = v.n_blocks;
+  // rows: sum over blocks of (step_hi - step_lo + 1) (columns.rs:254-257)
+  uint64_t rows = 0;
+  for (uint32_t k = 0; k < nblk; k++) {
+    const uint64_t len = v.step_hi[k] - v.step_lo[k] + 1;
+    const uint64_t steps = v.step_start[k + 1] - v.step_start[k];
+    if (len != steps)
+      throw Err{SEZKP_E_INVALID, "block " + std::to_string(k) + ": step_hi-step_lo+1=" + std::to_string(len) +
+                                     " but movement_log has " + std::to_string(steps) + " steps"};
+    rows += len;
+  }
+  if (rows == 0 || (rows & (rows - 1)) != 0)
+    throw Err{SEZKP_E_INVALID, "n_base must be a power of two (got " + std::to_string(rows) + ")"};  // lde.rs:51
+  if (rows > (1ULL << 28)) throw Err{SEZKP_E_INVALID, "trace too long for one device (n > 2^28)"};
+  n = rows;
+  logn = ilog2(n);
+  logN = logn + BLOWUP_LOG2;
+  N = 1ULL << logN;
+  ncols = 3 + 7 * (int)tau;
+  logChunks = logn > COL_CHUNK_LOG2 ? logn - COL_CHUNK_LOG2 : 0;
+
+  // ---- trace image (tape-major)
+  std::vector<int8_t> mv((size_t)tau * n);
+  std::vector<uint8_t> wf((size_t)tau * n);
+  std::vector<uint16_t> ws((size_t)tau * n);
+  for (uint64_t s = 0; s < n; s++)
+    for (uint32_t r = 0; r < tau; r++) {
+      const size_t i = (size_t)s * tau + r, o = (size_t)r * n + s;
+      mv[o] = v.mv[i];
+      wf[o] = v.has_write[i] ? 1 : 0;
+      ws[o] = v.has_write[i] ? v.wsym[i] : 0;
+    }
+  std::vector<uint64_t> bw((size_t)tau * nblk), bi((size_t)tau * nblk), bo((size_t)tau * nblk);
+  for (uint32_t k = 0; k < nblk; k++)
+    for (uint32_t r = 0; r < tau; r++) {
+      const size_t i = (size_t)k * tau + r, o = (size_t)r * nblk + k;
+      const int64_t d = v.win_right[i] - v.win_left[i];
+      const uint64_t wl = (d < 0 ? 0 - (uint64_t)d : (uint64_t)d) + 1;  // openings.rs:217
+      bw[o] = wl % GL_P_HOST;
+      bi[o] = v.off_in[i];
+      bo[o] = v.off_out[i];
+    }
+  auto up = [&](auto* dst, const auto* src, size_t count) {
+    if (count) HIP_OR_THROW(hipMemcpy(dst, src, count * sizeof(*src), hipMemcpyHostToDevice));
+  };
+  int8_t* d_imv = dalloc<int8_t>(n);
+  int8_t* d_mv = dalloc<int8_t>((size_t)tau * n);
+  uint8_t* d_wf = dalloc<uint8_t>((size_t)tau * n);
+  uint16_t* d_ws = dalloc<uint16_t>((size_t)tau * n);
+  uint64_t* d_bs = dalloc<uint64_t>(nblk + 1);
+  uint64_t* d_bw = dalloc<uint64_t>((size_t)tau * nblk);
+  uint64_t* d_bi = dalloc<uint64_t>((size_t)tau * nblk);
+  uint64_t* d_bo = dalloc<uint64_t>((size_t)tau * nblk);
+  up(d_imv, v.input_mv, n);
+  up(d_mv, mv.data(), mv.size());
+  up(d_wf, wf.data(), wf.size());
+  up(d_ws, ws.data(), ws.size());
+  up(d_bs, v.step_start, nblk + 1);
+  up(d_bw, bw.data(), bw.size());
+  up(d_bi, bi.data(), bi.size());
+  up(d_bo, bo.data(), bo.size());
+  T.n = n;
+  T.tau = (int)tau;
+  T.nblk = nblk;
+  T.input_mv = d_imv;
+  T.mv = d_mv;
+  T.wflag = d_wf;
+  T.wsym = d_ws;
+  T.blk_start = d_bs;
+  T.blk_winlen = d_bw;
+  T.blk_offin = d_bi;
+  T.blk_offout = d_bo;
+  T.row_blk = dalloc<uint32_t>(n);
+  T.row_flags = dalloc<uint8_t>(n);
+  T.head = dalloc<int64_t>((size_t)tau * n + 1);
+
+  // ---- column templates + outer trees (all levels kept)
+  labels.clear();
+  std::vector<ColTemplate> tm;
+  for (int c = 0; c < ncols; c++) {
+    labels.push_back(label_of(c, tau));
+    if (labels.back().size() > 44) throw Err{SEZKP_E_INVALID, "column label too long"};
+    tm.push_back(make_template(c, tau, labels.back()));
+  }
+  d_tmpl = dalloc<ColTemplate>(ncols);
+  up(d_tmpl, tm.data(), tm.size());
+  outer_stride = tree_stored_nodes(logChunks, 0);
+  d_outer = dalloc<uint32_t>((size_t)ncols * outer_stride * 8);
+  d_colroots = dalloc<uint32_t>((size_t)ncols * 8);
+
+  // ---- LDE / FRI workspace
+  d_base = dalloc<uint64_t>(n);
+  d_lde = dalloc<uint64_t>(N);
+  d_fri = dalloc<uint64_t>(N);
+  const int k = logN;
+  trees.assign(k + 1, TreeDev{});
+  uint64_t total_nodes = 0;
+  for (int r = 0; r <= k; r++) total_nodes += tree_stored_nodes(k - r, LSTORE_FRI);
+  uint32_t* d_nodes = dalloc<uint32_t>(total_nodes * 8 + 8);
+  d_roots = dalloc<uint32_t>((size_t)(k + 1) * 8);
+  std::vector<FriLayerDev> ly(k + 1);
+  uint64_t off = 0;
+  for (int r = 0; r <= k; r++) {
+    trees[r].nodes = d_nodes + off * 8;
+    trees[r].root = d_roots + 8 * r;
+    trees[r].logLen = k - r;
+    trees[r].lstore = LSTORE_FRI;
+    off += tree_stored_nodes(k - r, LSTORE_FRI);
+    ly[r].vals = r == 0 ? d_lde : d_fri + (N - (N >> (r - 1)));
+    ly[r].tree = trees[r];
+  }
+  d_layers = dalloc<FriLayerDev>(k + 1);
+  up(d_layers, ly.data(), ly.size());
+  max_fri_req = (size_t)NUM_QUERIES * 2 * k;
+  max_open_req = (size_t)NUM_QUERIES * (3 + 9 * tau);
+  d_req = dalloc<uint32_t>(max_fri_req * 2 + max_open_req * 3);
+  d_fri_out = dalloc<uint32_t>(max_fri_req * PATH_REC_WORDS);
+  d_open_out = dalloc<uint32_t>(max_open_req * OPEN_REC_WORDS);
+  h_req = halloc<uint32_t>(max_fri_req * 2 + max_open_req * 3);
+  h_fri_out = halloc<uint32_t>(max_fri_req * PATH_REC_WORDS);
+  h_open_out = halloc<uint32_t>(max_open_req * OPEN_REC_WORDS);
+  h_small = halloc<uint32_t>((size_t)(ncols + k + 2) * 8);
+  loaded = true;
+}
+
+std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
+  if (!loaded) throw Err{SEZKP_E_INVALID, "no trace uploaded"};
+  HIP_OR_THROW(hipSetDevice(device));
+  const int k = logN;
+  auto rec = [&](int s) { HIP_OR_THROW(hipEventRecord(ev[s], st)); };
+  auto ok = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess) throw Err{SEZKP_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
+  };
+
+  rec(0);
+  // ---- column commitments (openings.rs:306-398)
+  ok(launch_expand(st, T), "expand");
+  rec(1);
+  ok(launch_col_commit(st, T, d_tmpl, ncols, d_outer, outer_stride, logChunks), "col_commit");
+  rec(2);
+  TreeDev outer0{d_outer, d_colroots, logChunks, 0};
+  ok(launch_tree_upper(st, &outer0, ncols, outer_stride, 8, 0), "col_outer");
+  rec(3);
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipStreamSynchronize(st));
+  std::vector<uint8_t> colroots((uint8_t*)h_small, (uint8_t*)h_small + (size_t)ncols * 32);
+
+  // ---- transcript prelude + column roots (prover.rs:67-81)
+  Transcript tr("sezkp-stark/v1");
+  tr.absorb("manifest_root", mroot, 32);
+  tr.absorb_u64("n", n);
+  tr.absorb_u64("tau", tau);
+  tr.absorb_u64("n_cols", (uint64_t)ncols);
+  for (int c = 0; c < ncols; c++) tr.absorb("col_root", colroots.data() + 32 * c, 32);
+  // alphas (params.rs:82-92) with the reuse of prover.rs:86-98
+  auto ab = tr.challenge("alphas", 64);
+  uint64_t a[8];
+  for (int i = 0; i < 8; i++) a[i] = rd64(ab.data() + 8 * i) % GL_P_HOST;
+  Alphas A{a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[0], a[2], a[2]};
+  // masks (masking.rs:56-79): one cubic
+  tr.absorb("masks", "masks", 5);
+  tr.absorb_u64("n_masks", 1);
+  tr.absorb_u64("deg", 4);
+  uint64_t mask[4];
+  for (int j = 0; j < 4; j++) mask[j] = rd64(tr.challenge("mask_coeff", 8).data()) % GL_P_HOST;
+  // OOD point + coset nudge (prover.rs:119-135)
+  uint64_t z = rd64(tr.challenge("ood_point", 8).data()) % GL_P_HOST;
+  const uint64_t shift_inv = hgl_inv(3);
+  for (;;) {
+    uint64_t t = hgl_mul(z, shift_inv);
+    for (int i = 0; i < k; i++) t = hgl_mul(t, t);
+    if (t != 1) break;
+    z = hgl_add(z, 1);
+  }
+
+  // ---- composition + LDE + DEEP + layer-0 tree (prover.rs:137-189, lde.rs:42-97)
+  ok(launch_compose(st, T, A, mask, tw, logn, d_base), "compose");
+  rec(4);
+  ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
+  rec(5);
+  const uint64_t inv_n = hgl_inv(n % GL_P_HOST);
+  ok(ntt_dit(st, d_lde, logN, false, tw, d_base, logn, inv_n), "lde_ntt");
+  rec(6);
+  ok(launch_deep(st, d_lde, logN, z, tw), "deep");
+  rec(7);
+  ok(launch_leaf_subtree(st, d_lde, nullptr, logN, 0, 0, trees[0]), "layer0_tree");
+  rec(8);
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipStreamSynchronize(st));
+  std::vector<uint8_t> roots((size_t)(k + 1) * 32);
+  memcpy(roots.data(), h_small, 32);
+  tr.absorb("fri_layer_root", roots.data(), 32);
+
+  // ---- FRI folds + layer trees (prover.rs:192-239)
+  auto bb = tr.challenge("fri_betas", 8 * (size_t)k);
+  for (int r = 0; r < k; r++) {
+    const uint64_t beta = rd64(bb.data() + 8 * r) % GL_P_HOST;
+    const uint64_t* in = r == 0 ? d_lde : d_fri + (N - (N >> (r - 1)));
+    uint64_t* out = d_fri + (N - (N >> r));
+    ok(launch_leaf_subtree(st, in, out, logN - r - 1, 1, beta, trees[r + 1]), "fri_fold");
+  }
+  rec(9);
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipStreamSynchronize(st));
+  memcpy(roots.data(), h_small, (size_t)(k + 1) * 32);
+  for (int r = 1; r <= k; r++) tr.absorb("fri_layer_root", roots.data() + 32 * r, 32);
+
+  // ---- queries (prover.rs:248, 297)
+  auto qb = tr.challenge("row_queries", 8 * NUM_QUERIES);
+  uint64_t rows[NUM_QUERIES], frows[NUM_QUERIES];
+  for (int i = 0; i < NUM_QUERIES; i++) rows[i] = rd64(qb.data() + 8 * i) % n;
+  auto fb = tr.challenge("row_queries", 8 * NUM_QUERIES);
+  for (int i = 0; i < NUM_QUERIES; i++) frows[i] = rd64(fb.data() + 8 * i) % N;
+
+  // FRI path requests: per query, per layer r < k: (r, i), (r, i ^ half)
+  std::vector<uint64_t> pos((size_t)NUM_QUERIES * (k + 1));
+  size_t nf = 0;
+  for (int q = 0; q < NUM_QUERIES; q++) {
+    uint64_t* p = &pos[(size_t)q * (k + 1)];
+    p[0] = frows[q];
+    uint64_t len = N;
+    for (int r = 0; r < k; r++) {
+      const uint64_t half = len / 2;
+      h_req[2 * nf] = r; h_req[2 * nf + 1] = (uint32_t)p[r]; nf++;
+      h_req[2 * nf] = r; h_req[2 * nf + 1] = (uint32_t)(p[r] ^ half); nf++;
+      p[r + 1] = p[r] % half;
+      len = half;
+    }
+  }
+  // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66)
+  uint32_t* oreq = h_req + 2 * max_fri_req;
+  size_t no = 0;
+  auto push_open = [&](int c, uint64_t row) {
+    oreq[3 * no] = (uint32_t)c;
+    oreq[3 * no + 1] = (uint32_t)row;
+    oreq[3 * no + 2] = (uint32_t)(row >> 32);
+    no++;
+  };
+  for (int q = 0; q < NUM_QUERIES; q++) {
+    const uint64_t row = rows[q], ip1 = row + 1 < n ? row + 1 : 0;  // next_wrap
+    for (uint32_t r = 0; r < tau; r++) {
+      push_open(3 + 0 * tau + r, row);   // mv
+      push_open(3 + 0 * tau + r, ip1);   // next_mv
+      push_open(3 + 1 * tau + r, row);   // write_flag
+      push_open(3 + 2 * tau + r, row);   // write_sym
+      push_open(3 + 3 * tau + r, row);   // head
+      push_open(3 + 3 * tau + r, ip1);   // next_head
+      push_open(3 + 4 * tau + r, row);   // win_len
+      push_open(3 + 5 * tau + r, row);   // in_off
+      push_open(3 + 6 * tau + r, row);   // out_off
+    }
+    push_open(1, row);  // is_first
+    push_open(2, row);  // is_last
+    push_open(0, row);  // input_mv
+  }
+  HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (2 * max_fri_req + 3 * no) * 4, hipMemcpyHostToDevice, st));
+  ok(launch_fri_paths(st, d_layers, d_req, (int)nf, d_fri_out), "fri_paths");
+  rec(10);
+  ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 2 * max_fri_req, (int)no, d_open_out),
+     "col_open");
+  rec(11);
+  HIP_OR_THROW(hipMemcpyAsync(h_fri_out, d_fri_out, nf * PATH_REC_WORDS * 4, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipMemcpyAsync(h_open_out, d_open_out, no * OPEN_REC_WORDS * 4, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), d_fri + (N - 2), 8, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipStreamSynchronize(st));
+  for (int s = 0; s < ST_NSTAGE; s++) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ev[s], ev[s + 1]) == hipSuccess) stage_ms[s] = ms;
+  }
+  float tot = 0;
+  (void)hipEventElapsedTime(&tot, ev[0], ev[ST_NSTAGE]);
+  stage_ms[ST_NSTAGE] = tot;
+  have_times = true;
+
+  // ---- bincode ProofV1 (proof.rs:80-98)
+  BinWriter w;
+  w.b.reserve(4u << 20);
+  w.u64(N);    // domain_n
+  w.u64(tau);  // tau
+  w.u64((uint64_t)ncols);
+  for (int c = 0; c < ncols; c++) {
+    w.u64(labels[c].size());
+    w.raw(labels[c].data(), labels[c].size());
+    w.raw(colroots.data() + 32 * c, 32);
+  }
+  const int logcl = logn < COL_CHUNK_LOG2 ? logn : COL_CHUNK_LOG2;
+  w.u64(NUM_QUERIES);
+  size_t oi = 0;
+  auto emit_open = [&](uint64_t row) {
+    const uint32_t* o = h_open_out + oi * OPEN_REC_WORDS;
+    oi++;
+    const uint64_t ch = row >> COL_CHUNK_LOG2;
+    w.raw(o, 8);                        // value_le
+    w.u64(row);                         // index
+    w.u64(ch);                          // chunk_index
+    w.u64(row - (ch << COL_CHUNK_LOG2));  // index_in_chunk
+    w.raw(o + 2, 32);                   // chunk_root
+    w.u64((uint64_t)logcl);
+    w.raw(o + 10, 32 * (size_t)logcl);  // path_in_chunk
+    w.u64((uint64_t)logChunks);
+    w.raw(o + 90, 32 * (size_t)logChunks);  // path_to_chunk
+  };
+  for (int q = 0; q < NUM_QUERIES; q++) {
+    const uint64_t row = rows[q], ip1 = row + 1 < n ? row + 1 : 0;
+    w.u64(row);
+    w.u64(tau);
+    for (uint32_t r = 0; r < tau; r++) {
+      emit_open(row); emit_open(ip1); emit_open(row); emit_open(row); emit_open(row);
+      emit_open(ip1); emit_open(row); emit_open(row); emit_open(row);
+    }
+    emit_open(row); emit_open(row); emit_open(row);
+  }
+  w.u64((uint64_t)k + 1);  // fri_roots
+  w.raw(roots.data(), roots.size());
+  w.u64(NUM_QUERIES);      // fri_queries
+  size_t fi = 0;
+  for (int q = 0; q < NUM_QUERIES; q++) {
+    const uint64_t* p = &pos[(size_t)q * (k + 1)];
+    w.u64((uint64_t)k + 1);
+    for (int r = 0; r <= k; r++) w.u64(p[r]);
+    w.u64((uint64_t)k);
+    for (int r = 0; r < k; r++) {
+      const uint64_t L = (uint64_t)(k - r);
+      for (int side = 0; side < 2; side++) {
+        const uint32_t* o = h_fri_out + (fi++) * PATH_REC_WORDS;
+        w.raw(o, 8);
+        w.u64(L);
+        w.raw(o + 4, 32 * L);
+      }
+    }
+  }
+  uint8_t fv[8];
+  memcpy(fv, h_small + 8 * (k + 1), 8);  // final value = layer k's single element (prover.rs:242-243)
+  w.raw(fv, 8);
+  w.raw(mroot, 32);
+  return std::move(w.b);
+}
+
+// ==================================================================== C ABI
+extern "C" {
+
+uint32_t sezkp_abi_version(void) { return SEZKP_ABI_VERSION; }
+const char* sezkp_version(void) { return "sezkp-mi355x 0.1.0 (stark-v1, gfx950)"; }
+
+void sezkp_buf_free(sezkp_buf* b) {
+  if (b && b->data) {
+    free(b->data);
+    b->data = nullptr;
+    b->len = 0;
+  }
+}
+
+static void to_buf(const std::vector<uint8_t>& v, sezkp_buf* out) {
+  out->data = (uint8_t*)malloc(v.size() ? v.size() : 1);
+  if (!out->data) throw Err{SEZKP_E_NOMEM, "out of host memory"};
+  memcpy(out->data, v.data(), v.size());
+  out->len = v.size();
+}
+static void to_buf(const std::string& s, sezkp_buf* out) { to_buf(std::vector<uint8_t>(s.begin(), s.end()), out); }
+
+sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len) {
+  try {
+    std::unique_ptr<sezkp_ctx> c(new sezkp_ctx());
+    c->device = device;
+    int cnt = 0;
+    HIP_OR_THROW(hipGetDeviceCount(&cnt));
+    if (device < 0 || device >= cnt) throw Err{SEZKP_E_DEVICE, "no such HIP device " + std::to_string(device)};
+    HIP_OR_THROW(hipSetDevice(device));
+    HIP_OR_THROW(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    for (auto& e : c->ev) HIP_OR_THROW(hipEventCreate(&e));
+    c->tw = tables_for_device(device);
+    return c.release();
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+  }
+  return nullptr;
+}
+void sezkp_ctx_destroy(sezkp_ctx* ctx) { delete ctx; }
+
+int32_t sezkp_ctx_upload(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len) {
+  try {
+    if (!ctx || !blocks) throw Err{SEZKP_E_INVALID, "null argument"};
+    ctx->upload(*blocks);
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+    return SEZKP_E_NOMEM;
+  }
+}
+
+int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, sezkp_buf* proof_bytes,
+                        char* err, size_t err_len) {
+  (void)flags;
+  try {
+    if (!ctx || !manifest_root || !proof_bytes) throw Err{SEZKP_E_INVALID, "null argument"};
+    to_buf(ctx->prove(manifest_root), proof_bytes);
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+    return SEZKP_E_NOMEM;
+  }
+}
+
+int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max) {
+  if (!ctx || !ctx->have_times) return 0;
+  int cnt = 0;
+  for (int s = 0; s <= ST_NSTAGE && cnt < max; s++) out_ms[cnt++] = ctx->stage_ms[s];
+  return cnt;
+}
+void* sezkp_ctx_stream(const sezkp_ctx* ctx) { return ctx ? (void*)ctx->st : nullptr; }
+
+static std::vector<MetaEntry> meta_for(uint64_t domain_n, uint32_t tau, uint32_t flags) {
+  std::vector<MetaEntry> m = {{"proto", true, "stark-v1", 0}, {"domain_n", false, "", domain_n}, {"tau", false, "", tau}};
+  if (flags & SEZKP_FLAG_STREAMING) m.push_back({"mode", true, "streaming", 0});
+  return m;
+}
+
+int32_t sezkp_stark_v1_prove(const sezkp_block_view* blocks, const uint8_t manifest_root[32], uint32_t flags,
+                             sezkp_buf* proof_bytes, sezkp_buf* meta_json, char* err, size_t err_len) {
+  sezkp_ctx* ctx = sezkp_ctx_create(0, err, err_len);
+  if (!ctx) return SEZKP_E_DEVICE;
+  int32_t rc = sezkp_ctx_upload(ctx, blocks, err, err_len);
+  if (rc == SEZKP_OK) rc = sezkp_ctx_prove(ctx, manifest_root, flags, proof_bytes, err, err_len);
+  if (rc == SEZKP_OK && meta_json) {
+    try {
+      to_buf(meta_to_json(meta_for(ctx->N, ctx->tau, flags)), meta_json);
+    } catch (const Err& e) {
+      set_err(err, err_len, e.msg);
+      rc = e.code;
+    }
+  }
+  sezkp_ctx_destroy(ctx);
+  return rc;
+}
+
+int32_t sezkp_stark_v1_prove_artifact_cbor(const sezkp_block_view* blocks, const uint8_t manifest_root[32],
+                                           uint32_t flags, sezkp_buf* artifact_cbor, char* err, size_t err_len) {
+  sezkp_buf pb{};
+  int32_t rc = sezkp_stark_v1_prove(blocks, manifest_root, flags, &pb, nullptr, err, err_len);
+  if (rc != SEZKP_OK) return rc;
+  try {
+    std::vector<uint8_t> proof(pb.data, pb.data + pb.len);
+    sezkp_buf_free(&pb);
+    const uint64_t domain_n = rd64(proof.data());
+    const uint32_t tau = blocks->tau;
+    to_buf(encode_artifact_cbor("stark", manifest_root, proof, meta_for(domain_n, tau, flags)), artifact_cbor);
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+    return e.code;
+  }
+}
+
+// ---------------------------------------------------------- kernel level
+int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir, void* stream) {
+  try {
+    int dev = 0;
+    HIP_OR_THROW(hipGetDevice(&dev));
+    const NttTables& T = tables_for_device(dev);
+    hipStream_t st = (hipStream_t)stream;
+    if (log_n > 28 || (dir != 1 && dir != -1)) return SEZKP_E_INVALID;
+    if (log_n == 0) return SEZKP_OK;
+    const bool inv = dir < 0;
+    if (ntt_dif(st, d, (int)log_n, inv, T) != hipSuccess) return SEZKP_E_DEVICE;
+    const uint64_t scale = inv ? hgl_inv((1ULL << log_n) % GL_P_HOST) : 1;
+    if (bitrev_permute(st, d, scratch, (int)log_n, scale, inv) != hipSuccess) return SEZKP_E_DEVICE;
+    if (hipMemcpyAsync(d, scratch, 8ULL << log_n, hipMemcpyDeviceToDevice, st) != hipSuccess) return SEZKP_E_DEVICE;
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    return e.code;
+  }
+}
+
+int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_blowup, uint64_t z, uint64_t* out,
+                                void* stream) {
+  try {
+    int dev = 0;
+    HIP_OR_THROW(hipGetDevice(&dev));
+    const NttTables& T = tables_for_device(dev);
+    hipStream_t st = (hipStream_t)stream;
+    if (log_blowup != 3 || log_n + log_blowup > 31) return SEZKP_E_INVALID;
+    const int logN = (int)(log_n + log_blowup);
+    if (ntt_dif(st, evals, (int)log_n, true, T) != hipSuccess) return SEZKP_E_DEVICE;
+    const uint64_t inv_n = hgl_inv((1ULL << log_n) % GL_P_HOST);
+    if (ntt_dit(st, out, logN, false, T, evals, (int)log_n, inv_n) != hipSuccess) return SEZKP_E_DEVICE;
+    if (launch_deep(st, out, logN, z, T) != hipSuccess) return SEZKP_E_DEVICE;
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    return e.code;
+  }
+}
+
+int32_t sezkp_fri_fold_commit(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, uint8_t* root32,
+                              void* stream) {
+  if (n_out == 0 || (n_out & (n_out - 1))) return SEZKP_E_INVALID;
+  const int L = ilog2(n_out);
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* nodes = nullptr;
+  const uint64_t cnt = tree_stored_nodes(L, LSTORE_FRI) + 1;
+  if (hipMalloc(&nodes, cnt * 32 + 32) != hipSuccess) return SEZKP_E_DEVICE;
+  TreeDev t{nodes, nodes + cnt * 8, L, LSTORE_FRI};
+  int32_t rc = SEZKP_OK;
+  if (launch_leaf_subtree(st, in, out, L, 1, beta % GL_P_HOST, t) != hipSuccess) rc = SEZKP_E_DEVICE;
+  if (rc == SEZKP_OK && hipMemcpyAsync(root32, t.root, 32, hipMemcpyDeviceToHost, st) != hipSuccess) rc = SEZKP_E_DEVICE;
+  if (rc == SEZKP_OK && hipStreamSynchronize(st) != hipSuccess) rc = SEZKP_E_DEVICE;
+  (void)hipFree(nodes);
+  return rc;
+}
+
+int32_t sezkp_merkle_root_u64(const uint64_t* vals, uint64_t n, uint8_t* root32, void* stream) {
+  if (n == 0 || (n & (n - 1))) return SEZKP_E_INVALID;
+  const int L = ilog2(n);
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* nodes = nullptr;
+  const uint64_t cnt = tree_stored_nodes(L, LSTORE_FRI) + 1;
+  if (hipMalloc(&nodes, cnt * 32 + 32) != hipSuccess) return SEZKP_E_DEVICE;
+  TreeDev t{nodes, nodes + cnt * 8, L, LSTORE_FRI};
+  int32_t rc = SEZKP_OK;
+  if (launch_leaf_subtree(st, vals, nullptr, L, 0, 0, t) != hipSuccess) rc = SEZKP_E_DEVICE;
+  if (rc == SEZKP_OK && hipMemcpyAsync(root32, t.root, 32, hipMemcpyDeviceToHost, st) != hipSuccess) rc = SEZKP_E_DEVICE;
+  if (rc == SEZKP_OK && hipStreamSynchronize(st) != hipSuccess) rc = SEZKP_E_DEVICE;
+  (void)hipFree(nodes);
+  return rc;
+}
+
+// ---------------------------------------------------------- host helpers
+int32_t sezkp_manifest_root(const sezkp_block_view* blocks, uint8_t out[32]) {
+  if (!blocks || !out) return SEZKP_E_INVALID;
+  manifest_root(*blocks, out);
+  return SEZKP_OK;
+}
+
+struct sezkp_blocks {
+  BlockStore s;
+};
+int32_t sezkp_blocks_decode_cbor(const uint8_t* data, size_t len, sezkp_blocks** out, char* err, size_t err_len) {
+  std::unique_ptr<sezkp_blocks> b(new sezkp_blocks());
+  std::string e;
+  if (!decode_blocks_cbor(data, len, b->s, e)) {
+    set_err(err, err_len, e);
+    return SEZKP_E_DECODE;
+  }
+  *out = b.release();
+  return SEZKP_OK;
+}
+const sezkp_block_view* sezkp_blocks_view(const sezkp_blocks* b) { return b ? &b->s.view : nullptr; }
+void sezkp_blocks_free(sezkp_blocks* b) { delete b; }
+void sezkp_blake3(const uint8_t* data, size_t len, uint8_t* out, size_t out_len) {
+  Blake3 h;
+  h.update(data, len);
+  h.finalize(out, out_len);
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+// sezkp_internal.h — structures shared by the HIP kernels and the host
+// orchestrator of the MI355X STARK v1 prover (not part of the public C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sezkp {
+
+// w_{2^K}^e = hi[e >> S] * lo[e & (2^S - 1)]; p3_* likewise for 3^e.
+struct NttTables {
+  const uint64_t* hi;
+  const uint64_t* lo;
+  const uint64_t* p3_hi;
+  const uint64_t* p3_lo;
+  int K;
+  int S;
+};
+
+struct NttPassArgs {
+  uint64_t* a;
+  const uint64_t* src;  // replicated LDE load source (bit-reversed coeffs), or null
+  NttTables tw;
+  uint64_t inv_n;
+  int m, sL, logC, inverse, skip, log_src;
+};
+
+hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
+hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
+                   const uint64_t* src, int log_src, uint64_t inv_n);
+hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale,
+                          bool do_scale);
+
+// A binary Merkle tree over 2^logLen leaves whose levels >= lstore are kept
+// in HBM: level l (lstore <= l <= logLen) starts at node
+// off(l) = 2^(logLen-lstore+1) - 2^(logLen-l+1); 8 u32 words per node.
+// Lower levels are recomputed from the leaf values when a path is opened.
+struct TreeDev {
+  uint32_t* nodes;
+  uint32_t* root;   // 8 words
+  int logLen;
+  int lstore;
+};
+__host__ __device__ inline uint64_t tree_level_off(int logLen, int lstore, int l) {
+  return (1ULL << (logLen - lstore + 1)) - (1ULL << (logLen - l + 1));
+}
+__host__ __device__ inline uint64_t tree_stored_nodes(int logLen, int lstore) {
+  return logLen >= lstore ? (1ULL << (logLen - lstore + 1)) - 1 : 0;
+}
+
+// Device image of the trace (struct-of-arrays, tape-major), built by upload.
+struct TraceDev {
+  uint64_t n;
+  int tau;
+  uint32_t nblk;
+  const int8_t* input_mv;     // [n]
+  const int8_t* mv;           // [tau][n]
+  const uint8_t* wflag;       // [tau][n]
+  const uint16_t* wsym;       // [tau][n]  (0 when no write)
+  const uint64_t* blk_start;  // [nblk+1] row offsets
+  const uint64_t* blk_winlen; // [tau][nblk] canonical field values
+  const uint64_t* blk_offin;  // [tau][nblk]
+  const uint64_t* blk_offout; // [tau][nblk]
+  uint32_t* row_blk;          // [n]   (derived)
+  uint8_t* row_flags;         // [n]   bit0 first, bit1 last (derived)
+  int64_t* head;              // [tau][n] post-move head (derived)
+};
+
+struct Alphas {
+  uint64_t bool_flag, mv_domain, head_update, head_bits_bool, head_reconstruct, slack_bits_bool,
+      slack_reconstruct, sym_bits_bool, sym_reconstruct, boundary_first, boundary_last;
+};
+
+// Per-column BLAKE3 message template for labelled leaves
+// BLAKE3("col_leaf" || u32 len || label || v LE)  (merkle.rs:132-147).
+struct ColTemplate {
+  uint32_t words[16];
+  uint32_t block_len;  // 20 + len(label)
+  uint32_t kind;       // 0 input_mv,1 is_first,2 is_last,3+k: per-tape kind k
+  uint32_t tape;
+  uint32_t off;        // byte offset of the value = 12 + len(label)
+};
+
+constexpr int LSTORE_FRI = 6;
+constexpr int COL_CHUNK_LOG2 = 10;
+constexpr int PATH_REC_WORDS = 264;   // FRI path record: 2 value + 2 pad + 32*8 siblings
+constexpr int OPEN_REC_WORDS = 352;   // column opening record
+
+// kernels launched by the host orchestrator (prover.cpp)
+hipError_t launch_expand(hipStream_t st, const TraceDev& T);
+hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, int ncols,
+                             uint32_t* outer_nodes, uint64_t outer_stride_nodes, int logChunks);
+hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
+                          const NttTables& tw, int logn, uint64_t* out);
+hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw);
+hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold,
+                               uint64_t beta, TreeDev tree);
+hipError_t launch_tree_upper(hipStream_t st, TreeDev* trees, int ntrees_same_shape, uint64_t tree_stride_nodes,
+                             uint64_t root_stride_words, int from_level);
+struct FriLayerDev {
+  const uint64_t* vals;
+  TreeDev tree;
+};
+hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
+                            uint32_t* d_out);
+hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
+                           uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
+                           uint32_t* d_out);
+
+}  // namespace sezkp

@@ -1,0 +1,415 @@
+// trace.hip — trace-column kernels for CDNA4 (gfx950): row expansion, chunked
+// column commitments, AIR composition and column openings.
+//
+// Reference semantics:
+//  * columns (3+7*tau, label order openings.rs:89-116) with RowIter values
+//    (openings.rs:227-273; == TraceColumns::build columns.rs:252-365)
+//  * labelled leaf BLAKE3("col_leaf"||u32 len||label||v LE) (merkle.rs:132-147)
+//  * 1024-row chunk trees + outer tree over chunk roots (openings.rs:306-398)
+//  * composition C(i) = compose_row + compose_boundary (air.rs:49-136) with the
+//    alpha reuse of prover.rs:86-98, plus the cubic mask R(w_n^i)
+//    (masking.rs:86-103, prover.rs:142-158)
+//  * openings (openings.rs:403-497): value, chunk root, path in chunk, path of
+//    the chunk root in the outer tree.
+#include "dev_common.h"
+#include "sezkp_internal.h"
+
+namespace sezkp {
+
+constexpr int TR_THREADS = 256;
+
+// ------------------------------------------------------------ expansion
+// One workgroup per block: row -> block id, first/last flags, and the
+// post-move head prefix sums per tape (head starts at 0 in every block).
+__global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T) {
+  __shared__ int64_t wsum[TR_THREADS / 64];
+  const uint32_t b = blockIdx.x;
+  const uint64_t s = T.blk_start[b], e = T.blk_start[b + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (uint64_t r = s + tid; r < e; r += TR_THREADS) {
+    T.row_blk[r] = b;
+    T.row_flags[r] = (uint8_t)((r == s ? 1 : 0) | (r + 1 == e ? 2 : 0));
+  }
+  for (int tp = 0; tp < T.tau; tp++) {
+    const int8_t* mv = T.mv + (uint64_t)tp * T.n;
+    int64_t* hd = T.head + (uint64_t)tp * T.n;
+    int64_t carry = 0;
+    for (uint64_t r0 = s; r0 < e; r0 += TR_THREADS) {
+      const uint64_t r = r0 + tid;
+      int64_t x = (r < e) ? (int64_t)mv[r] : 0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) wsum[wave] = x;
+      __syncthreads();
+      int64_t pre = carry, tot = 0;
+#pragma unroll
+      for (int w = 0; w < TR_THREADS / 64; w++) {
+        if (w < wave) pre += wsum[w];
+        tot += wsum[w];
+      }
+      if (r < e) hd[r] = pre + x;
+      carry += tot;
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------ column values
+// value of column `ct` at `row` (canonical field element)
+__device__ __forceinline__ uint64_t col_value(const TraceDev& T, const ColTemplate& ct, uint64_t row) {
+  const uint64_t o = (uint64_t)ct.tape * T.n + row;
+  switch (ct.kind) {
+    case 0: return gl_from_i64(T.input_mv[row]);
+    case 1: return T.row_flags[row] & 1;
+    case 2: return (T.row_flags[row] >> 1) & 1;
+    case 3: return gl_from_i64(T.mv[o]);
+    case 4: return T.wflag[o];
+    case 5: return T.wsym[o];
+    case 6: return gl_from_i64(T.head[o]);
+    case 7: return T.blk_winlen[(uint64_t)ct.tape * T.nblk + T.row_blk[row]];
+    case 8: return T.blk_offin[(uint64_t)ct.tape * T.nblk + T.row_blk[row]];
+    default: return T.blk_offout[(uint64_t)ct.tape * T.nblk + T.row_blk[row]];
+  }
+}
+// 4 consecutive rows (row0 % 4 == 0): vector loads of the narrow columns
+__device__ __forceinline__ void col_values4(const TraceDev& T, const ColTemplate& ct, uint64_t row0, uint64_t (&v)[4]) {
+  const uint64_t o = (uint64_t)ct.tape * T.n + row0;
+  switch (ct.kind) {
+    case 0: {
+      uint32_t w = *reinterpret_cast<const uint32_t*>(T.input_mv + row0);
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = gl_from_i64((int8_t)(w >> (8 * j)));
+      return;
+    }
+    case 1:
+    case 2: {
+      uint32_t w = *reinterpret_cast<const uint32_t*>(T.row_flags + row0);
+      const int sh = ct.kind - 1;
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = (w >> (8 * j + sh)) & 1;
+      return;
+    }
+    case 3: {
+      uint32_t w = *reinterpret_cast<const uint32_t*>(T.mv + o);
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = gl_from_i64((int8_t)(w >> (8 * j)));
+      return;
+    }
+    case 4: {
+      uint32_t w = *reinterpret_cast<const uint32_t*>(T.wflag + o);
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = (w >> (8 * j)) & 0xff;
+      return;
+    }
+    case 5: {
+      uint2 w = *reinterpret_cast<const uint2*>(T.wsym + o);
+      v[0] = w.x & 0xffff; v[1] = w.x >> 16; v[2] = w.y & 0xffff; v[3] = w.y >> 16;
+      return;
+    }
+    case 6: {
+      const longlong2* p = reinterpret_cast<const longlong2*>(T.head + o);
+      longlong2 a = p[0], b = p[1];
+      v[0] = gl_from_i64(a.x); v[1] = gl_from_i64(a.y); v[2] = gl_from_i64(b.x); v[3] = gl_from_i64(b.y);
+      return;
+    }
+    default: {
+      const uint64_t* tab = ct.kind == 7 ? T.blk_winlen : (ct.kind == 8 ? T.blk_offin : T.blk_offout);
+      tab += (uint64_t)ct.tape * T.nblk;
+      uint4 bl = *reinterpret_cast<const uint4*>(T.row_blk + row0);
+      v[0] = tab[bl.x]; v[1] = tab[bl.y]; v[2] = tab[bl.z]; v[3] = tab[bl.w];
+      return;
+    }
+  }
+}
+
+// labelled leaf with the value at compile-time byte offset OFF (= 12 + len(label))
+template <int OFF>
+__device__ __forceinline__ void leaf_labeled_t(const ColTemplate& ct, uint64_t v, uint32_t (&out)[8]) {
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) m[i] = ct.words[i];
+  constexpr int W = OFF / 4, B = OFF % 4;
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  if (B == 0) {
+    m[W] |= lo;
+    m[W + 1] |= hi;
+  } else {
+    m[W] |= lo << (8 * B);
+    m[W + 1] |= (lo >> (32 - 8 * B)) | (hi << (8 * B));
+    m[W + 2] |= hi >> (32 - 8 * B);
+  }
+  b3_hash_block(m, OFF + 8, out);
+}
+// generic (any label length <= 44): value words inserted with runtime shifts
+__device__ __forceinline__ void leaf_labeled_rt(const ColTemplate& ct, uint64_t v, uint32_t (&out)[8]) {
+  uint32_t m[16];
+  const int W = ct.off >> 2, B = ct.off & 3;
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t x0 = B ? lo << (8 * B) : lo;
+  const uint32_t x1 = B ? (lo >> (32 - 8 * B)) | (hi << (8 * B)) : hi;
+  const uint32_t x2 = B ? hi >> (32 - 8 * B) : 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+    m[i] = ct.words[i] | (i == W ? x0 : 0) | (i == W + 1 ? x1 : 0) | (i == W + 2 ? x2 : 0);
+  b3_hash_block(m, ct.off + 8, out);
+}
+template <int OFF>
+__device__ __forceinline__ void leaf_labeled(const ColTemplate& ct, uint64_t v, uint32_t (&out)[8]) {
+  if constexpr (OFF == 0) leaf_labeled_rt(ct, v, out);
+  else leaf_labeled_t<OFF>(ct, v, out);
+}
+
+__device__ __forceinline__ void lds_put8(uint32_t (*lds)[TR_THREADS], int i, const uint32_t (&h)[8]) {
+#pragma unroll
+  for (int w = 0; w < 8; w++) lds[w][i] = h[w];
+}
+
+// 4 consecutive labelled leaves -> level-2 node
+template <int OFF>
+__device__ __forceinline__ void hash4_labeled(const ColTemplate& ct, const uint64_t (&v)[4], uint32_t (&h)[8]) {
+  uint32_t a[8], b[8], p0[8], p1[8];
+  leaf_labeled<OFF>(ct, v[0], a);
+  leaf_labeled<OFF>(ct, v[1], b);
+  b3_parent(a, b, p0);
+  leaf_labeled<OFF>(ct, v[2], a);
+  leaf_labeled<OFF>(ct, v[3], b);
+  b3_parent(a, b, p1);
+  b3_parent(p0, p1, h);
+}
+
+// -------------------------------------------------------- column commit
+// grid (n_chunks, ncols); one 256-lane WG per (chunk, column): 1024 rows,
+// 4 rows per lane folded to a level-2 node in registers, 8 LDS levels above.
+// Writes the chunk root as leaf `chunk` of the column's outer tree.
+template <int OFF>
+__device__ __forceinline__ void commit_body(const TraceDev& T, const ColTemplate& ct, uint64_t row0, uint32_t (&h)[8]) {
+  uint64_t v[4];
+  col_values4(T, ct, row0, v);
+  hash4_labeled<OFF>(ct, v, h);
+}
+
+__global__ void __launch_bounds__(TR_THREADS) k_col_commit(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                           uint32_t* __restrict__ outer, uint64_t outer_stride) {
+  __shared__ uint32_t lds[8][TR_THREADS];
+  const int c = blockIdx.y;
+  const uint64_t ch = blockIdx.x;
+  const ColTemplate ct = tmpl[c];
+  const int tid = threadIdx.x;
+  const uint64_t n = T.n;
+  const uint64_t cl = n < 1024 ? n : 1024;
+  int logcl = 0;
+  while ((1ULL << logcl) < cl) logcl++;
+  const int logper = logcl < 2 ? logcl : 2;
+  const int nact = (int)(cl >> logper);
+  if (tid < nact) {
+    const uint64_t row0 = (ch << COL_CHUNK_LOG2) + ((uint64_t)tid << logper);
+    uint32_t h[8];
+    if (logper == 2) {
+      switch (ct.off) {
+        case 16: commit_body<16>(T, ct, row0, h); break;
+        case 17: commit_body<17>(T, ct, row0, h); break;
+        case 18: commit_body<18>(T, ct, row0, h); break;
+        case 19: commit_body<19>(T, ct, row0, h); break;
+        case 20: commit_body<20>(T, ct, row0, h); break;
+        case 21: commit_body<21>(T, ct, row0, h); break;
+        case 22: commit_body<22>(T, ct, row0, h); break;
+        case 23: commit_body<23>(T, ct, row0, h); break;
+        default: commit_body<0>(T, ct, row0, h); break;
+      }
+    } else if (logper == 1) {
+      uint32_t a[8], b[8];
+      leaf_labeled_rt(ct, col_value(T, ct, row0), a);
+      leaf_labeled_rt(ct, col_value(T, ct, row0 + 1), b);
+      b3_parent(a, b, h);
+    } else {
+      leaf_labeled_rt(ct, col_value(T, ct, row0), h);
+    }
+    lds_put8(lds, tid, h);
+  }
+  __syncthreads();
+  int cnt = nact;
+  while (cnt > 1) {
+    const int half = cnt >> 1;
+    uint32_t h[8];
+    const bool act = tid < half;
+    if (act) {
+      uint32_t l[8], r[8];
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        uint2 p = *reinterpret_cast<const uint2*>(&lds[w][2 * tid]);
+        l[w] = p.x;
+        r[w] = p.y;
+      }
+      b3_parent(l, r, h);
+    }
+    __syncthreads();
+    if (act) lds_put8(lds, tid, h);
+    __syncthreads();
+    cnt = half;
+  }
+  if (tid < 8) outer[(uint64_t)c * outer_stride * 8 + ch * 8 + tid] = lds[tid][0];
+}
+
+// ------------------------------------------------------------ composition
+// C(i) per air.rs:49-136. Exact simplifications (flags are 0/1 by
+// construction, bit columns are boolean): every alpha*flag*(flag-1) and
+// alpha*flg*sum(b(b-1)) term is identically zero and is skipped; the bit
+// reconstructions equal x & 0xFFFF / x & 0xF of the canonical value.
+__global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, uint64_t m0, uint64_t m1, uint64_t m2,
+                                                        uint64_t m3, NttTables tw, int logn, uint64_t* __restrict__ out) {
+  const uint64_t n = T.n;
+  const uint64_t i0 = ((uint64_t)blockIdx.x * TR_THREADS + threadIdx.x) * 4;
+  if (i0 >= n) return;
+  // x = w_n^i0, then incremental
+  const uint64_t e0 = i0 << (tw.K - logn), e1 = 1ULL << (tw.K - logn);
+  const uint64_t smask = (1ULL << tw.S) - 1;
+  uint64_t x = gl_mul(tw.hi[e0 >> tw.S], tw.lo[e0 & smask]);
+  const uint64_t wn = gl_mul(tw.hi[e1 >> tw.S], tw.lo[e1 & smask]);
+  const int cnt = n - i0 < 4 ? (int)(n - i0) : 4;
+  for (int j = 0; j < cnt; j++) {
+    const uint64_t i = i0 + j;
+    const uint64_t ip1 = (i + 1) & (n - 1);
+    const uint8_t fl = T.row_flags[i];
+    const bool is_first = fl & 1, is_last = (fl >> 1) & 1;
+    const uint32_t blk = T.row_blk[i];
+    uint64_t acc = 0;
+    for (int r = 0; r < T.tau; r++) {
+      const uint64_t o = (uint64_t)r * n;
+      const int64_t mv = T.mv[o + i];
+      const int64_t head = T.head[o + i];
+      const uint64_t head_f = gl_from_i64(head);
+      const uint64_t mv_f = gl_from_i64(mv);
+      // C2: mv(mv-1)(mv+1) = mv^3 - mv  (|mv| <= 128: exact in i64)
+      const int64_t c2 = mv * mv * mv - mv;
+      if (c2) acc = gl_add(acc, gl_mul(A.mv_domain, gl_from_i64(c2)));
+      // C3: (1 - is_last) * (head' - head - mv')
+      if (!is_last) {
+        const int64_t d = T.head[o + ip1] - head - (int64_t)T.mv[o + ip1];
+        if (d) acc = gl_add(acc, gl_mul(A.head_update, gl_from_i64(d)));
+      }
+      if (T.wflag[o + i]) {
+        // head - sum(head_bits * 2^k)
+        acc = gl_add(acc, gl_mul(A.head_reconstruct, gl_sub(head_f, head_f & 0xFFFF)));
+        // slack = (win_len - 1) - head, reconstructed from 16 bits
+        const uint64_t winlen = T.blk_winlen[(uint64_t)r * T.nblk + blk];
+        const uint64_t slack = gl_sub(gl_sub(winlen, 1), head_f);
+        acc = gl_add(acc, gl_mul(A.slack_reconstruct, gl_sub(slack, slack & 0xFFFF)));
+        // symbol 4-bit decomposition
+        const uint64_t sym = T.wsym[o + i];
+        acc = gl_add(acc, gl_mul(A.sym_reconstruct, sym - (sym & 0xF)));
+      }
+      if (is_first) {
+        const uint64_t offin = T.blk_offin[(uint64_t)r * T.nblk + blk];
+        acc = gl_add(acc, gl_mul(A.boundary_first, gl_sub(gl_sub(head_f, mv_f), offin)));
+      }
+      if (is_last) {
+        const uint64_t offout = T.blk_offout[(uint64_t)r * T.nblk + blk];
+        acc = gl_add(acc, gl_mul(A.boundary_last, gl_sub(head_f, offout)));
+      }
+    }
+    // mask R(x) = m0 + m1 x + m2 x^2 + m3 x^3 (Horner)
+    uint64_t R = gl_add(gl_mul(gl_add(gl_mul(gl_add(gl_mul(m3, x), m2), x), m1), x), m0);
+    out[i] = gl_add(acc, R);
+    x = gl_mul(x, wn);
+  }
+}
+
+// -------------------------------------------------------- column openings
+// One 256-lane WG per request (column, row): rebuild the row's chunk tree in
+// LDS (<= 1024 leaves), emit value, chunk root, path in chunk, and the chunk
+// root's path in the stored outer tree.
+// Record words: [0,1] value, [2..9] chunk_root, [10..89] path_in (<=10),
+// [90..345] path_to_chunk (<=32).
+__global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                         const uint32_t* __restrict__ outer, uint64_t outer_stride,
+                                                         int logChunks, const uint32_t* __restrict__ req,
+                                                         uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[8][1024];
+  const uint32_t q = blockIdx.x;
+  const int c = req[3 * q];
+  const uint64_t row = (uint64_t)req[3 * q + 1] | ((uint64_t)req[3 * q + 2] << 32);
+  const ColTemplate ct = tmpl[c];
+  const int tid = threadIdx.x;
+  const uint64_t n = T.n;
+  const uint64_t ch = row >> COL_CHUNK_LOG2;
+  const uint64_t start = ch << COL_CHUNK_LOG2;
+  const uint64_t cl = n < 1024 ? n : 1024;
+  int logcl = 0;
+  while ((1ULL << logcl) < cl) logcl++;
+  uint32_t* o = out + (uint64_t)q * OPEN_REC_WORDS;
+  for (uint64_t i = tid; i < cl; i += TR_THREADS) {
+    uint32_t h[8];
+    leaf_labeled_rt(ct, col_value(T, ct, start + i), h);
+#pragma unroll
+    for (int w = 0; w < 8; w++) lds[w][i] = h[w];
+  }
+  if (tid == 0) {
+    const uint64_t v = col_value(T, ct, row);
+    o[0] = (uint32_t)v;
+    o[1] = (uint32_t)(v >> 32);
+  }
+  __syncthreads();
+  const uint64_t in = row - start;
+  int cnt = (int)cl;
+  for (int lvl = 0; lvl < logcl; lvl++) {
+    const int sib = (int)((in >> lvl) ^ 1);
+    if (tid < 8) o[10 + 8 * lvl + tid] = lds[tid][sib];
+    const int half = cnt >> 1;
+    uint32_t hh[2][8];
+    int k = 0;
+    for (int p = tid; p < half; p += TR_THREADS, k++) {
+      uint32_t a[8], b[8];
+#pragma unroll
+      for (int w = 0; w < 8; w++) { a[w] = lds[w][2 * p]; b[w] = lds[w][2 * p + 1]; }
+      b3_parent(a, b, hh[k]);
+    }
+    __syncthreads();
+    k = 0;
+    for (int p = tid; p < half; p += TR_THREADS, k++)
+#pragma unroll
+      for (int w = 0; w < 8; w++) lds[w][p] = hh[k][w];
+    __syncthreads();
+    cnt = half;
+  }
+  if (tid < 8) o[2 + tid] = lds[tid][0];
+  // path_to_chunk from the stored outer tree (all levels kept)
+  const uint32_t* ob = outer + (uint64_t)c * outer_stride * 8;
+  for (int lvl = 0; lvl < logChunks; lvl++) {
+    const uint64_t sib = (ch >> lvl) ^ 1;
+    if (tid < 8) o[90 + 8 * lvl + tid] = ob[8 * (tree_level_off(logChunks, 0, lvl) + sib) + tid];
+  }
+}
+
+// ------------------------------------------------------------------ host
+hipError_t launch_expand(hipStream_t st, const TraceDev& T) {
+  if (T.nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_expand, dim3(T.nblk), dim3(TR_THREADS), 0, st, T);
+  return hipGetLastError();
+}
+hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, int ncols,
+                             uint32_t* outer_nodes, uint64_t outer_stride_nodes, int logChunks) {
+  hipLaunchKernelGGL(k_col_commit, dim3((unsigned)(1ULL << logChunks), ncols), dim3(TR_THREADS), 0, st, T, d_tmpl,
+                     outer_nodes, outer_stride_nodes);
+  return hipGetLastError();
+}
+hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
+                          const NttTables& tw, int logn, uint64_t* out) {
+  const uint64_t thr = (T.n + 3) / 4;
+  const unsigned grid = (unsigned)((thr + TR_THREADS - 1) / TR_THREADS);
+  hipLaunchKernelGGL(k_compose, dim3(grid), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3], tw,
+                     logn, out);
+  return hipGetLastError();
+}
+hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
+                           uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
+                           uint32_t* d_out) {
+  if (nreq == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_col_open, dim3(nreq), dim3(TR_THREADS), 0, st, T, d_tmpl, outer_nodes, outer_stride_nodes,
+                     logChunks, d_req, d_out);
+  return hipGetLastError();
+}
+
+}  // namespace sezkp

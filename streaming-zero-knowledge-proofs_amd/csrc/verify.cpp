@@ -1,0 +1,299 @@
+// verify.cpp — host CPU restatement of StarkV1::verify
+// (crates/sezkp-stark/src/lib.rs:144-162 -> v1/verify.rs:60-196, fri.rs:130-222,
+// merkle.rs:110-126,243-281). O(Q k^2) hashes: not a hot path, stays on the CPU.
+#include <stdio.h>
+#include <string.h>
+
+#include <array>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/sezkp_stark.h"
+#include "codec.h"
+#include "host_crypto.h"
+
+using namespace sezkp;
+
+namespace {
+
+struct VErr {
+  int32_t code;
+  std::string msg;
+};
+#define ENSURE(c, m) \
+  do {               \
+    if (!(c)) throw VErr{SEZKP_E_VERIFY, (m)}; \
+  } while (0)
+
+struct Reader {  // bincode 1.3.3 fixint LE
+  const uint8_t* p;
+  const uint8_t* e;
+  void need(size_t n) {
+    if ((size_t)(e - p) < n) throw VErr{SEZKP_E_DECODE, "truncated proof bytes"};
+  }
+  uint64_t u64() {
+    need(8);
+    uint64_t x = 0;
+    for (int i = 7; i >= 0; i--) x = (x << 8) | p[i];
+    p += 8;
+    return x;
+  }
+  void raw(void* d, size_t n) {
+    need(n);
+    memcpy(d, p, n);
+    p += n;
+  }
+  uint64_t len(size_t elem) {
+    uint64_t n = u64();
+    if (elem && n > (uint64_t)(e - p) / elem) throw VErr{SEZKP_E_DECODE, "bad length prefix"};
+    return n;
+  }
+};
+
+typedef std::vector<std::array<uint8_t, 32>> Path;
+struct Opening {
+  uint8_t value[8];
+  uint64_t index, chunk_index, index_in_chunk;
+  uint8_t chunk_root[32];
+  std::vector<uint8_t> path_in, path_to;  // 32 B each
+};
+Opening read_opening(Reader& r) {
+  Opening o;
+  r.raw(o.value, 8);
+  o.index = r.u64();
+  o.chunk_index = r.u64();
+  o.index_in_chunk = r.u64();
+  r.raw(o.chunk_root, 32);
+  uint64_t a = r.len(32);
+  o.path_in.resize(32 * a);
+  r.raw(o.path_in.data(), o.path_in.size());
+  uint64_t b = r.len(32);
+  o.path_to.resize(32 * b);
+  r.raw(o.path_to.data(), o.path_to.size());
+  return o;
+}
+
+void hash2(const uint8_t* l, const uint8_t* r, uint8_t* out) {
+  uint8_t b[64];
+  memcpy(b, l, 32);
+  memcpy(b + 32, r, 32);
+  blake3_oneshot(b, 64, out);
+}
+bool merkle_verify(const uint8_t root[32], const uint8_t leaf[32], uint64_t idx, const uint8_t* sibs, size_t ns) {
+  uint8_t cur[32], t[32];  // merkle.rs:110-126
+  memcpy(cur, leaf, 32);
+  for (size_t i = 0; i < ns; i++) {
+    if ((idx & 1) == 0) hash2(cur, sibs + 32 * i, t);
+    else hash2(sibs + 32 * i, cur, t);
+    memcpy(cur, t, 32);
+    idx >>= 1;
+  }
+  return memcmp(cur, root, 32) == 0;
+}
+void leaf_u64(const uint8_t v[8], uint8_t out[32]) { blake3_oneshot(v, 8, out); }
+void leaf_labeled(const uint8_t v[8], const std::string& label, uint8_t out[32]) {
+  std::vector<uint8_t> m;
+  m.insert(m.end(), (const uint8_t*)"col_leaf", (const uint8_t*)"col_leaf" + 8);
+  uint32_t L = (uint32_t)label.size();
+  for (int i = 0; i < 4; i++) m.push_back((uint8_t)(L >> (8 * i)));
+  m.insert(m.end(), label.begin(), label.end());
+  m.insert(m.end(), v, v + 8);
+  blake3_oneshot(m.data(), m.size(), out);
+}
+uint64_t fe(const uint8_t v[8]) {
+  uint64_t x = 0;
+  for (int i = 7; i >= 0; i--) x = (x << 8) | v[i];
+  return x % GL_P_HOST;
+}
+uint64_t rd64(const uint8_t* p) {
+  uint64_t x = 0;
+  for (int i = 7; i >= 0; i--) x = (x << 8) | p[i];
+  return x;
+}
+
+void verify_opening(const std::map<std::string, std::array<uint8_t, 32>>& roots, const std::string& label,
+                    const Opening& o) {  // verify.rs:33-56 -> merkle.rs:243-281
+  auto it = roots.find(label);
+  ENSURE(it != roots.end(), "missing col root for " + label);
+  uint8_t leaf[32];
+  leaf_labeled(o.value, label, leaf);
+  bool ok = merkle_verify(o.chunk_root, leaf, o.index_in_chunk, o.path_in.data(), o.path_in.size() / 32) &&
+            merkle_verify(it->second.data(), o.chunk_root, o.chunk_index, o.path_to.data(), o.path_to.size() / 32);
+  ENSURE(ok, "chunked merkle path failed for column " + label + " @ " + std::to_string(o.index));
+}
+
+void verify_v1(const uint8_t* bytes, size_t len, const sezkp_block_view* blocks) {
+  Reader r{bytes, bytes + len};
+  const uint64_t domain_n = r.u64();
+  const uint64_t tau = r.u64();
+  const uint64_t ncols = r.len(40);
+  std::vector<std::string> labels(ncols);
+  std::vector<std::array<uint8_t, 32>> col_roots(ncols);
+  for (uint64_t c = 0; c < ncols; c++) {
+    uint64_t l = r.len(1);
+    labels[c].resize(l);
+    r.raw(&labels[c][0], l);
+    r.raw(col_roots[c].data(), 32);
+  }
+  struct Tape { Opening o[9]; };
+  struct Row { uint64_t row; std::vector<Tape> tapes; Opening is_first, is_last, input_mv; };
+  const uint64_t nq = r.len(8);
+  std::vector<Row> qs(nq);
+  for (auto& q : qs) {
+    q.row = r.u64();
+    uint64_t nt = r.len(9 * 80);
+    q.tapes.resize(nt);
+    for (auto& t : q.tapes)
+      for (auto& o : t.o) o = read_opening(r);
+    q.is_first = read_opening(r);
+    q.is_last = read_opening(r);
+    q.input_mv = read_opening(r);
+  }
+  const uint64_t nroots = r.len(32);
+  std::vector<std::array<uint8_t, 32>> roots(nroots);
+  for (auto& x : roots) r.raw(x.data(), 32);
+  struct Pair { uint8_t vi[8]; std::vector<uint8_t> pi; uint8_t vj[8]; std::vector<uint8_t> pj; };
+  struct FQ { std::vector<uint64_t> pos; std::vector<Pair> pairs; };
+  const uint64_t nfq = r.len(16);
+  std::vector<FQ> fq(nfq);
+  for (auto& f : fq) {
+    uint64_t np = r.len(8);
+    f.pos.resize(np);
+    for (auto& x : f.pos) x = r.u64();
+    uint64_t npr = r.len(32);
+    f.pairs.resize(npr);
+    for (auto& p : f.pairs) {
+      r.raw(p.vi, 8);
+      uint64_t a = r.len(32);
+      p.pi.resize(32 * a);
+      r.raw(p.pi.data(), p.pi.size());
+      r.raw(p.vj, 8);
+      uint64_t b = r.len(32);
+      p.pj.resize(32 * b);
+      r.raw(p.pj.data(), p.pj.size());
+    }
+  }
+  uint8_t final_le[8], mroot[32];
+  r.raw(final_le, 8);
+  r.raw(mroot, 32);
+  ENSURE(r.p == r.e, "trailing bytes in proof");
+
+  // shape (verify.rs:62-82)
+  ENSURE(domain_n % 8 == 0, "FRI domain_n not multiple of blowup");
+  const uint64_t n = domain_n / 8;
+  ENSURE(n && (n & (n - 1)) == 0, "trace length n must be a power of two");
+  if (blocks && blocks->n_blocks) ENSURE(blocks->tau == tau, "tau mismatch vs. block windows");
+
+  Transcript tr("sezkp-stark/v1");
+  tr.absorb("manifest_root", mroot, 32);
+  tr.absorb_u64("n", n);
+  tr.absorb_u64("tau", tau);
+  tr.absorb_u64("n_cols", ncols);
+  for (auto& c : col_roots) tr.absorb("col_root", c.data(), 32);
+  auto ab = tr.challenge("alphas", 64);
+  uint64_t a[8];
+  for (int i = 0; i < 8; i++) a[i] = rd64(ab.data() + 8 * i) % GL_P_HOST;
+  tr.absorb("masks", "masks", 5);
+  tr.absorb_u64("n_masks", 1);
+  tr.absorb_u64("deg", 4);
+  for (int j = 0; j < 4; j++) tr.challenge("mask_coeff", 8);
+  tr.challenge("ood_point", 8);
+  const size_t n_layers = roots.size();
+  Transcript tr_rows = tr;
+  if (n_layers > 0) {
+    tr_rows.absorb("fri_layer_root", roots[0].data(), 32);
+    tr_rows.challenge("fri_betas", 8 * (n_layers - 1));
+    for (size_t l = 1; l < n_layers; l++) tr_rows.absorb("fri_layer_root", roots[l].data(), 32);
+  }
+  auto qb = tr_rows.challenge("row_queries", 8 * 30);
+  ENSURE(qs.size() == 30, "AIR query count mismatch");
+  for (size_t i = 0; i < qs.size(); i++)
+    ENSURE(qs[i].row == rd64(qb.data() + 8 * i) % n, "AIR query row mismatch at position " + std::to_string(i));
+
+  std::map<std::string, std::array<uint8_t, 32>> root_map;
+  for (uint64_t c = 0; c < ncols; c++) root_map[labels[c]] = col_roots[c];
+  const char* KN[9] = {"mv", "mv", "wflag", "wsym", "head", "head", "winlen", "in_off", "out_off"};
+  for (auto& q : qs) {
+    verify_opening(root_map, "input_mv", q.input_mv);
+    verify_opening(root_map, "is_first", q.is_first);
+    verify_opening(root_map, "is_last", q.is_last);
+    for (size_t t = 0; t < q.tapes.size(); t++)
+      for (int j = 0; j < 9; j++) verify_opening(root_map, std::string(KN[j]) + "_" + std::to_string(t), q.tapes[t].o[j]);
+    // openings-only AIR (air.rs:209-238) with alpha reuse (verify.rs:86-98)
+    uint64_t acc = 0;
+    const uint64_t is_first = fe(q.is_first.value), is_last = fe(q.is_last.value);
+    for (auto& t : q.tapes) {
+      const uint64_t mv = fe(t.o[0].value), nmv = fe(t.o[1].value), flg = fe(t.o[2].value);
+      const uint64_t head = fe(t.o[4].value), nhead = fe(t.o[5].value);
+      acc = hgl_add(acc, hgl_mul(hgl_mul(a[0], flg), hgl_sub(flg, 1)));
+      acc = hgl_add(acc, hgl_mul(hgl_mul(hgl_mul(a[1], mv), hgl_sub(mv, 1)), hgl_add(mv, 1)));
+      acc = hgl_add(acc, hgl_mul(hgl_mul(a[2], hgl_sub(1, is_last)), hgl_sub(hgl_sub(nhead, head), nmv)));
+    }
+    for (auto& t : q.tapes) {
+      const uint64_t mv = fe(t.o[0].value), head = fe(t.o[4].value);
+      const uint64_t in_off = fe(t.o[7].value), out_off = fe(t.o[8].value);
+      acc = hgl_add(acc, hgl_mul(hgl_mul(a[2], is_first), hgl_sub(hgl_sub(head, mv), in_off)));
+      acc = hgl_add(acc, hgl_mul(hgl_mul(a[2], is_last), hgl_sub(head, out_off)));
+    }
+    ENSURE(acc == 0, "AIR composition non-zero at row " + std::to_string(q.row));
+  }
+
+  // FRI (fri.rs:130-222) on the transcript aligned with the prover
+  ENSURE(n_layers > 0, "no FRI roots");
+  tr.absorb("fri_layer_root", roots[0].data(), 32);
+  auto bb = tr.challenge("fri_betas", 8 * (n_layers - 1));
+  {
+    uint8_t fh[32];
+    leaf_u64(final_le, fh);
+    ENSURE(memcmp(fh, roots[n_layers - 1].data(), 32) == 0, "final FRI value mismatch with last root");
+  }
+  for (auto& f : fq) {
+    ENSURE(f.pos.size() == n_layers, "positions length mismatch");
+    ENSURE(f.pairs.size() == n_layers - 1, "pairs length mismatch");
+    uint64_t idx = f.pos[0];
+    uint64_t layer_len = 1ULL << (n_layers - 1);
+    for (size_t l = 0; l + 1 < n_layers; l++) {
+      const uint64_t half = layer_len / 2, j = idx ^ half;
+      const Pair& p = f.pairs[l];
+      uint8_t li[32], lj[32];
+      leaf_u64(p.vi, li);
+      leaf_u64(p.vj, lj);
+      bool ok = merkle_verify(roots[l].data(), li, idx, p.pi.data(), p.pi.size() / 32) &&
+                merkle_verify(roots[l].data(), lj, j, p.pj.data(), p.pj.size() / 32);
+      ENSURE(ok, "FRI Merkle path failed at layer " + std::to_string(l));
+      const uint64_t vi = fe(p.vi), vj = fe(p.vj), beta = rd64(bb.data() + 8 * l) % GL_P_HOST;
+      const uint64_t lower = idx < half ? vi : vj, upper = idx < half ? vj : vi;
+      const uint64_t vf = hgl_add(lower, hgl_mul(beta, upper));
+      ENSURE(f.pos[l + 1] == idx % half, "FRI index propagation failed at layer " + std::to_string(l));
+      if (l + 2 < n_layers) {
+        ENSURE(fe(f.pairs[l + 1].vi) == vf, "FRI fold mismatch at layer " + std::to_string(l));
+      } else {
+        uint8_t b[8];
+        for (int i = 0; i < 8; i++) b[i] = (uint8_t)(vf >> (8 * i));
+        ENSURE(memcmp(b, final_le, 8) == 0, "final FRI value mismatch");
+      }
+      idx %= half;
+      layer_len = half;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int32_t sezkp_stark_v1_verify(const uint8_t* proof_bytes, size_t len, const sezkp_block_view* blocks,
+                                         const uint8_t manifest_root[32], char* err, size_t err_len) {
+  try {
+    if (!proof_bytes) throw VErr{SEZKP_E_INVALID, "null proof"};
+    if (len >= 40 && manifest_root && memcmp(proof_bytes + len - 32, manifest_root, 32) != 0)
+      throw VErr{SEZKP_E_VERIFY, "manifest root mismatch"};
+    verify_v1(proof_bytes, len, blocks);
+    return SEZKP_OK;
+  } catch (const VErr& e) {
+    if (err && err_len) snprintf(err, err_len, "%s", e.msg.c_str());
+    return e.code;
+  } catch (const std::exception& e) {
+    if (err && err_len) snprintf(err, err_len, "%s", e.what());
+    return SEZKP_E_DECODE;
+  }
+}

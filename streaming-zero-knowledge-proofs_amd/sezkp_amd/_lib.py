@@ -1,0 +1,98 @@
+"""ctypes loader for the MI355X C ABI (include/sezkp_stark.h).
+
+The product path has no CPU fallback: if lib/libsezkp_stark.so is missing or
+fails to load, importing this module raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libsezkp_stark.so")
+
+SEZKP_OK = 0
+SEZKP_E_INVALID = -1
+SEZKP_E_DEVICE = -2
+SEZKP_E_NOMEM = -3
+SEZKP_E_DECODE = -4
+SEZKP_E_VERIFY = -5
+SEZKP_FLAG_STREAMING = 1
+
+# every symbol include/sezkp_stark.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "sezkp_abi_version", "sezkp_version", "sezkp_buf_free", "sezkp_stark_v1_prove",
+    "sezkp_stark_v1_prove_artifact_cbor", "sezkp_stark_v1_verify", "sezkp_ctx_create", "sezkp_ctx_destroy",
+    "sezkp_ctx_upload", "sezkp_ctx_prove", "sezkp_ctx_stage_times", "sezkp_ctx_stream", "sezkp_gl_ntt",
+    "sezkp_gl_coset_lde_deep", "sezkp_fri_fold_commit", "sezkp_merkle_root_u64", "sezkp_manifest_root",
+    "sezkp_blocks_decode_cbor", "sezkp_blocks_view", "sezkp_blocks_free", "sezkp_blake3",
+]
+
+
+class SezkpError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class Buf(C.Structure):
+    _fields_ = [("data", C.POINTER(C.c_uint8)), ("len", C.c_size_t)]
+
+
+VIEW_FIELDS = [
+    ("version", C.c_uint16), ("block_id", C.c_uint32), ("step_lo", C.c_uint64), ("step_hi", C.c_uint64),
+    ("ctrl_in", C.c_uint16), ("ctrl_out", C.c_uint16), ("in_head_in", C.c_int64), ("in_head_out", C.c_int64),
+    ("win_left", C.c_int64), ("win_right", C.c_int64), ("off_in", C.c_uint32), ("off_out", C.c_uint32),
+    ("step_start", C.c_uint64), ("input_mv", C.c_int8), ("mv", C.c_int8), ("has_write", C.c_uint8),
+    ("wsym", C.c_uint16),
+]
+
+
+class BlockView(C.Structure):
+    _fields_ = [("n_blocks", C.c_uint32), ("tau", C.c_uint32)] + [(f, C.POINTER(t)) for f, t in VIEW_FIELDS]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    L.sezkp_abi_version.restype = C.c_uint32
+    L.sezkp_version.restype = C.c_char_p
+    L.sezkp_buf_free.argtypes = [C.POINTER(Buf)]
+    E = [C.c_char_p, C.c_size_t]
+    L.sezkp_stark_v1_prove.argtypes = [C.POINTER(BlockView), C.c_char_p, C.c_uint32, C.POINTER(Buf), C.POINTER(Buf)] + E
+    L.sezkp_stark_v1_prove_artifact_cbor.argtypes = [C.POINTER(BlockView), C.c_char_p, C.c_uint32, C.POINTER(Buf)] + E
+    L.sezkp_stark_v1_verify.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(BlockView), C.c_char_p] + E
+    L.sezkp_ctx_create.restype = C.c_void_p
+    L.sezkp_ctx_create.argtypes = [C.c_int32] + E
+    L.sezkp_ctx_destroy.argtypes = [C.c_void_p]
+    L.sezkp_ctx_upload.argtypes = [C.c_void_p, C.POINTER(BlockView)] + E
+    L.sezkp_ctx_prove.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.POINTER(Buf)] + E
+    L.sezkp_ctx_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int32]
+    L.sezkp_ctx_stream.restype = C.c_void_p
+    L.sezkp_ctx_stream.argtypes = [C.c_void_p]
+    L.sezkp_gl_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p]
+    L.sezkp_gl_coset_lde_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.sezkp_fri_fold_commit.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_char_p, C.c_void_p]
+    L.sezkp_merkle_root_u64.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p, C.c_void_p]
+    L.sezkp_manifest_root.argtypes = [C.POINTER(BlockView), C.c_char_p]
+    L.sezkp_blocks_decode_cbor.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p)] + E
+    L.sezkp_blocks_view.restype = C.POINTER(BlockView)
+    L.sezkp_blocks_view.argtypes = [C.c_void_p]
+    L.sezkp_blocks_free.argtypes = [C.c_void_p]
+    L.sezkp_blake3.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+    return L
+
+
+lib = _load()
+
+
+def take_buf(b: Buf) -> bytes:
+    out = C.string_at(b.data, b.len) if b.len else b""
+    lib.sezkp_buf_free(C.byref(b))
+    return out
+
+
+def check(rc: int, err) -> None:
+    if rc != SEZKP_OK:
+        raise SezkpError(rc, err.value.decode(errors="replace"))

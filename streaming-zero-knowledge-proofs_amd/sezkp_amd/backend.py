@@ -1,0 +1,142 @@
+"""Host-side mirror of the reference's `ProvingBackend` for `StarkV1`
+(crates/sezkp-core/src/backend.rs:41-61, crates/sezkp-stark/src/lib.rs:126-190)
+over the MI355X C ABI. Same names, same argument meaning, same artifact
+(`ProofArtifact`, crates/sezkp-core/src/artifact.rs:55-68); errors raise
+`SezkpError` where the reference returns `anyhow::Error`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import struct
+from dataclasses import dataclass, field
+
+from ._lib import SEZKP_FLAG_STREAMING, Buf, SezkpError, check, lib, take_buf
+from .blocks import BlockSoA
+
+STAGES = ["expand", "col_commit", "col_outer", "compose", "intt", "lde_ntt", "deep", "layer0_tree",
+          "fri_fold_trees", "fri_paths", "col_openings", "total"]
+
+
+@dataclass
+class ProofArtifact:
+    backend: str
+    manifest_root: bytes
+    proof_bytes: bytes
+    meta: dict = field(default_factory=dict)
+
+    def to_cbor(self) -> bytes:
+        """ciborium encoding (io.rs:176-183): map{backend, manifest_root, proof_bytes, meta},
+        byte vectors as arrays of uints, meta keys sorted."""
+        out = bytearray(b"\xa4")
+        def text(s: str):
+            b = s.encode()
+            return _head(3, len(b)) + b
+        def barr(bs: bytes):
+            return _head(4, len(bs)) + b"".join(bytes([x]) if x < 24 else bytes([0x18, x]) for x in bs)
+        out += text("backend") + text(self.backend)
+        out += text("manifest_root") + barr(self.manifest_root)
+        out += text("proof_bytes") + barr(self.proof_bytes)
+        out += text("meta") + _head(5, len(self.meta))
+        for k in sorted(self.meta):
+            v = self.meta[k]
+            out += text(k) + (text(v) if isinstance(v, str) else _head(0, int(v)))
+        return bytes(out)
+
+
+def _head(major: int, v: int) -> bytes:
+    if v < 24:
+        return bytes([(major << 5) | v])
+    for nb, ai in ((1, 24), (2, 25), (4, 26), (8, 27)):
+        if v < 1 << (8 * nb):
+            return bytes([(major << 5) | ai]) + v.to_bytes(nb, "big")
+    raise ValueError(v)
+
+
+def _meta(proof: bytes, tau: int, streaming: bool) -> dict:
+    m = {"proto": "stark-v1", "domain_n": struct.unpack_from("<Q", proof, 0)[0], "tau": tau}
+    if streaming:
+        m["mode"] = "streaming"
+    return m
+
+
+class StarkV1:
+    """`impl ProvingBackend for StarkV1` on MI355X (stateless associated functions)."""
+
+    @staticmethod
+    def prove(blocks: BlockSoA, manifest_root: bytes) -> ProofArtifact:
+        return StarkV1._prove(blocks, manifest_root, False)
+
+    @staticmethod
+    def prove_streaming(blocks: BlockSoA, manifest_root: bytes) -> ProofArtifact:
+        """StarkV1::prove_streaming (lib.rs:170-190): same bytes, meta gains mode=streaming."""
+        return StarkV1._prove(blocks, manifest_root, True)
+
+    @staticmethod
+    def _prove(blocks: BlockSoA, manifest_root: bytes, streaming: bool) -> ProofArtifact:
+        if len(manifest_root) != 32:
+            raise SezkpError(-1, "manifest_root must be 32 bytes")
+        pb, mb = Buf(), Buf()
+        err = C.create_string_buffer(1024)
+        rc = lib.sezkp_stark_v1_prove(C.byref(blocks.view()), bytes(manifest_root),
+                                      SEZKP_FLAG_STREAMING if streaming else 0, C.byref(pb), C.byref(mb), err, 1024)
+        check(rc, err)
+        proof = take_buf(pb)
+        meta = json.loads(take_buf(mb).decode())
+        return ProofArtifact("stark", bytes(manifest_root), proof, meta)
+
+    @staticmethod
+    def verify(artifact: ProofArtifact, blocks: BlockSoA, manifest_root: bytes) -> None:
+        """StarkV1::verify (lib.rs:144-162 -> v1/verify.rs:60-196), host CPU."""
+        if artifact.backend != "stark":
+            raise SezkpError(-5, "backend kind mismatch: expected STARK")
+        if bytes(artifact.manifest_root) != bytes(manifest_root):
+            raise SezkpError(-5, "manifest root mismatch")
+        err = C.create_string_buffer(1024)
+        rc = lib.sezkp_stark_v1_verify(artifact.proof_bytes, len(artifact.proof_bytes), C.byref(blocks.view()),
+                                       bytes(manifest_root), err, 1024)
+        check(rc, err)
+
+
+class ProverContext:
+    """Resident-input prover: upload once (trace image in HBM), prove many times."""
+
+    def __init__(self, device: int = 0):
+        err = C.create_string_buffer(1024)
+        self._h = lib.sezkp_ctx_create(device, err, 1024)
+        if not self._h:
+            raise SezkpError(-2, err.value.decode())
+        self.tau = 0
+
+    def upload(self, blocks: BlockSoA) -> None:
+        err = C.create_string_buffer(1024)
+        check(lib.sezkp_ctx_upload(self._h, C.byref(blocks.view()), err, 1024), err)
+        self.tau = blocks.tau
+
+    def prove(self, manifest_root: bytes, streaming: bool = False) -> ProofArtifact:
+        pb = Buf()
+        err = C.create_string_buffer(1024)
+        check(lib.sezkp_ctx_prove(self._h, bytes(manifest_root), SEZKP_FLAG_STREAMING if streaming else 0,
+                                  C.byref(pb), err, 1024), err)
+        proof = take_buf(pb)
+        return ProofArtifact("stark", bytes(manifest_root), proof, _meta(proof, self.tau, streaming))
+
+    def stage_times_ms(self) -> dict:
+        buf = (C.c_double * 16)()
+        n = lib.sezkp_ctx_stage_times(self._h, buf, 16)
+        return {STAGES[i]: buf[i] for i in range(n)}
+
+    @property
+    def stream(self) -> int:
+        return lib.sezkp_ctx_stream(self._h) or 0
+
+    def close(self):
+        if self._h:
+            lib.sezkp_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,132 @@
+"""Block summaries as struct-of-arrays (the `sezkp_block_view` of the C ABI).
+
+`BlockSoA` mirrors `Vec<BlockSummary>` (crates/sezkp-core/src/types.rs:116-151).
+`simulate()` + `partition()` restate the input producer of the reference
+(`sezkp-cli simulate`: crates/sezkp-trace/src/generator.rs:38-73 and
+partition.rs:43-150) with numpy: same distributions (input/tape moves uniform
+in {-1,0,1}, writes with p=0.4 of a symbol in 0..=15) and the same partition
+semantics, but a numpy PCG64 stream instead of rand 0.9's ChaCha12 StdRng, so
+the traces are a deterministic stand-in, not the reference's exact bytes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import VIEW_FIELDS, BlockView, SezkpError, lib
+
+_NP = {C.c_uint16: np.uint16, C.c_uint32: np.uint32, C.c_uint64: np.uint64, C.c_int64: np.int64,
+       C.c_int8: np.int8, C.c_uint8: np.uint8}
+
+
+class BlockSoA:
+    """Struct-of-arrays block summaries; per-step tape arrays are step-major."""
+
+    def __init__(self, tau: int, **arrays):
+        self.tau = int(tau)
+        for f, t in VIEW_FIELDS:
+            setattr(self, f, np.ascontiguousarray(arrays[f], dtype=_NP[t]))
+        self.n_blocks = int(self.version.size)
+        self._view = None
+
+    # total trace rows n = sum(step_hi - step_lo + 1)
+    @property
+    def n_rows(self) -> int:
+        return int((self.step_hi - self.step_lo + 1).sum()) if self.n_blocks else 0
+
+    def view(self) -> BlockView:
+        v = BlockView()
+        v.n_blocks = self.n_blocks
+        v.tau = self.tau
+        for f, t in VIEW_FIELDS:
+            a = getattr(self, f)
+            if a.size == 0:  # keep a valid pointer for empty arrays
+                a = np.zeros(1, dtype=_NP[t])
+                setattr(self, "_empty_" + f, a)
+            setattr(v, f, a.ctypes.data_as(C.POINTER(t)))
+        self._view = v
+        return v
+
+    def manifest_root(self) -> bytes:
+        out = C.create_string_buffer(32)
+        lib.sezkp_manifest_root(C.byref(self.view()), out)
+        return out.raw
+
+    @classmethod
+    def from_cbor(cls, data: bytes) -> "BlockSoA":
+        """Decode CBOR Vec<BlockSummary> (crates/sezkp-core/src/io.rs:57-65) via the C ABI."""
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = lib.sezkp_blocks_decode_cbor(data, len(data), C.byref(h), err, 512)
+        if rc != 0:
+            raise SezkpError(rc, err.value.decode())
+        try:
+            v = lib.sezkp_blocks_view(h).contents
+            nb, tau = v.n_blocks, v.tau
+            counts = {"step_start": nb + 1}
+            arr = {}
+            base = {f: nb for f, _ in VIEW_FIELDS}
+            for f in ("win_left", "win_right", "off_in", "off_out"):
+                base[f] = nb * tau
+            step_start = np.ctypeslib.as_array(v.step_start, shape=(nb + 1,)).copy() if nb else np.zeros(1, np.uint64)
+            S = int(step_start[-1])
+            base.update(step_start=nb + 1, input_mv=S, mv=S * tau, has_write=S * tau, wsym=S * tau)
+            for f, t in VIEW_FIELDS:
+                cnt = base[f]
+                arr[f] = (np.ctypeslib.as_array(getattr(v, f), shape=(cnt,)).copy() if cnt
+                          else np.zeros(0, _NP[t]))
+            del counts
+            return cls(tau, **arr)
+        finally:
+            lib.sezkp_blocks_free(h)
+
+
+def simulate(t: int, tau: int, seed: int = 42):
+    """Synthetic trace (generator.rs:38-73 distribution): returns
+    (input_mv[t], mv[t,tau], has_write[t,tau], wsym[t,tau])."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    input_mv = rng.integers(-1, 2, size=t, dtype=np.int8)
+    has_write = (rng.random((t, tau)) < 0.4).astype(np.uint8)
+    wsym = rng.integers(0, 16, size=(t, tau), dtype=np.uint16) * has_write
+    mv = rng.integers(-1, 2, size=(t, tau), dtype=np.int8)
+    return input_mv, mv, has_write, wsym.astype(np.uint16)
+
+
+def partition(input_mv, mv, has_write, wsym, b: int) -> BlockSoA:
+    """partition_trace (partition.rs:43-150): contiguous blocks of b steps,
+    per-tape windows covering the post-move heads (relative, starting at 0)."""
+    t = int(input_mv.size)
+    tau = int(mv.shape[1]) if mv.ndim == 2 else 0
+    nb = (t + b - 1) // b
+    starts = np.arange(nb, dtype=np.int64) * b
+    ends = np.minimum(starts + b, t)
+    lens = ends - starts
+    gin = np.concatenate([[0], np.cumsum(input_mv.astype(np.int64))])
+    win_left = np.zeros((nb, tau), np.int64)
+    win_right = np.zeros((nb, tau), np.int64)
+    off_out = np.zeros((nb, tau), np.int64)
+    for k in range(nb):  # per block (vectorised over steps and tapes)
+        heads = np.cumsum(mv[starts[k]:ends[k]].astype(np.int64), axis=0)
+        lo = np.minimum(heads.min(axis=0), 0) if heads.size else np.zeros(tau, np.int64)
+        hi = np.maximum(heads.max(axis=0), 0) if heads.size else np.zeros(tau, np.int64)
+        win_left[k], win_right[k] = lo, hi
+        off_out[k] = (heads[-1] if heads.size else 0) - lo
+    off_in = -win_left
+    clamp = lambda x: np.where((x >= 0) & (x <= 0xFFFFFFFF), x, 0xFFFFFFFF).astype(np.uint32)
+    return BlockSoA(
+        tau,
+        version=np.ones(nb, np.uint16), block_id=np.arange(1, nb + 1, dtype=np.uint32),
+        step_lo=(starts + 1).astype(np.uint64), step_hi=ends.astype(np.uint64),
+        ctrl_in=np.zeros(nb, np.uint16), ctrl_out=np.zeros(nb, np.uint16),
+        in_head_in=gin[starts], in_head_out=gin[ends],
+        win_left=win_left.reshape(-1), win_right=win_right.reshape(-1),
+        off_in=clamp(off_in).reshape(-1), off_out=clamp(off_out).reshape(-1),
+        step_start=np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64),
+        input_mv=input_mv, mv=mv.reshape(-1), has_write=has_write.reshape(-1), wsym=wsym.reshape(-1),
+    )
+
+
+def synthetic_blocks(t: int, b: int = 512, tau: int = 8, seed: int = 42) -> BlockSoA:
+    """`sezkp-cli simulate --t T --b b --tau tau` stand-in (b = steps per block)."""
+    return partition(*simulate(t, tau, seed), b)

@@ -1,0 +1,44 @@
+"""Shared test setup: paths, the `gpu` marker, oracle/product handles.
+
+CPU tests (-m "not gpu") exercise the oracle against the reference fixtures,
+the host codec/ABI of the product, and the Python-vs-C oracle cross-check.
+GPU tests (-m gpu) are the parity tests proper: HIP path vs oracle through the
+C ABI.
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "streaming-zero-knowledge-proofs_amd")
+ORACLE = os.path.join(ROOT, "oracle")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (PKG, ORACLE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle_ctypes
+    oracle_ctypes.build()
+    return oracle_ctypes
+
+
+@pytest.fixture(scope="session")
+def product():
+    import sezkp_amd
+    return sezkp_amd
+
+
+@pytest.fixture(scope="session")
+def gpu_ok():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    return torch

@@ -1,0 +1,234 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle.
+
+Bit-exact equality is required everywhere (Goldilocks integer arithmetic and
+BLAKE3 bytes; there is no floating point on this path). Sizes are chosen so
+the single-threaded oracle finishes in seconds, plus one T=2^18 full prove
+(BASELINE config 3's size) and the 2^20 NTT round trip (config 2).
+"""
+import ctypes as C
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, PKG, ROOT
+
+pytestmark = pytest.mark.gpu
+P = 0xFFFFFFFF00000001
+FIXTURES = {
+    "root_blocks": ("tests/golden/ref_blocks.cbor", "tests/golden/ref_manifest.cbor"),
+    "minimal_riscv": ("tests/golden/riscv_blocks.cbor", "tests/golden/riscv_manifest.cbor"),
+}
+
+
+def _dev(torch, arr: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(arr).view(np.int64)).cuda()
+
+
+def _host(t) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("log_n", list(range(1, 13)) + [14, 16, 20])
+def test_ntt_roundtrip_matches_oracle(gpu_ok, product, oracle, log_n):
+    """ntt_roundtrip.rs:29-81 + exact forward values vs sezkp-ffts (config 2 at 2^20)."""
+    torch = gpu_ok
+    n = 1 << log_n
+    x = oracle.det_vec(n, 2024)
+    d = _dev(torch, x)
+    scratch = torch.empty_like(d)
+    assert product.lib.sezkp_gl_ntt(d.data_ptr(), scratch.data_ptr(), log_n, 1, None) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d), oracle.ntt_forward(x))
+    assert product.lib.sezkp_gl_ntt(d.data_ptr(), scratch.data_ptr(), log_n, -1, None) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d), x)
+
+
+@pytest.mark.parametrize("vec", ["zeros", "delta", "ap"])
+def test_ntt_special_vectors(gpu_ok, product, oracle, vec):
+    torch = gpu_ok
+    for log_n in (1, 5, 10):
+        n = 1 << log_n
+        x = {"zeros": np.zeros(n, np.uint64), "delta": np.eye(1, n, dtype=np.uint64)[0],
+             "ap": np.arange(n, dtype=np.uint64)}[vec]
+        d = _dev(torch, x)
+        s = torch.empty_like(d)
+        product.lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), log_n, 1, None)
+        product.lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), log_n, -1, None)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(_host(d), x)
+
+
+@pytest.mark.parametrize("log_n", [0, 1, 2, 3, 5, 8, 11, 13])
+def test_coset_lde_deep_matches_oracle(gpu_ok, product, oracle, log_n):
+    """lde.rs:42-97: INTT -> coset(3) NTT x8 -> DEEP divide."""
+    torch = gpu_ok
+    n = 1 << log_n
+    base = oracle.det_vec(n, 7 + log_n)
+    z = 0x1234567890ABCDEF % P
+    want = oracle.lde_deep(base, 3, z)
+    d_in = _dev(torch, base)
+    d_out = torch.empty(8 * n, dtype=torch.int64, device="cuda")
+    assert product.lib.sezkp_gl_coset_lde_deep(d_in.data_ptr(), log_n, 3, z, d_out.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d_out), want)
+
+
+@pytest.mark.parametrize("log_n", [0, 1, 2, 3, 6, 7, 10, 11, 15])
+def test_merkle_root_matches_oracle(gpu_ok, product, oracle, log_n):
+    """hash_field_leaves + MerkleTree::from_leaves (merkle.rs:46-71,150-160)."""
+    torch = gpu_ok
+    n = 1 << log_n
+    vals = oracle.det_vec(n, 99)
+    leaves = b"".join(oracle.hash_leaf_u64(int(v)) for v in vals)
+    d = _dev(torch, vals)
+    root = C.create_string_buffer(32)
+    assert product.lib.sezkp_merkle_root_u64(d.data_ptr(), n, root, None) == 0
+    assert root.raw == oracle.merkle_root(leaves)
+
+
+@pytest.mark.parametrize("log_out", [0, 1, 4, 10, 12])
+def test_fri_fold_commit_matches_oracle(gpu_ok, product, oracle, log_out):
+    """fold y'_i = y_i + beta*y_{i+h} (prover.rs:208-230) + its layer root."""
+    torch = gpu_ok
+    n = 1 << log_out
+    vals = oracle.det_vec(2 * n, 5)
+    beta = 0xDEADBEEFCAFEF00D % P
+    want = np.array([(int(vals[i]) + beta * int(vals[i + n])) % P for i in range(n)], dtype=np.uint64)
+    d_in = _dev(torch, vals)
+    d_out = torch.empty(n, dtype=torch.int64, device="cuda")
+    root = C.create_string_buffer(32)
+    assert product.lib.sezkp_fri_fold_commit(d_in.data_ptr(), n, beta, d_out.data_ptr(), root, None) == 0
+    np.testing.assert_array_equal(_host(d_out), want)
+    assert root.raw == oracle.merkle_root(b"".join(oracle.hash_leaf_u64(int(v)) for v in want))
+
+
+# ------------------------------------------------------------- full prove
+def _fixture(name):
+    import cbor_min
+    b, m = FIXTURES[name]
+    raw = open(os.path.join(ROOT, b), "rb").read()
+    man = cbor_min.loads(open(os.path.join(ROOT, m), "rb").read())
+    return raw, bytes(man["root"])
+
+
+@pytest.mark.parametrize("name", sorted(FIXTURES))
+def test_prove_reference_fixtures_bit_exact(gpu_ok, product, oracle, name):
+    """The reference's own committed block files: GPU proof == oracle proof ==
+    committed golden digest (tests/golden/v1_proofs.json)."""
+    raw, mroot = _fixture(name)
+    blocks = product.BlockSoA.from_cbor(raw)
+    art = product.StarkV1.prove(blocks, mroot)
+    want = oracle.prove_v1(blocks, mroot)
+    assert art.proof_bytes == want
+    gold = json.load(open(os.path.join(GOLDEN, "v1_proofs.json")))[name]
+    assert hashlib.sha256(art.proof_bytes).hexdigest() == gold["proof_sha256"]
+    assert art.meta == {"proto": "stark-v1", "domain_n": 8 * blocks.n_rows, "tau": blocks.tau}
+
+
+CASES = [  # (T, b, tau, seed)
+    (4096, 512, 8, 42),     # config 1 shape (CLI plumbing case)
+    (1024, 64, 2, 1),
+    (2048, 100, 3, 2),      # ragged last block
+    (256, 1, 1, 3),         # one-row blocks (first == last)
+    (8, 8, 2, 4),           # n < 1024: single short column chunk
+    (2, 2, 1, 5),
+    (1, 1, 1, 6),           # n = 1 -> N = 8
+    (512, 512, 0, 7),       # tau = 0: only the 3 scalar columns
+    (1 << 13, 8192, 4, 8),  # one block spanning many column chunks
+]
+
+
+@pytest.mark.parametrize("T,b,tau,seed", CASES)
+def test_prove_synthetic_bit_exact(gpu_ok, product, oracle, T, b, tau, seed):
+    blocks = product.synthetic_blocks(T, b, tau, seed)
+    mroot = blocks.manifest_root()
+    assert mroot == oracle.manifest_root(blocks)
+    art = product.StarkV1.prove(blocks, mroot)
+    assert art.proof_bytes == oracle.prove_v1(blocks, mroot)
+
+
+def test_prove_wide_values_bit_exact(gpu_ok, product, oracle):
+    """Edge values the domain allows: i8 moves outside {-1,0,1}, u16 symbols,
+    large/negative windows and offsets (AIR C2 and range terms non-zero)."""
+    rng = np.random.default_rng(11)
+    T, tau = 1024, 3
+    imv = rng.integers(-128, 128, T, dtype=np.int8)
+    mv = rng.integers(-128, 128, (T, tau), dtype=np.int8)
+    hw = (rng.random((T, tau)) < 0.7).astype(np.uint8)
+    ws = (rng.integers(0, 65536, (T, tau)) * hw).astype(np.uint16)
+    blocks = product.partition(imv, mv, hw, ws, 128)
+    blocks.win_left[:] = rng.integers(-(1 << 40), 1 << 40, blocks.win_left.size)
+    blocks.off_out[:] = 0xFFFFFFFF
+    mroot = bytes(range(32))
+    art = product.StarkV1.prove(blocks, mroot)
+    assert art.proof_bytes == oracle.prove_v1(blocks, mroot)
+
+
+def test_prove_rejects_bad_shapes(gpu_ok, product):
+    blocks = product.synthetic_blocks(96, 32, 2)  # n = 96, not a power of two
+    with pytest.raises(product.SezkpError, match="power of two"):
+        product.StarkV1.prove(blocks, bytes(32))
+    blocks = product.synthetic_blocks(64, 32, 2)
+    blocks.step_hi[0] += 1  # step count disagrees with step_lo/step_hi
+    with pytest.raises(product.SezkpError):
+        product.StarkV1.prove(blocks, bytes(32))
+
+
+def test_prove_full_size_config3(gpu_ok, product, oracle):
+    """T = 2^18 (BASELINE config 3 size, N = 2^21): bytes identical to the oracle."""
+    blocks = product.synthetic_blocks(1 << 18, 512, 8, 42)
+    mroot = blocks.manifest_root()
+    ctx = product.ProverContext(0)
+    ctx.upload(blocks)
+    art = ctx.prove(mroot)
+    assert art.proof_bytes == oracle.prove_v1(blocks, mroot)
+    again = ctx.prove(mroot)  # resident inputs: repeated proofs are deterministic
+    assert again.proof_bytes == art.proof_bytes
+
+
+def test_streaming_meta_and_verify(gpu_ok, product, oracle):
+    """prove_streaming: same bytes, meta gains mode; the host verifier accepts
+    proofs of a trace whose AIR holds (non-negative heads) and rejects tampering."""
+    rng = np.random.default_rng(3)
+    T, tau = 4096, 4
+    mv = rng.integers(0, 2, (T, tau), dtype=np.int8)  # heads never go left of 0
+    hw = (rng.random((T, tau)) < 0.4).astype(np.uint8)
+    ws = (rng.integers(0, 16, (T, tau)) * hw).astype(np.uint16)
+    blocks = product.partition(rng.integers(-1, 2, T, dtype=np.int8), mv, hw, ws, 512)
+    mroot = blocks.manifest_root()
+    a = product.StarkV1.prove(blocks, mroot)
+    s = product.StarkV1.prove_streaming(blocks, mroot)
+    assert s.proof_bytes == a.proof_bytes and s.meta["mode"] == "streaming"
+    product.StarkV1.verify(a, blocks, mroot)
+    bad = bytearray(a.proof_bytes)
+    bad[len(bad) // 2] ^= 1
+    with pytest.raises(product.SezkpError):
+        product.StarkV1.verify(product.ProofArtifact("stark", mroot, bytes(bad), a.meta), blocks, mroot)
+
+
+def test_cli_prove_verify_matches_oracle_artifact(gpu_ok, product, oracle, tmp_path):
+    """`sezkp-cli prove --backend stark` drop-in: CBOR artifact byte-identical
+    to the reference layout built from the oracle's proof bytes."""
+    import cbor_min
+    raw, mroot = _fixture("minimal_riscv")
+    bpath, mpath = tmp_path / "blocks.cbor", tmp_path / "manifest.cbor"
+    bpath.write_bytes(raw)
+    cli = os.path.join(PKG, "bin", "sezkp-cli")
+    subprocess.run([cli, "commit", "--blocks", str(bpath), "--out", str(mpath)], check=True)
+    assert bytes(cbor_min.loads(mpath.read_bytes())["root"]) == mroot
+    out = tmp_path / "proof.cbor"
+    r = subprocess.run([cli, "prove", "--backend", "stark", "--blocks", str(bpath), "--manifest", str(mpath),
+                        "--out", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    blocks = product.BlockSoA.from_cbor(raw)
+    want = cbor_min.proof_artifact_cbor("stark", mroot, oracle.prove_v1(blocks, mroot),
+                                        {"proto": "stark-v1", "domain_n": 8 * blocks.n_rows, "tau": blocks.tau})
+    assert out.read_bytes() == want
+    r = subprocess.run([cli, "prove", "--backend", "stark", "--blocks", str(tmp_path / "b.jsonl"), "--manifest",
+                        str(mpath), "--out", str(out)], capture_output=True, text=True)
+    assert r.returncode != 0
