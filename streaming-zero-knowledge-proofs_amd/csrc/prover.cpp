@@ -9,8 +9,10 @@
 //   [query indices] -> paths/openings.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -140,7 +142,18 @@ struct sezkp_ctx {
   TraceDev T{};
   std::vector<std::string> labels;
   ColTemplate* d_tmpl = nullptr;
+  uint32_t* d_tabs = nullptr;       // leaf tables + uniform-subtree tables
+  uint32_t* d_tab_cols = nullptr;
+  int n_tab_cols = 0;
+  uint64_t tab_units = 0;
+  uint32_t* d_work = nullptr;       // dense (column, chunk) work items
+  int n_work = 0;
+  uint32_t* d_pw_cols = nullptr;    // piecewise-constant columns
+  int n_pw_cols = 0;
+  uint32_t* d_pw_chunks = nullptr;  // chunks committed by the piecewise kernel
+  int n_pw_chunks = 0;
   uint32_t* d_outer = nullptr;
+  uint32_t* d_err = nullptr;  // device-side guard word: non-zero = a kernel saw an out-of-range index
   uint64_t outer_stride = 0;
   uint32_t* d_colroots = nullptr;
   uint64_t* d_base = nullptr;
@@ -283,8 +296,69 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     if (labels.back().size() > 44) throw Err{SEZKP_E_INVALID, "column label too long"};
     tm.push_back(make_template(c, tau, labels.back()));
   }
+  // per-column tables: leaf tables for small raw domains (i8/u8: 256, u16:
+  // 65536 entries) and uniform-subtree tables U_0..U_10 for piecewise columns
+  uint64_t tab_nodes = 0;
+  std::vector<uint32_t> tab_cols, pw_cols;
+  tab_units = 0;
+  for (int c = 0; c < ncols; c++) {
+    ColTemplate& t = tm[c];
+    t.tab = NO_TAB;
+    t.tab_log = 0;
+    if (kind_has_leaf_table(t.kind)) {
+      t.tab_log = t.kind == 5 ? 16 : 8;
+      t.tab = tab_nodes;
+      tab_nodes += 1ULL << t.tab_log;
+      tab_units = std::max<uint64_t>(tab_units, 1ULL << t.tab_log);
+      tab_cols.push_back(c);
+    } else if (kind_piecewise(t.kind)) {
+      const uint64_t units = (t.kind == 1 || t.kind == 2) ? 2 : nblk;
+      t.tab = tab_nodes;
+      tab_nodes += units * U_LEVELS;
+      tab_units = std::max<uint64_t>(tab_units, units);
+      tab_cols.push_back(c);
+      pw_cols.push_back(c);
+    }
+  }
+  // chunks whose rows cross few block boundaries go to the piecewise kernel;
+  // the rest (many short blocks) are committed densely for every column
+  const uint64_t nchunks = 1ULL << logChunks, chunk_rows = n < 1024 ? n : 1024;
+  std::vector<uint32_t> work, pw_chunks;
+  std::vector<uint8_t> dense_chunk(nchunks, 0);
+  {
+    uint32_t k = 0;
+    for (uint64_t ch = 0; ch < nchunks; ch++) {
+      const uint64_t c0 = ch * chunk_rows, c1 = c0 + chunk_rows;
+      while (k < nblk && v.step_start[k] <= c0) k++;
+      int inside = 0;
+      for (uint32_t j = k; j < nblk && v.step_start[j] < c1; j++)
+        if (j == 0 || v.step_start[j] != v.step_start[j - 1]) inside++;
+      if (inside <= 4) pw_chunks.push_back((uint32_t)ch);
+      else dense_chunk[ch] = 1;
+    }
+  }
+  for (int c = 0; c < ncols; c++) {
+    const bool pw = kind_piecewise(tm[c].kind);
+    for (uint64_t ch = 0; ch < nchunks; ch++)
+      if (!pw || dense_chunk[ch]) { work.push_back((uint32_t)c); work.push_back((uint32_t)ch); }
+  }
   d_tmpl = dalloc<ColTemplate>(ncols);
   up(d_tmpl, tm.data(), tm.size());
+  d_err = dalloc<uint32_t>(4);
+  HIP_OR_THROW(hipMemset(d_err, 0, 16));
+  d_tabs = dalloc<uint32_t>(tab_nodes * 8 + 8);
+  n_tab_cols = (int)tab_cols.size();
+  d_tab_cols = dalloc<uint32_t>(tab_cols.size() + 1);
+  up(d_tab_cols, tab_cols.data(), tab_cols.size());
+  n_pw_cols = (int)pw_cols.size();
+  d_pw_cols = dalloc<uint32_t>(pw_cols.size() + 1);
+  up(d_pw_cols, pw_cols.data(), pw_cols.size());
+  n_pw_chunks = (int)pw_chunks.size();
+  d_pw_chunks = dalloc<uint32_t>(pw_chunks.size() + 1);
+  up(d_pw_chunks, pw_chunks.data(), pw_chunks.size());
+  n_work = (int)(work.size() / 2);
+  d_work = dalloc<uint32_t>(work.size() + 2);
+  up(d_work, work.data(), work.size());
   outer_stride = tree_stored_nodes(logChunks, 0);
   d_outer = dalloc<uint32_t>((size_t)ncols * outer_stride * 8);
   d_colroots = dalloc<uint32_t>((size_t)ncols * 8);
@@ -329,7 +403,9 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
   HIP_OR_THROW(hipSetDevice(device));
   const int k = logN;
   auto rec = [&](int s) { HIP_OR_THROW(hipEventRecord(ev[s], st)); };
+  static const bool sync_debug = getenv("SEZKP_SYNC_DEBUG") != nullptr;  // name the failing kernel
   auto ok = [&](hipError_t e, const char* what) {
+    if (e == hipSuccess && sync_debug) e = hipStreamSynchronize(st);
     if (e != hipSuccess) throw Err{SEZKP_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
   };
 
@@ -337,13 +413,18 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
   // ---- column commitments (openings.rs:306-398)
   ok(launch_expand(st, T), "expand");
   rec(1);
-  ok(launch_col_commit(st, T, d_tmpl, ncols, d_outer, outer_stride, logChunks), "col_commit");
+  ok(launch_col_tables(st, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs), "col_tables");
+  ok(launch_col_commit(st, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
+  ok(launch_col_commit_pw(st, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
+                          outer_stride, d_err), "col_commit_pw");
   rec(2);
   TreeDev outer0{d_outer, d_colroots, logChunks, 0};
   ok(launch_tree_upper(st, &outer0, ncols, outer_stride, 8, 0), "col_outer");
   rec(3);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * ncols, d_err, 4, hipMemcpyDeviceToHost, st));
   HIP_OR_THROW(hipStreamSynchronize(st));
+  if (h_small[8 * ncols]) throw Err{SEZKP_E_DEVICE, "column commitment guard tripped (code " + std::to_string(h_small[8 * ncols]) + ")"};
   std::vector<uint8_t> colroots((uint8_t*)h_small, (uint8_t*)h_small + (size_t)ncols * 32);
 
   // ---- transcript prelude + column roots (prover.rs:67-81)

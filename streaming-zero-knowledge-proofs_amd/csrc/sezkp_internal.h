@@ -79,7 +79,19 @@ struct ColTemplate {
   uint32_t kind;       // 0 input_mv,1 is_first,2 is_last,3+k: per-tape kind k
   uint32_t tape;
   uint32_t off;        // byte offset of the value = 12 + len(label)
+  uint64_t tab;        // node offset of this column's leaf/uniform table, or NO_TAB
+  uint32_t tab_log;    // leaf table: log2(entries) (8 or 16); 0 otherwise
+  uint32_t pad;
 };
+constexpr uint64_t NO_TAB = ~0ULL;
+constexpr int U_LEVELS = 11;  // uniform-subtree hashes U_0..U_10 (chunk = 2^10 rows)
+
+// Column kinds whose leaf depends on a small raw domain (i8 / u8 / u16):
+// leaves come from a per-column table of all possible labelled leaves.
+__host__ __device__ inline bool kind_has_leaf_table(uint32_t kind) { return kind == 0 || kind == 3 || kind == 4 || kind == 5; }
+// Columns that are piecewise constant along the trace (per-block constants and
+// the block-boundary flags): committed from uniform-subtree hashes.
+__host__ __device__ inline bool kind_piecewise(uint32_t kind) { return kind == 1 || kind == 2 || kind >= 7; }
 
 constexpr int LSTORE_FRI = 6;
 constexpr int COL_CHUNK_LOG2 = 10;
@@ -88,8 +100,13 @@ constexpr int OPEN_REC_WORDS = 352;   // column opening record
 
 // kernels launched by the host orchestrator (prover.cpp)
 hipError_t launch_expand(hipStream_t st, const TraceDev& T);
-hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, int ncols,
-                             uint32_t* outer_nodes, uint64_t outer_stride_nodes, int logChunks);
+hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_tab_cols,
+                             int n_tab_cols, uint64_t tab_entries, uint32_t* tabs);
+hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_work,
+                             int nwork, const uint32_t* tabs, uint32_t* outer_nodes, uint64_t outer_stride_nodes);
+hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
+                                int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
+                                uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
                           const NttTables& tw, int logn, uint64_t* out);
 hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw);

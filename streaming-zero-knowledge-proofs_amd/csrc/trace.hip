@@ -180,10 +180,60 @@ __device__ __forceinline__ void hash4_labeled(const ColTemplate& ct, const uint6
   b3_parent(p0, p1, h);
 }
 
+// -------------------------------------------------------- column tables
+// grid (work/256, table columns). Leaf-table columns: entry e -> labelled leaf
+// of the raw value e (i8 reinterpreted, u8, u16). Piecewise columns: one lane
+// per run value computes U_0..U_10 with U_0 = leaf(v), U_{l+1} = H(U_l || U_l),
+// the root of a 2^l-row subtree whose rows all hold v.
+__global__ void __launch_bounds__(TR_THREADS) k_col_tables(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                           const uint32_t* __restrict__ cols, uint32_t* __restrict__ tabs) {
+  const ColTemplate ct = tmpl[cols[blockIdx.y]];
+  const uint64_t i = (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
+  uint32_t h[8];
+  if (kind_has_leaf_table(ct.kind)) {
+    if (i >= (1ULL << ct.tab_log)) return;
+    const uint64_t v = (ct.kind == 0 || ct.kind == 3) ? gl_from_i64((int8_t)(uint8_t)i) : i;
+    leaf_labeled_rt(ct, v, h);
+    node_store(tabs + 8 * (ct.tab + i), h);
+    return;
+  }
+  const uint64_t units = (ct.kind == 1 || ct.kind == 2) ? 2 : T.nblk;
+  if (i >= units) return;
+  uint64_t v;
+  if (ct.kind == 1 || ct.kind == 2) v = i;
+  else {
+    const uint64_t* tab = ct.kind == 7 ? T.blk_winlen : (ct.kind == 8 ? T.blk_offin : T.blk_offout);
+    v = tab[(uint64_t)ct.tape * T.nblk + i];
+  }
+  leaf_labeled_rt(ct, v, h);
+  uint32_t* o = tabs + 8 * (ct.tab + i * U_LEVELS);
+  node_store(o, h);
+  for (int l = 1; l < U_LEVELS; l++) {
+    b3_parent(h, h, h);
+    node_store(o + 8 * l, h);
+  }
+}
+
+// raw table index of 4 consecutive rows (leaf-table kinds)
+__device__ __forceinline__ void col_index4(const TraceDev& T, const ColTemplate& ct, uint64_t row0, uint32_t (&ix)[4]) {
+  const uint64_t o = (uint64_t)ct.tape * T.n + row0;
+  if (ct.kind == 5) {
+    uint2 w = *reinterpret_cast<const uint2*>(T.wsym + o);
+    ix[0] = w.x & 0xffff; ix[1] = w.x >> 16; ix[2] = w.y & 0xffff; ix[3] = w.y >> 16;
+    return;
+  }
+  const uint8_t* src = ct.kind == 0 ? reinterpret_cast<const uint8_t*>(T.input_mv) + row0
+                     : ct.kind == 3 ? reinterpret_cast<const uint8_t*>(T.mv) + o : T.wflag + o;
+  uint32_t w = *reinterpret_cast<const uint32_t*>(src);
+#pragma unroll
+  for (int j = 0; j < 4; j++) ix[j] = (w >> (8 * j)) & 0xff;
+}
+
 // -------------------------------------------------------- column commit
-// grid (n_chunks, ncols); one 256-lane WG per (chunk, column): 1024 rows,
-// 4 rows per lane folded to a level-2 node in registers, 8 LDS levels above.
-// Writes the chunk root as leaf `chunk` of the column's outer tree.
+// One 256-lane WG per work item (column, chunk): 1024 rows, 4 rows per lane
+// folded to a level-2 node in registers, 8 LDS levels above. Leaf-table
+// columns read their 4 leaves from the table (3 compressions per lane instead
+// of 7). Writes the chunk root as leaf `chunk` of the column's outer tree.
 template <int OFF>
 __device__ __forceinline__ void commit_body(const TraceDev& T, const ColTemplate& ct, uint64_t row0, uint32_t (&h)[8]) {
   uint64_t v[4];
@@ -192,10 +242,12 @@ __device__ __forceinline__ void commit_body(const TraceDev& T, const ColTemplate
 }
 
 __global__ void __launch_bounds__(TR_THREADS) k_col_commit(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                           const uint32_t* __restrict__ work,
+                                                           const uint32_t* __restrict__ tabs,
                                                            uint32_t* __restrict__ outer, uint64_t outer_stride) {
   __shared__ uint32_t lds[8][TR_THREADS];
-  const int c = blockIdx.y;
-  const uint64_t ch = blockIdx.x;
+  const int c = work[2 * blockIdx.x];
+  const uint64_t ch = work[2 * blockIdx.x + 1];
   const ColTemplate ct = tmpl[c];
   const int tid = threadIdx.x;
   const uint64_t n = T.n;
@@ -207,7 +259,18 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_commit(TraceDev T, const Col
   if (tid < nact) {
     const uint64_t row0 = (ch << COL_CHUNK_LOG2) + ((uint64_t)tid << logper);
     uint32_t h[8];
-    if (logper == 2) {
+    if (logper == 2 && kind_has_leaf_table(ct.kind)) {
+      uint32_t ix[4], a[8], b[8], p0[8], p1[8];
+      col_index4(T, ct, row0, ix);
+      const uint32_t* tb = tabs + 8 * ct.tab;
+      node_load(tb + 8 * ix[0], a);
+      node_load(tb + 8 * ix[1], b);
+      b3_parent(a, b, p0);
+      node_load(tb + 8 * ix[2], a);
+      node_load(tb + 8 * ix[3], b);
+      b3_parent(a, b, p1);
+      b3_parent(p0, p1, h);
+    } else if (logper == 2) {
       switch (ct.off) {
         case 16: commit_body<16>(T, ct, row0, h); break;
         case 17: commit_body<17>(T, ct, row0, h); break;
@@ -251,6 +314,100 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_commit(TraceDev T, const Col
     cnt = half;
   }
   if (tid < 8) outer[(uint64_t)c * outer_stride * 8 + ch * 8 + tid] = lds[tid][0];
+}
+
+// ------------------------------------------- piecewise-constant columns
+// One 64-lane WG per chunk, looping over the piecewise columns. A node covering
+// rows [a, a+2^l) is pure when its first and last rows lie in the same run
+// (same block; for is_first/is_last also the same flag value) and then equals
+// the uniform hash U_l(v); only nodes straddling a run boundary are hashed
+// from their children, and a node is evaluated only if its parent straddles
+// (or it is the chunk root).
+constexpr int PW_THREADS = 64;
+// run id of chunk-relative row r: rows in one run hold one value
+__device__ __forceinline__ uint32_t pw_run(uint32_t kind, const uint32_t* blk, const uint8_t* flg, int r) {
+  if (kind == 1) return blk[r] * 2u + (flg[r] & 1u);
+  if (kind == 2) return blk[r] * 2u + ((flg[r] >> 1) & 1u);
+  return blk[r];
+}
+// index of the run's value in the column's U table
+__device__ __forceinline__ uint32_t pw_uidx(uint32_t kind, const uint32_t* blk, const uint8_t* flg, int r) {
+  if (kind == 1) return flg[r] & 1u;
+  if (kind == 2) return (flg[r] >> 1) & 1u;
+  return blk[r];
+}
+__global__ void __launch_bounds__(PW_THREADS) k_col_commit_pw(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                              const uint32_t* __restrict__ pw_cols, int n_pw,
+                                                              const uint32_t* __restrict__ chunks,
+                                                              const uint32_t* __restrict__ tabs,
+                                                              uint32_t* __restrict__ outer, uint64_t outer_stride,
+                                                              uint32_t* __restrict__ err) {
+  __shared__ uint32_t blk[1024];
+  __shared__ uint8_t flg[1024];
+  __shared__ uint32_t slot[2][8][512];  // mixed nodes of the previous/current level (<= 512)
+  const int lane = threadIdx.x;
+  const uint64_t ch = chunks[blockIdx.x];
+  const uint64_t n = T.n;
+  const int cl = n < 1024 ? (int)n : 1024;
+  int logcl = 0;
+  while ((1 << logcl) < cl) logcl++;
+  const uint64_t c0 = ch << COL_CHUNK_LOG2;
+  for (int i = lane; i < cl; i += PW_THREADS) {
+    const uint32_t bk = T.row_blk[c0 + i];
+    blk[i] = bk < T.nblk ? bk : 0;
+    if (bk >= T.nblk) atomicOr(err, 1u);
+    flg[i] = T.row_flags[c0 + i];
+  }
+  __syncthreads();
+  for (int pc = 0; pc < n_pw; pc++) {
+    const uint32_t c = pw_cols[pc];
+    const uint32_t kind = tmpl[c].kind;
+    const uint64_t units = (kind == 1 || kind == 2) ? 2 : T.nblk;
+    const uint32_t* U = tabs + 8 * tmpl[c].tab;
+    // Only mixed nodes (first and last row in different runs) are hashed;
+    // a mixed node reads mixed children from the previous level's slots and
+    // looks pure children up as U_{l-1}(v). Rows (level 0) are always pure.
+    int cur = 0;
+    for (int l = 1; l <= logcl; l++) {
+      const int cnt = cl >> l;
+      for (int q = lane; q < cnt; q += PW_THREADS) {
+        const int a = q << l, e = a + (1 << l) - 1, m = a + (1 << (l - 1));
+        if (pw_run(kind, blk, flg, a) == pw_run(kind, blk, flg, e)) continue;
+        uint32_t x[8], y[8], h[8];
+        if (l > 1 && pw_run(kind, blk, flg, a) != pw_run(kind, blk, flg, m - 1)) {
+#pragma unroll
+          for (int w = 0; w < 8; w++) x[w] = slot[cur ^ 1][w][2 * q];
+        } else {
+          const uint64_t u = pw_uidx(kind, blk, flg, a);
+          node_load(U + 8 * (u * U_LEVELS + (l - 1)), x);
+        }
+        if (l > 1 && pw_run(kind, blk, flg, m) != pw_run(kind, blk, flg, e)) {
+#pragma unroll
+          for (int w = 0; w < 8; w++) y[w] = slot[cur ^ 1][w][2 * q + 1];
+        } else {
+          const uint64_t u = pw_uidx(kind, blk, flg, m);
+          node_load(U + 8 * (u * U_LEVELS + (l - 1)), y);
+        }
+        b3_parent(x, y, h);
+#pragma unroll
+        for (int w = 0; w < 8; w++) slot[cur][w][q] = h[w];
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+    if (lane < 8) {
+      uint32_t r;
+      if (pw_run(kind, blk, flg, 0) != pw_run(kind, blk, flg, cl - 1)) {
+        r = slot[cur ^ 1][lane][0];
+      } else {
+        const uint64_t u = pw_uidx(kind, blk, flg, 0);
+        if (u >= units) atomicOr(err, 2u);
+        r = U[8 * ((u < units ? u : 0) * U_LEVELS + logcl) + lane];
+      }
+      outer[(uint64_t)c * outer_stride * 8 + ch * 8 + lane] = r;
+    }
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------ composition
@@ -389,10 +546,26 @@ hipError_t launch_expand(hipStream_t st, const TraceDev& T) {
   hipLaunchKernelGGL(k_expand, dim3(T.nblk), dim3(TR_THREADS), 0, st, T);
   return hipGetLastError();
 }
-hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, int ncols,
-                             uint32_t* outer_nodes, uint64_t outer_stride_nodes, int logChunks) {
-  hipLaunchKernelGGL(k_col_commit, dim3((unsigned)(1ULL << logChunks), ncols), dim3(TR_THREADS), 0, st, T, d_tmpl,
-                     outer_nodes, outer_stride_nodes);
+hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_tab_cols,
+                             int n_tab_cols, uint64_t max_units, uint32_t* tabs) {
+  if (n_tab_cols == 0) return hipSuccess;
+  const unsigned gx = (unsigned)((max_units + TR_THREADS - 1) / TR_THREADS);
+  hipLaunchKernelGGL(k_col_tables, dim3(gx, n_tab_cols), dim3(TR_THREADS), 0, st, T, d_tmpl, d_tab_cols, tabs);
+  return hipGetLastError();
+}
+hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_work,
+                             int nwork, const uint32_t* tabs, uint32_t* outer_nodes, uint64_t outer_stride_nodes) {
+  if (nwork == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_col_commit, dim3(nwork), dim3(TR_THREADS), 0, st, T, d_tmpl, d_work, tabs, outer_nodes,
+                     outer_stride_nodes);
+  return hipGetLastError();
+}
+hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
+                                int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
+                                uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err) {
+  if (nchunks == 0 || n_pw_cols == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_col_commit_pw, dim3(nchunks), dim3(PW_THREADS), 0, st, T, d_tmpl, d_pw_cols, n_pw_cols,
+                     d_chunks, tabs, outer_nodes, outer_stride_nodes, d_err);
   return hipGetLastError();
 }
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
