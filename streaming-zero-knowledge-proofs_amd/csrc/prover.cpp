@@ -333,7 +333,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
       int inside = 0;
       for (uint32_t j = k; j < nblk && v.step_start[j] < c1; j++)
         if (j == 0 || v.step_start[j] != v.step_start[j - 1]) inside++;
-      if (inside <= 4) pw_chunks.push_back((uint32_t)ch);
+      if (inside <= 16) pw_chunks.push_back((uint32_t)ch);
       else dense_chunk[ch] = 1;
     }
   }

@@ -323,91 +323,76 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_commit(TraceDev T, const Col
 // the uniform hash U_l(v); only nodes straddling a run boundary are hashed
 // from their children, and a node is evaluated only if its parent straddles
 // (or it is the chunk root).
+// One lane per (piecewise column, chunk). The chunk's rows split into runs
+// of one value (a block's rows; for is_first/is_last the flagged row is a run
+// of its own); each run piece is cut into maximal aligned dyadic intervals
+// [a, a+2^l), whose subtree hash is the table entry U_l(v), and these are
+// pushed left to right on a Merkle stack that merges equal-level neighbours
+// (always siblings for aligned intervals) — the streaming builder of
+// fri_stream.rs:172-218 on pre-hashed uniform subtrees. Compressions per
+// chunk = merges = O(run boundaries x levels); the stack lives in LDS.
 constexpr int PW_THREADS = 64;
-// run id of chunk-relative row r: rows in one run hold one value
-__device__ __forceinline__ uint32_t pw_run(uint32_t kind, const uint32_t* blk, const uint8_t* flg, int r) {
-  if (kind == 1) return blk[r] * 2u + (flg[r] & 1u);
-  if (kind == 2) return blk[r] * 2u + ((flg[r] >> 1) & 1u);
-  return blk[r];
-}
-// index of the run's value in the column's U table
-__device__ __forceinline__ uint32_t pw_uidx(uint32_t kind, const uint32_t* blk, const uint8_t* flg, int r) {
-  if (kind == 1) return flg[r] & 1u;
-  if (kind == 2) return (flg[r] >> 1) & 1u;
-  return blk[r];
-}
+constexpr int PW_STACK = 12;
 __global__ void __launch_bounds__(PW_THREADS) k_col_commit_pw(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                               const uint32_t* __restrict__ pw_cols, int n_pw,
-                                                              const uint32_t* __restrict__ chunks,
+                                                              const uint32_t* __restrict__ chunks, int nchunks,
                                                               const uint32_t* __restrict__ tabs,
                                                               uint32_t* __restrict__ outer, uint64_t outer_stride,
                                                               uint32_t* __restrict__ err) {
-  __shared__ uint32_t blk[1024];
-  __shared__ uint8_t flg[1024];
-  __shared__ uint32_t slot[2][8][512];  // mixed nodes of the previous/current level (<= 512)
+  __shared__ uint32_t stk[PW_STACK][8][PW_THREADS];
   const int lane = threadIdx.x;
-  const uint64_t ch = chunks[blockIdx.x];
+  const uint64_t item = (uint64_t)blockIdx.x * PW_THREADS + lane;
+  if (item >= (uint64_t)n_pw * nchunks) return;
+  const uint32_t c = pw_cols[item % n_pw];
+  const uint64_t ch = chunks[item / n_pw];
+  const uint32_t kind = tmpl[c].kind;
+  const uint32_t* U = tabs + 8 * tmpl[c].tab;
   const uint64_t n = T.n;
-  const int cl = n < 1024 ? (int)n : 1024;
+  const uint64_t cl = n < 1024 ? n : 1024;
+  const uint64_t c0 = ch << COL_CHUNK_LOG2, c1 = c0 + cl;
   int logcl = 0;
-  while ((1 << logcl) < cl) logcl++;
-  const uint64_t c0 = ch << COL_CHUNK_LOG2;
-  for (int i = lane; i < cl; i += PW_THREADS) {
-    const uint32_t bk = T.row_blk[c0 + i];
-    blk[i] = bk < T.nblk ? bk : 0;
-    if (bk >= T.nblk) atomicOr(err, 1u);
-    flg[i] = T.row_flags[c0 + i];
-  }
-  __syncthreads();
-  for (int pc = 0; pc < n_pw; pc++) {
-    const uint32_t c = pw_cols[pc];
-    const uint32_t kind = tmpl[c].kind;
-    const uint64_t units = (kind == 1 || kind == 2) ? 2 : T.nblk;
-    const uint32_t* U = tabs + 8 * tmpl[c].tab;
-    // Only mixed nodes (first and last row in different runs) are hashed;
-    // a mixed node reads mixed children from the previous level's slots and
-    // looks pure children up as U_{l-1}(v). Rows (level 0) are always pure.
-    int cur = 0;
-    for (int l = 1; l <= logcl; l++) {
-      const int cnt = cl >> l;
-      for (int q = lane; q < cnt; q += PW_THREADS) {
-        const int a = q << l, e = a + (1 << l) - 1, m = a + (1 << (l - 1));
-        if (pw_run(kind, blk, flg, a) == pw_run(kind, blk, flg, e)) continue;
-        uint32_t x[8], y[8], h[8];
-        if (l > 1 && pw_run(kind, blk, flg, a) != pw_run(kind, blk, flg, m - 1)) {
+  while ((1ULL << logcl) < cl) logcl++;
+  uint64_t lvpack = 0;  // 4-bit level of each stack entry
+  int sp = 0;
+  uint32_t k = T.row_blk[c0];
+  uint64_t row = c0;
+  while (row < c1) {
+    if (k >= T.nblk) { atomicOr(err, 4u); return; }
+    const uint64_t bs = T.blk_start[k], be = T.blk_start[k + 1];
+    if (be <= row) { k++; continue; }  // empty or finished block
+    const uint64_t pe = be < c1 ? be : c1;
+    // sub-piece [row, cut) holding one value u (table index)
+    uint64_t cut = pe;
+    uint32_t u = k;
+    if (kind == 1) { u = row == bs ? 1u : 0u; cut = row == bs ? row + 1 : pe; }
+    else if (kind == 2) { u = row + 1 == be ? 1u : 0u; cut = (row + 1 < be && pe == be) ? be - 1 : pe; }
+    while (row < cut) {
+      const uint64_t off = row - c0, len = cut - row;
+      int l = off ? __builtin_ctzll(off) : logcl;
+      if (l > logcl) l = logcl;
+      while ((1ULL << l) > len) l--;
+      const uint64_t step = 1ULL << l;
+      uint32_t h[8];
+      node_load(U + 8 * ((uint64_t)u * U_LEVELS + l), h);
+      while (sp > 0 && (int)((lvpack >> (4 * (sp - 1))) & 15) == l) {  // merge with the left sibling
+        uint32_t left[8];
 #pragma unroll
-          for (int w = 0; w < 8; w++) x[w] = slot[cur ^ 1][w][2 * q];
-        } else {
-          const uint64_t u = pw_uidx(kind, blk, flg, a);
-          node_load(U + 8 * (u * U_LEVELS + (l - 1)), x);
-        }
-        if (l > 1 && pw_run(kind, blk, flg, m) != pw_run(kind, blk, flg, e)) {
-#pragma unroll
-          for (int w = 0; w < 8; w++) y[w] = slot[cur ^ 1][w][2 * q + 1];
-        } else {
-          const uint64_t u = pw_uidx(kind, blk, flg, m);
-          node_load(U + 8 * (u * U_LEVELS + (l - 1)), y);
-        }
-        b3_parent(x, y, h);
-#pragma unroll
-        for (int w = 0; w < 8; w++) slot[cur][w][q] = h[w];
+        for (int w = 0; w < 8; w++) left[w] = stk[sp - 1][w][lane];
+        b3_parent(left, h, h);
+        sp--;
+        l++;
       }
-      __syncthreads();
-      cur ^= 1;
+      if (sp >= PW_STACK) { atomicOr(err, 8u); return; }
+#pragma unroll
+      for (int w = 0; w < 8; w++) stk[sp][w][lane] = h[w];
+      lvpack = (lvpack & ~(15ULL << (4 * sp))) | ((uint64_t)l << (4 * sp));
+      sp++;
+      row += step;
     }
-    if (lane < 8) {
-      uint32_t r;
-      if (pw_run(kind, blk, flg, 0) != pw_run(kind, blk, flg, cl - 1)) {
-        r = slot[cur ^ 1][lane][0];
-      } else {
-        const uint64_t u = pw_uidx(kind, blk, flg, 0);
-        if (u >= units) atomicOr(err, 2u);
-        r = U[8 * ((u < units ? u : 0) * U_LEVELS + logcl) + lane];
-      }
-      outer[(uint64_t)c * outer_stride * 8 + ch * 8 + lane] = r;
-    }
-    __syncthreads();
   }
+  if (sp != 1) { atomicOr(err, 16u); return; }
+#pragma unroll
+  for (int w = 0; w < 8; w++) outer[(uint64_t)c * outer_stride * 8 + ch * 8 + w] = stk[0][w][lane];
 }
 
 // ------------------------------------------------------------ composition
@@ -564,8 +549,9 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err) {
   if (nchunks == 0 || n_pw_cols == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_col_commit_pw, dim3(nchunks), dim3(PW_THREADS), 0, st, T, d_tmpl, d_pw_cols, n_pw_cols,
-                     d_chunks, tabs, outer_nodes, outer_stride_nodes, d_err);
+  const uint64_t items = (uint64_t)n_pw_cols * nchunks;
+  hipLaunchKernelGGL(k_col_commit_pw, dim3((unsigned)((items + PW_THREADS - 1) / PW_THREADS)), dim3(PW_THREADS), 0, st,
+                     T, d_tmpl, d_pw_cols, n_pw_cols, d_chunks, nchunks, tabs, outer_nodes, outer_stride_nodes, d_err);
   return hipGetLastError();
 }
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
