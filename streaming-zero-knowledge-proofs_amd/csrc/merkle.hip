@@ -26,12 +26,14 @@ __device__ __forceinline__ void store_level(const TreeDev& T, int l, uint64_t id
   if (l == T.logLen) node_store(T.root, h);
 }
 
-// LDS image: words-major [8][256]; nodes 2i and 2i+1 of word w are one b64.
-__device__ __forceinline__ void lds_put(uint32_t (*lds)[MK_THREADS], int i, const uint32_t (&h)[8]) {
+// LDS image: words-major [8][W]; nodes 2i and 2i+1 of word w are one b64.
+template <int W>
+__device__ __forceinline__ void lds_put(uint32_t (*lds)[W], int i, const uint32_t (&h)[8]) {
 #pragma unroll
   for (int w = 0; w < 8; w++) lds[w][i] = h[w];
 }
-__device__ __forceinline__ void lds_pair(uint32_t (*lds)[MK_THREADS], int i, uint32_t (&l)[8], uint32_t (&r)[8]) {
+template <int W>
+__device__ __forceinline__ void lds_pair(uint32_t (*lds)[W], int i, uint32_t (&l)[8], uint32_t (&r)[8]) {
 #pragma unroll
   for (int w = 0; w < 8; w++) {
     uint2 p = *reinterpret_cast<const uint2*>(&lds[w][2 * i]);
@@ -42,7 +44,8 @@ __device__ __forceinline__ void lds_pair(uint32_t (*lds)[MK_THREADS], int i, uin
 
 // Reduce `cnt` level-`lvl` nodes in LDS to one; WG-local node i at level l has
 // global index wg * (cnt_at_l) + i.
-__device__ __forceinline__ void wg_reduce(uint32_t (*lds)[MK_THREADS], int cnt, int lvl, uint64_t wg, const TreeDev& T) {
+template <int W>
+__device__ __forceinline__ void wg_reduce(uint32_t (*lds)[W], int cnt, int lvl, uint64_t wg, const TreeDev& T) {
   const int tid = threadIdx.x;
   while (cnt > 1) {
     const int half = cnt >> 1;
@@ -206,15 +209,8 @@ __global__ void __launch_bounds__(MK_THREADS) k_leaf_subtree(const uint64_t* __r
 // ------------------------------------------------------------ upper levels
 // Input: stored level `from` (count 2^(logLen-from)); one WG reduces up to
 // 1024 nodes (4 per lane, 2 levels in registers) and stores every level.
-// grid.y indexes trees of identical shape spaced tree_stride nodes apart.
-__global__ void __launch_bounds__(MK_THREADS) k_tree_upper(TreeDev T0, uint64_t tree_stride, uint64_t root_stride,
-                                                           int from) {
-  __shared__ uint32_t lds[8][MK_THREADS];
-  TreeDev T = T0;
-  T.nodes += 8 * tree_stride * blockIdx.y;
-  T.root += root_stride * blockIdx.y;
+__device__ __forceinline__ void upper_wg(const TreeDev& T, int from, uint64_t wg, uint32_t (*lds)[MK_THREADS]) {
   const int tid = threadIdx.x;
-  const uint64_t wg = blockIdx.x;
   const int cnt_log = T.logLen - from;
   const int sub_log = cnt_log < 10 ? cnt_log : 10;
   const int logper = cnt_log < 2 ? cnt_log : 2;
@@ -249,6 +245,170 @@ __global__ void __launch_bounds__(MK_THREADS) k_tree_upper(TreeDev T0, uint64_t 
   }
   __syncthreads();
   wg_reduce(lds, nact, from + logper, wg, T);
+}
+
+// grid.y indexes trees of identical shape spaced tree_stride nodes apart.
+__global__ void __launch_bounds__(MK_THREADS) k_tree_upper(TreeDev T0, uint64_t tree_stride, uint64_t root_stride,
+                                                           int from) {
+  __shared__ uint32_t lds[8][MK_THREADS];
+  TreeDev T = T0;
+  T.nodes += 8 * tree_stride * blockIdx.y;
+  T.root += root_stride * blockIdx.y;
+  upper_wg(T, from, blockIdx.x, lds);
+}
+
+// One WG per job: trees of different shapes reduced in one launch.
+__global__ void __launch_bounds__(MK_THREADS) k_upper_jobs(const UpperJob* __restrict__ jobs) {
+  __shared__ uint32_t lds[8][MK_THREADS];
+  const UpperJob J = jobs[blockIdx.x];
+  upper_wg(J.tree, J.from, J.wg, lds);
+}
+
+// ------------------------------------------------- layers of >= 4096 leaves
+// Depth-first subtree over v[B .. B + 2^LV) held in registers (static
+// indices only); leaf i0 + j is global leaf index. Keeps at most LV pending
+// left siblings live, like a binary counter.
+template <int LV, int B>
+__device__ __forceinline__ void subtree_regs(const uint64_t (&v)[16], uint64_t i0, const TreeDev& T, uint32_t (&h)[8]) {
+  if constexpr (LV == 0) {
+    b3_leaf_u64(v[B], h);
+    store_level(T, 0, i0 + B, h);
+  } else {
+    uint32_t l[8];
+    subtree_regs<LV - 1, B>(v, i0, T, l);
+    subtree_regs<LV - 1, B + (1 << (LV - 1))>(v, i0, T, h);
+    b3_parent(l, h, h);
+    store_level(T, LV, (i0 + B) >> LV, h);
+  }
+}
+
+// One WG = 4096 leaves, 16 consecutive leaves per lane folded to a level-4
+// node in registers (binary counter: 31 compressions per lane, all lanes
+// busy), then levels 5..12 through LDS. fold == 1 computes the layer from the
+// previous one first (y'_i = in[i] + beta*in[i+len]) and writes it to out.
+// Levels above 12 are left to the upper-level jobs.
+__device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int logLen,
+                                           int fold, uint64_t beta, const TreeDev& T, uint64_t wg,
+                                           uint32_t (*lds)[MK_THREADS]) {
+  const int tid = threadIdx.x;
+  const uint64_t len = 1ULL << logLen;
+  const uint64_t i0 = (wg << L16_LOG) + ((uint64_t)tid << 4);
+  uint64_t v[16];
+  {
+    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(in + i0);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const ulonglong2 a = p[k];
+      v[2 * k] = a.x;
+      v[2 * k + 1] = a.y;
+    }
+  }
+  if (fold) {
+    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(in + i0 + len);
+    ulonglong2* o = reinterpret_cast<ulonglong2*>(out + i0);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const ulonglong2 b = q[k];
+      v[2 * k] = gl_add(v[2 * k], gl_mul(beta, b.x));
+      v[2 * k + 1] = gl_add(v[2 * k + 1], gl_mul(beta, b.y));
+      o[k] = make_ulonglong2(v[2 * k], v[2 * k + 1]);
+    }
+  }
+  uint32_t h[8];
+  subtree_regs<4, 0>(v, i0, T, h);
+  lds_put(lds, tid, h);
+  __syncthreads();
+  wg_reduce(lds, MK_THREADS, 4, wg, T);
+}
+
+__global__ void __launch_bounds__(MK_THREADS) k_layer16(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                        int logLen, int fold, uint64_t beta, TreeDev T) {
+  __shared__ uint32_t lds[8][MK_THREADS];
+  layer16_wg(in, out, logLen, fold, beta, T, blockIdx.x, lds);
+}
+
+// All fold layers of >= 4096 leaves hashed in one launch (their values were
+// produced by the fold chain first): the per-layer trees are independent, so
+// the small layers no longer serialize behind each other's latency.
+__global__ void __launch_bounds__(MK_THREADS) k_forest16(const ForestLayer* __restrict__ layers, int nlayers) {
+  __shared__ uint32_t lds[8][MK_THREADS];
+  int l = 0;
+  while (l + 1 < nlayers && layers[l + 1].wg_start <= blockIdx.x) l++;
+  const ForestLayer F = layers[l];
+  layer16_wg(F.vals, nullptr, F.tree.logLen, 0, 0, F.tree, blockIdx.x - F.wg_start, lds);
+}
+
+// FRI fold y'_i = y_i + beta * y_{i+len} (prover.rs:200-239), 4 per lane.
+__global__ void __launch_bounds__(MK_THREADS) k_fold(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                     int logLen, uint64_t beta) {
+  const uint64_t len = 1ULL << logLen;
+  const uint64_t i = ((uint64_t)blockIdx.x * MK_THREADS + threadIdx.x) * 4;
+  if (i >= len) return;
+  const ulonglong2* p = reinterpret_cast<const ulonglong2*>(in + i);
+  const ulonglong2* q = reinterpret_cast<const ulonglong2*>(in + i + len);
+  ulonglong2* o = reinterpret_cast<ulonglong2*>(out + i);
+  const ulonglong2 a0 = p[0], a1 = p[1], b0 = q[0], b1 = q[1];
+  o[0] = make_ulonglong2(gl_add(a0.x, gl_mul(beta, b0.x)), gl_add(a0.y, gl_mul(beta, b0.y)));
+  o[1] = make_ulonglong2(gl_add(a1.x, gl_mul(beta, b1.x)), gl_add(a1.y, gl_mul(beta, b1.y)));
+}
+
+// ------------------------------------------------------ small FRI layers
+// All fold layers of <= 2048 leaves in one launch: WG j produces layer
+// logLen = Ls - j. Each WG reloads the (<= 4096-element) layer above the
+// first tail layer into LDS and replays the fold chain down to its own layer
+// (a few thousand mulmods), so the trees of all small layers are built
+// concurrently instead of as a dependent chain of tiny launches.
+constexpr int TAIL_THREADS = 1024;
+__global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
+  __shared__ uint64_t buf[2 * TAIL_THREADS * 2];
+  __shared__ uint32_t lds[8][TAIL_THREADS];
+  const int tid = threadIdx.x;
+  const int j = blockIdx.x;
+  const int L = A.Ls - j;
+  int cur = A.Ls + 1;
+  for (int i = tid; i < (1 << cur); i += TAIL_THREADS) buf[i] = A.src[i];
+  __syncthreads();
+  uint64_t* vals = nullptr;
+  TreeDev T{};
+#pragma unroll
+  for (int s = 0; s < TAIL_MAX; s++) {
+    if (s <= j) {
+      const int half = 1 << (cur - 1);
+      for (int i = tid; i < half; i += TAIL_THREADS) buf[i] = gl_add(buf[i], gl_mul(A.beta[s], buf[i + half]));
+      __syncthreads();
+      cur--;
+    }
+    if (s == j) {
+      vals = A.vals[s];
+      T = A.tree[s];
+    }
+  }
+  const int len = 1 << L;
+  for (int i = tid; i < len; i += TAIL_THREADS) vals[i] = buf[i];
+  int nact, lvl;
+  if (L > 10) {  // 2048 leaves: two per lane
+    uint32_t a[8], b[8], h[8];
+    b3_leaf_u64(buf[2 * tid], a);
+    b3_leaf_u64(buf[2 * tid + 1], b);
+    store_level(T, 0, 2 * tid, a);
+    store_level(T, 0, 2 * tid + 1, b);
+    b3_parent(a, b, h);
+    store_level(T, 1, tid, h);
+    lds_put(lds, tid, h);
+    nact = TAIL_THREADS;
+    lvl = 1;
+  } else {
+    if (tid < len) {
+      uint32_t h[8];
+      b3_leaf_u64(buf[tid], h);
+      store_level(T, 0, tid, h);
+      lds_put(lds, tid, h);
+    }
+    nact = len;
+    lvl = 0;
+  }
+  __syncthreads();
+  wg_reduce(lds, nact, lvl, 0, T);
 }
 
 // ---------------------------------------------------------- path extraction
@@ -315,6 +475,12 @@ hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const 
 
 hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold,
                                uint64_t beta, TreeDev tree) {
+  if (logLen >= L16_LOG) {
+    hipError_t e = launch_layer16(st, in, out_vals, logLen, fold, beta, tree);
+    if (e != hipSuccess) return e;
+    if (logLen == L16_LOG) return hipSuccess;  // the single WG wrote the root
+    return launch_tree_upper(st, &tree, 1, 0, 0, L16_LOG);
+  }
   const int sub_log = logLen < 10 ? logLen : 10;
   const unsigned grid = (unsigned)(1ULL << (logLen - sub_log));
   hipLaunchKernelGGL(k_leaf_subtree, dim3(grid), dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, tree);
@@ -331,6 +497,52 @@ hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out
     from += step;
   }
   return hipSuccess;
+}
+
+hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
+                          TreeDev tree) {
+  if (logLen < L16_LOG) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_layer16, dim3((unsigned)(1ULL << (logLen - L16_LOG))), dim3(MK_THREADS), 0, st, in, out_vals,
+                     logLen, fold, beta, tree);
+  return hipGetLastError();
+}
+
+hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta) {
+  if (logLen < 2) return hipErrorInvalidValue;
+  const uint64_t per = (uint64_t)MK_THREADS * 4;
+  const unsigned grid = (unsigned)(((1ULL << logLen) + per - 1) / per);
+  hipLaunchKernelGGL(k_fold, dim3(grid), dim3(MK_THREADS), 0, st, in, out, logLen, beta);
+  return hipGetLastError();
+}
+
+hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs) {
+  if (nlayers <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_forest16, dim3(total_wgs), dim3(MK_THREADS), 0, st, d_layers, nlayers);
+  return hipGetLastError();
+}
+
+hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a) {
+  if (a.Ls < 0 || a.Ls >= TAIL_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fri_tail, dim3((unsigned)(a.Ls + 1)), dim3(TAIL_THREADS), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_upper_jobs(hipStream_t st, const UpperJob* d_jobs, int njobs) {
+  if (njobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_upper_jobs, dim3((unsigned)njobs), dim3(MK_THREADS), 0, st, d_jobs);
+  return hipGetLastError();
+}
+
+void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes) {
+  int p = 0;
+  while (from < T.logLen) {
+    const int c = T.logLen - from;
+    const int step = c < 10 ? c : 10;
+    if ((int)passes.size() <= p) passes.resize(p + 1);
+    for (uint64_t w = 0; w < (1ULL << (c - step)); w++) passes[p].push_back(UpperJob{T, from, (uint32_t)w, 0});
+    from += step;
+    p++;
+  }
 }
 
 hipError_t launch_tree_upper(hipStream_t st, TreeDev* trees, int ntrees, uint64_t tree_stride_nodes,

@@ -131,6 +131,8 @@ int ilog2(uint64_t x) {
 struct sezkp_ctx {
   int device = 0;
   hipStream_t st = nullptr;
+  hipStream_t st2 = nullptr;  // side stream: small FRI layers overlap the forest
+  hipEvent_t ev_fold = nullptr, ev_tail = nullptr;
   NttTables tw{};
   std::vector<void*> dev_allocs;
   std::vector<void*> host_allocs;
@@ -162,6 +164,11 @@ struct sezkp_ctx {
   std::vector<TreeDev> trees;
   uint32_t* d_roots = nullptr;
   FriLayerDev* d_layers = nullptr;
+  ForestLayer* d_forest = nullptr;
+  int n_forest = 0;
+  uint32_t forest_wgs = 0;
+  UpperJob* d_jobs = nullptr;  // upper-level passes: layer 0, then all fold layers
+  std::vector<std::pair<size_t, int>> jobs0, jobsF;
   uint32_t* d_req = nullptr;
   uint32_t* d_fri_out = nullptr;
   uint32_t* d_open_out = nullptr;
@@ -200,7 +207,11 @@ struct sezkp_ctx {
     free_all();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    if (st2) (void)hipStreamSynchronize(st2);
+    if (ev_fold) (void)hipEventDestroy(ev_fold);
+    if (ev_tail) (void)hipEventDestroy(ev_tail);
     if (st) (void)hipStreamDestroy(st);
+    if (st2) (void)hipStreamDestroy(st2);
   }
 
   void upload(const sezkp_block_view& v);
@@ -386,6 +397,33 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   }
   d_layers = dalloc<FriLayerDev>(k + 1);
   up(d_layers, ly.data(), ly.size());
+  // forest of fold-layer trees with >= 4096 leaves (layers 1 .. k-12)
+  {
+    std::vector<ForestLayer> fl;
+    uint32_t wgs = 0;
+    for (int r = 1; r <= k && k - r >= L16_LOG; r++) {
+      fl.push_back(ForestLayer{ly[r].vals, trees[r], wgs, 0});
+      wgs += (uint32_t)(1ULL << (k - r - L16_LOG));
+    }
+    n_forest = (int)fl.size();
+    forest_wgs = wgs;
+    d_forest = dalloc<ForestLayer>(fl.size() + 1);
+    if (!fl.empty()) up(d_forest, fl.data(), fl.size());
+  }
+  // upper levels (> 12) of the layers built by the 16-leaves-per-lane kernel
+  {
+    std::vector<std::vector<UpperJob>> p0, pF;
+    if (k > L16_LOG) plan_upper_jobs(trees[0], L16_LOG, p0);
+    for (int r = 1; r <= k; r++)
+      if (k - r > L16_LOG) plan_upper_jobs(trees[r], L16_LOG, pF);
+    std::vector<UpperJob> all;
+    jobs0.clear();
+    jobsF.clear();
+    for (auto& v : p0) { jobs0.push_back({all.size(), (int)v.size()}); all.insert(all.end(), v.begin(), v.end()); }
+    for (auto& v : pF) { jobsF.push_back({all.size(), (int)v.size()}); all.insert(all.end(), v.begin(), v.end()); }
+    d_jobs = dalloc<UpperJob>(all.size() + 1);
+    if (!all.empty()) up(d_jobs, all.data(), all.size());
+  }
   max_fri_req = (size_t)NUM_QUERIES * 2 * k;
   max_open_req = (size_t)NUM_QUERIES * (3 + 9 * tau);
   d_req = dalloc<uint32_t>(max_fri_req * 2 + max_open_req * 3);
@@ -465,7 +503,12 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
   rec(6);
   ok(launch_deep(st, d_lde, logN, z, tw), "deep");
   rec(7);
-  ok(launch_leaf_subtree(st, d_lde, nullptr, logN, 0, 0, trees[0]), "layer0_tree");
+  if (logN >= L16_LOG) {
+    ok(launch_layer16(st, d_lde, nullptr, logN, 0, 0, trees[0]), "layer0_tree");
+    for (auto& p : jobs0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_upper");
+  } else {
+    ok(launch_leaf_subtree(st, d_lde, nullptr, logN, 0, 0, trees[0]), "layer0_tree");
+  }
   rec(8);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
   HIP_OR_THROW(hipStreamSynchronize(st));
@@ -475,12 +518,29 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
 
   // ---- FRI folds + layer trees (prover.rs:192-239)
   auto bb = tr.challenge("fri_betas", 8 * (size_t)k);
-  for (int r = 0; r < k; r++) {
+  auto layer_vals = [&](int r) { return r == 0 ? d_lde : d_fri + (N - (N >> (r - 1))); };
+  const int r1 = k > L16_LOG ? k - L16_LOG : 0;  // first fold producing a layer of <= 2^11 leaves
+  for (int r = 0; r < r1; r++) {  // fold chain of the big layers (values only)
     const uint64_t beta = rd64(bb.data() + 8 * r) % GL_P_HOST;
-    const uint64_t* in = r == 0 ? d_lde : d_fri + (N - (N >> (r - 1)));
-    uint64_t* out = d_fri + (N - (N >> r));
-    ok(launch_leaf_subtree(st, in, out, logN - r - 1, 1, beta, trees[r + 1]), "fri_fold");
+    ok(launch_fold(st, layer_vals(r), layer_vals(r + 1), logN - r - 1, beta), "fri_fold");
   }
+  {  // layers of <= 2^11 leaves on the side stream, concurrent with the forest
+    TailArgs ta{};
+    ta.src = layer_vals(r1);
+    ta.Ls = logN - r1 - 1;
+    for (int j = 0; j <= ta.Ls; j++) {
+      ta.beta[j] = rd64(bb.data() + 8 * (r1 + j)) % GL_P_HOST;
+      ta.vals[j] = layer_vals(r1 + 1 + j);
+      ta.tree[j] = trees[r1 + 1 + j];
+    }
+    HIP_OR_THROW(hipEventRecord(ev_fold, st));
+    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+    ok(launch_fri_tail(st2, ta), "fri_tail");
+    HIP_OR_THROW(hipEventRecord(ev_tail, st2));
+  }
+  ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
+  HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
+  for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
   rec(9);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
   HIP_OR_THROW(hipStreamSynchronize(st));
@@ -650,6 +710,9 @@ sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len) {
     HIP_OR_THROW(hipSetDevice(device));
     HIP_OR_THROW(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto& e : c->ev) HIP_OR_THROW(hipEventCreate(&e));
+    HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+    HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
+    HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     c->tw = tables_for_device(device);
     return c.release();
   } catch (const Err& e) {

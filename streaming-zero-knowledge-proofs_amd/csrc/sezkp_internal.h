@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace sezkp {
 
 // w_{2^K}^e = hi[e >> S] * lo[e & (2^S - 1)]; p3_* likewise for 3^e.
@@ -118,6 +120,40 @@ struct FriLayerDev {
   const uint64_t* vals;
   TreeDev tree;
 };
+// Upper-level reduction job: one WG reduces <= 1024 stored nodes of `tree`
+// from level `from` (WG index wg within that level).
+struct UpperJob {
+  TreeDev tree;
+  int from;
+  uint32_t wg;
+  uint64_t pad;
+};
+void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes);
+hipError_t launch_upper_jobs(hipStream_t st, const UpperJob* d_jobs, int njobs);
+
+constexpr int L16_LOG = 12;  // leaves per WG of the 16-leaves-per-lane layer kernel
+hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
+                          TreeDev tree);
+// Fold chain kernel (values only) and the one-launch forest of layer trees.
+hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta);
+struct ForestLayer {
+  const uint64_t* vals;
+  TreeDev tree;
+  uint32_t wg_start;  // first WG of this layer in the forest launch
+  uint32_t pad;
+};
+hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs);
+// Small FRI layers (logLen <= Ls <= 11) in one launch; layer Ls - j is
+// folded from layer Ls - j + 1 with beta[j]; src = layer Ls + 1.
+constexpr int TAIL_MAX = 12;
+struct TailArgs {
+  const uint64_t* src;
+  int Ls;
+  uint64_t beta[TAIL_MAX];
+  uint64_t* vals[TAIL_MAX];
+  TreeDev tree[TAIL_MAX];
+};
+hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a);
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
                             uint32_t* d_out);
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
