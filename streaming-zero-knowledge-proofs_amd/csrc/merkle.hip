@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
 // One 64-lane workgroup per (layer, index): recompute the 64-leaf group that
 // holds the index (levels < lstore), then read stored siblings above.
 __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict__ layers, const uint32_t* __restrict__ req,
-                                                  uint32_t* __restrict__ out) {
+                                                  ProofLayout P, const uint64_t* __restrict__ final_val) {
   __shared__ uint32_t lds[8][64];
   const int lane = threadIdx.x;
   const uint32_t q = blockIdx.x;
@@ -427,13 +427,40 @@ __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict_
   const int glog = L < T.lstore ? L : T.lstore;
   const uint64_t g = 1ULL << glog;
   const uint64_t base = idx & ~(g - 1);
-  uint32_t* o = out + (uint64_t)q * PATH_REC_WORDS;
+  // FriQuery (proof.rs:68-78): positions then k pairs of (value, path) records
+  const int k = P.k;
+  const uint32_t qi = q / (2 * k), side = q & 1;
+  uint32_t* fq = P.base + (P.fq_off + 8 + (uint64_t)qi * P.fq_bytes) / 4;
+  const uint64_t off_r = 2 * (16 * (uint64_t)r + 32 * ((uint64_t)r * k - (uint64_t)r * (r - 1) / 2));
+  uint32_t* o = fq + (8 + 8 * (uint64_t)(k + 1) + 8 + off_r + side * (16 + 32 * (uint64_t)L)) / 4;
   if (lane == 0) {
-    uint64_t v = Ly.vals[idx];
+    const uint64_t v = Ly.vals[idx];
     o[0] = (uint32_t)v;
     o[1] = (uint32_t)(v >> 32);
-    o[2] = 0;
+    o[2] = (uint32_t)L;
     o[3] = 0;
+    if (r == 0 && side == 0) {  // query header: k+1 positions (prover.rs:390-393)
+      fq[0] = (uint32_t)(k + 1);
+      fq[1] = 0;
+      uint64_t p = idx, len = 1ULL << k;
+      for (int j = 0; j <= k; j++) {
+        fq[2 + 2 * j] = (uint32_t)p;
+        fq[3 + 2 * j] = (uint32_t)(p >> 32);
+        len >>= 1;
+        if (len) p %= len;
+      }
+      fq[2 + 2 * (k + 1)] = (uint32_t)k;
+      fq[3 + 2 * (k + 1)] = 0;
+    }
+    if (q == 0) {
+      uint32_t* f0 = P.base + P.fq_off / 4;
+      f0[0] = P.nq;
+      f0[1] = 0;
+      uint32_t* t = P.base + P.tail_off / 4;
+      const uint64_t fv = *final_val;
+      t[0] = (uint32_t)fv;
+      t[1] = (uint32_t)(fv >> 32);
+    }
   }
   if (lane < (int)g) {
     uint32_t h[8];
@@ -567,9 +594,10 @@ hipError_t launch_tree_upper(hipStream_t st, TreeDev* trees, int ntrees, uint64_
 }
 
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
-                            uint32_t* d_out) {
+                            const ProofLayout& P, const uint64_t* final_val) {
   if (nreq == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fri_paths, dim3(nreq), dim3(64), 0, st, d_layers, d_req, d_out);
+  if ((uint64_t)nreq != (uint64_t)P.nq * 2 * P.k) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fri_paths, dim3(nreq), dim3(64), 0, st, d_layers, d_req, P, final_val);
   return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -154,6 +155,11 @@ struct sezkp_ctx {
   int n_pw_cols = 0;
   uint32_t* d_pw_chunks = nullptr;  // chunks committed by the piecewise kernel
   int n_pw_chunks = 0;
+  DictCol* d_dcols = nullptr;       // dense small-range columns (dictionary commitment)
+  int n_dict = 0;
+  int64_t* d_dpart = nullptr;
+  DictPlan* d_dplans = nullptr;
+  uint32_t* d_dtabs = nullptr;
   uint32_t* d_outer = nullptr;
   uint32_t* d_err = nullptr;  // device-side guard word: non-zero = a kernel saw an out-of-range index
   uint64_t outer_stride = 0;
@@ -170,15 +176,18 @@ struct sezkp_ctx {
   UpperJob* d_jobs = nullptr;  // upper-level passes: layer 0, then all fold layers
   std::vector<std::pair<size_t, int>> jobs0, jobsF;
   uint32_t* d_req = nullptr;
-  uint32_t* d_fri_out = nullptr;
-  uint32_t* d_open_out = nullptr;
   uint32_t* h_req = nullptr;
-  uint32_t* h_fri_out = nullptr;
-  uint32_t* h_open_out = nullptr;
+  ProofLayout PL{};             // device proof body (after the column-root header)
+  size_t hdr_bytes = 0;         // bincode header: domain_n, tau, col_roots
+  std::vector<size_t> root_pos; // byte offset of each column root in the header
+  uint8_t* h_proof = nullptr;   // pinned: header + body
   uint32_t* h_small = nullptr;  // col roots / fri roots staging
   size_t max_fri_req = 0, max_open_req = 0;
   hipEvent_t ev[ST_NSTAGE + 1]{};
   double stage_ms[ST_NSTAGE + 1]{};
+  // host-side split of one prove(): wall, time blocked in stream syncs,
+  // final D2H wait, proof serialization (after the last sync)
+  double host_ms[4]{};
   bool have_times = false;
 
   template <class Tp>
@@ -215,7 +224,8 @@ struct sezkp_ctx {
   }
 
   void upload(const sezkp_block_view& v);
-  std::vector<uint8_t> prove(const uint8_t root[32]);
+  // proves into the pinned staging buffer; returns its size (bytes at h_proof)
+  size_t prove(const uint8_t root[32]);
 };
 
 void sezkp_ctx::upload(const sezkp_block_view& v) {
@@ -311,12 +321,16 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   // 65536 entries) and uniform-subtree tables U_0..U_10 for piecewise columns
   uint64_t tab_nodes = 0;
   std::vector<uint32_t> tab_cols, pw_cols;
+  std::vector<DictCol> dcols;
+  const bool use_dict = n >= (1ULL << COL_CHUNK_LOG2) && getenv("SEZKP_NO_DICT") == nullptr;
   tab_units = 0;
   for (int c = 0; c < ncols; c++) {
     ColTemplate& t = tm[c];
     t.tab = NO_TAB;
     t.tab_log = 0;
-    if (kind_has_leaf_table(t.kind)) {
+    if (use_dict && kind_dict(t.kind)) {
+      dcols.push_back(DictCol{(uint32_t)c, 0, (uint64_t)dcols.size() * DICT_LEVELS * DICT_CAP});
+    } else if (kind_has_leaf_table(t.kind)) {
       t.tab_log = t.kind == 5 ? 16 : 8;
       t.tab = tab_nodes;
       tab_nodes += 1ULL << t.tab_log;
@@ -349,6 +363,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     }
   }
   for (int c = 0; c < ncols; c++) {
+    if (use_dict && kind_dict(tm[c].kind)) continue;
     const bool pw = kind_piecewise(tm[c].kind);
     for (uint64_t ch = 0; ch < nchunks; ch++)
       if (!pw || dense_chunk[ch]) { work.push_back((uint32_t)c); work.push_back((uint32_t)ch); }
@@ -361,6 +376,12 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   n_tab_cols = (int)tab_cols.size();
   d_tab_cols = dalloc<uint32_t>(tab_cols.size() + 1);
   up(d_tab_cols, tab_cols.data(), tab_cols.size());
+  n_dict = (int)dcols.size();
+  d_dcols = dalloc<DictCol>(dcols.size() + 1);
+  up(d_dcols, dcols.data(), dcols.size());
+  d_dpart = dalloc<int64_t>(2 * dcols.size() * ((n + 4095) / 4096) + 2);
+  d_dplans = dalloc<DictPlan>(dcols.size() + 1);
+  d_dtabs = dalloc<uint32_t>(dcols.size() * DICT_LEVELS * DICT_CAP * 8 + 8);
   n_pw_cols = (int)pw_cols.size();
   d_pw_cols = dalloc<uint32_t>(pw_cols.size() + 1);
   up(d_pw_cols, pw_cols.data(), pw_cols.size());
@@ -427,17 +448,53 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   max_fri_req = (size_t)NUM_QUERIES * 2 * k;
   max_open_req = (size_t)NUM_QUERIES * (3 + 9 * tau);
   d_req = dalloc<uint32_t>(max_fri_req * 2 + max_open_req * 3);
-  d_fri_out = dalloc<uint32_t>(max_fri_req * PATH_REC_WORDS);
-  d_open_out = dalloc<uint32_t>(max_open_req * OPEN_REC_WORDS);
   h_req = halloc<uint32_t>(max_fri_req * 2 + max_open_req * 3);
-  h_fri_out = halloc<uint32_t>(max_fri_req * PATH_REC_WORDS);
-  h_open_out = halloc<uint32_t>(max_open_req * OPEN_REC_WORDS);
+  // ---- proof layout (proof.rs:80-98, bincode fixint LE)
+  {
+    BinWriter w;
+    w.u64(N);
+    w.u64(tau);
+    w.u64((uint64_t)ncols);
+    root_pos.assign(ncols, 0);
+    for (int c = 0; c < ncols; c++) {
+      w.u64(labels[c].size());
+      w.raw(labels[c].data(), labels[c].size());
+      root_pos[c] = w.b.size();
+      w.raw(std::string(32, '\0').data(), 32);
+    }
+    hdr_bytes = w.b.size();
+    PL = ProofLayout{};
+    PL.open_per_q = 9 * tau + 3;
+    PL.nq = NUM_QUERIES;
+    PL.k = k;
+    PL.tau = tau;
+    PL.open_bytes = 80 + 32 * (uint64_t)logn;  // path_in_chunk + path_to_chunk = log2(n) levels
+    PL.q_bytes = 16 + PL.open_per_q * PL.open_bytes;
+    PL.fr_off = 8 + NUM_QUERIES * PL.q_bytes;
+    PL.fq_off = PL.fr_off + 8 + 32 * (uint64_t)(k + 1);
+    PL.fq_bytes = 8 + 8 * (uint64_t)(k + 1) + 8;
+    for (int r = 0; r < k; r++) PL.fq_bytes += 2 * (16 + 32 * (uint64_t)(k - r));
+    PL.tail_off = PL.fq_off + 8 + NUM_QUERIES * PL.fq_bytes;
+    PL.total = PL.tail_off + 8 + 32;
+    PL.base = dalloc<uint32_t>(PL.total / 4 + 2);
+    h_proof = halloc<uint8_t>(hdr_bytes + PL.total);
+    memcpy(h_proof, w.b.data(), hdr_bytes);
+  }
   h_small = halloc<uint32_t>((size_t)(ncols + k + 2) * 8);
   loaded = true;
 }
 
-std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
+size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   if (!loaded) throw Err{SEZKP_E_INVALID, "no trace uploaded"};
+  using clk = std::chrono::steady_clock;
+  const auto t_enter = clk::now();
+  double t_sync = 0, t_last = 0;
+  auto sync = [&]() {
+    const auto t0 = clk::now();
+    HIP_OR_THROW(hipStreamSynchronize(st));
+    t_last = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    t_sync += t_last;
+  };
   HIP_OR_THROW(hipSetDevice(device));
   const int k = logN;
   auto rec = [&](int s) { HIP_OR_THROW(hipEventRecord(ev[s], st)); };
@@ -451,6 +508,8 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
   // ---- column commitments (openings.rs:306-398)
   ok(launch_expand(st, T), "expand");
   rec(1);
+  ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride),
+     "col_commit_dict");
   ok(launch_col_tables(st, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs), "col_tables");
   ok(launch_col_commit(st, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
   ok(launch_col_commit_pw(st, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
@@ -461,9 +520,10 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
   rec(3);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
   HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * ncols, d_err, 4, hipMemcpyDeviceToHost, st));
-  HIP_OR_THROW(hipStreamSynchronize(st));
+  sync();
   if (h_small[8 * ncols]) throw Err{SEZKP_E_DEVICE, "column commitment guard tripped (code " + std::to_string(h_small[8 * ncols]) + ")"};
   std::vector<uint8_t> colroots((uint8_t*)h_small, (uint8_t*)h_small + (size_t)ncols * 32);
+  for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
 
   // ---- transcript prelude + column roots (prover.rs:67-81)
   Transcript tr("sezkp-stark/v1");
@@ -511,7 +571,7 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
   }
   rec(8);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
-  HIP_OR_THROW(hipStreamSynchronize(st));
+  sync();
   std::vector<uint8_t> roots((size_t)(k + 1) * 32);
   memcpy(roots.data(), h_small, 32);
   tr.absorb("fri_layer_root", roots.data(), 32);
@@ -543,7 +603,7 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
   for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
   rec(9);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
-  HIP_OR_THROW(hipStreamSynchronize(st));
+  sync();
   memcpy(roots.data(), h_small, (size_t)(k + 1) * 32);
   for (int r = 1; r <= k; r++) tr.absorb("fri_layer_root", roots.data() + 32 * r, 32);
 
@@ -596,15 +656,13 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
     push_open(0, row);  // input_mv
   }
   HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (2 * max_fri_req + 3 * no) * 4, hipMemcpyHostToDevice, st));
-  ok(launch_fri_paths(st, d_layers, d_req, (int)nf, d_fri_out), "fri_paths");
+  ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL, d_fri + (N - 2)), "fri_paths");
   rec(10);
-  ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 2 * max_fri_req, (int)no, d_open_out),
+  ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 2 * max_fri_req, (int)no, PL),
      "col_open");
   rec(11);
-  HIP_OR_THROW(hipMemcpyAsync(h_fri_out, d_fri_out, nf * PATH_REC_WORDS * 4, hipMemcpyDeviceToHost, st));
-  HIP_OR_THROW(hipMemcpyAsync(h_open_out, d_open_out, no * OPEN_REC_WORDS * 4, hipMemcpyDeviceToHost, st));
-  HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), d_fri + (N - 2), 8, hipMemcpyDeviceToHost, st));
-  HIP_OR_THROW(hipStreamSynchronize(st));
+  HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.total, hipMemcpyDeviceToHost, st));
+  sync();
   for (int s = 0; s < ST_NSTAGE; s++) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, ev[s], ev[s + 1]) == hipSuccess) stage_ms[s] = ms;
@@ -614,68 +672,20 @@ std::vector<uint8_t> sezkp_ctx::prove(const uint8_t mroot[32]) {
   stage_ms[ST_NSTAGE] = tot;
   have_times = true;
 
-  // ---- bincode ProofV1 (proof.rs:80-98)
-  BinWriter w;
-  w.b.reserve(4u << 20);
-  w.u64(N);    // domain_n
-  w.u64(tau);  // tau
-  w.u64((uint64_t)ncols);
-  for (int c = 0; c < ncols; c++) {
-    w.u64(labels[c].size());
-    w.raw(labels[c].data(), labels[c].size());
-    w.raw(colroots.data() + 32 * c, 32);
-  }
-  const int logcl = logn < COL_CHUNK_LOG2 ? logn : COL_CHUNK_LOG2;
-  w.u64(NUM_QUERIES);
-  size_t oi = 0;
-  auto emit_open = [&](uint64_t row) {
-    const uint32_t* o = h_open_out + oi * OPEN_REC_WORDS;
-    oi++;
-    const uint64_t ch = row >> COL_CHUNK_LOG2;
-    w.raw(o, 8);                        // value_le
-    w.u64(row);                         // index
-    w.u64(ch);                          // chunk_index
-    w.u64(row - (ch << COL_CHUNK_LOG2));  // index_in_chunk
-    w.raw(o + 2, 32);                   // chunk_root
-    w.u64((uint64_t)logcl);
-    w.raw(o + 10, 32 * (size_t)logcl);  // path_in_chunk
-    w.u64((uint64_t)logChunks);
-    w.raw(o + 90, 32 * (size_t)logChunks);  // path_to_chunk
-  };
-  for (int q = 0; q < NUM_QUERIES; q++) {
-    const uint64_t row = rows[q], ip1 = row + 1 < n ? row + 1 : 0;
-    w.u64(row);
-    w.u64(tau);
-    for (uint32_t r = 0; r < tau; r++) {
-      emit_open(row); emit_open(ip1); emit_open(row); emit_open(row); emit_open(row);
-      emit_open(ip1); emit_open(row); emit_open(row); emit_open(row);
-    }
-    emit_open(row); emit_open(row); emit_open(row);
-  }
-  w.u64((uint64_t)k + 1);  // fri_roots
-  w.raw(roots.data(), roots.size());
-  w.u64(NUM_QUERIES);      // fri_queries
-  size_t fi = 0;
-  for (int q = 0; q < NUM_QUERIES; q++) {
-    const uint64_t* p = &pos[(size_t)q * (k + 1)];
-    w.u64((uint64_t)k + 1);
-    for (int r = 0; r <= k; r++) w.u64(p[r]);
-    w.u64((uint64_t)k);
-    for (int r = 0; r < k; r++) {
-      const uint64_t L = (uint64_t)(k - r);
-      for (int side = 0; side < 2; side++) {
-        const uint32_t* o = h_fri_out + (fi++) * PATH_REC_WORDS;
-        w.raw(o, 8);
-        w.u64(L);
-        w.raw(o + 4, 32 * L);
-      }
-    }
-  }
-  uint8_t fv[8];
-  memcpy(fv, h_small + 8 * (k + 1), 8);  // final value = layer k's single element (prover.rs:242-243)
-  w.raw(fv, 8);
-  w.raw(mroot, 32);
-  return std::move(w.b);
+  // ---- host-known parts of the body: FRI roots, manifest root
+  const auto t_ser = clk::now();
+  uint8_t* body = h_proof + hdr_bytes;
+  const uint64_t kr = (uint64_t)k + 1;
+  memcpy(body + PL.fr_off, &kr, 8);
+  memcpy(body + PL.fr_off + 8, roots.data(), roots.size());
+  memcpy(body + PL.tail_off + 8, mroot, 32);
+  const size_t out = hdr_bytes + PL.total;
+  const auto t_end = clk::now();
+  host_ms[0] = std::chrono::duration<double, std::milli>(t_end - t_enter).count();
+  host_ms[1] = t_sync;
+  host_ms[2] = t_last;
+  host_ms[3] = std::chrono::duration<double, std::milli>(t_end - t_ser).count();
+  return out;
 }
 
 // ==================================================================== C ABI
@@ -743,7 +753,11 @@ int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_
   (void)flags;
   try {
     if (!ctx || !manifest_root || !proof_bytes) throw Err{SEZKP_E_INVALID, "null argument"};
-    to_buf(ctx->prove(manifest_root), proof_bytes);
+    const size_t len = ctx->prove(manifest_root);
+    proof_bytes->data = (uint8_t*)malloc(len ? len : 1);
+    if (!proof_bytes->data) throw Err{SEZKP_E_NOMEM, "out of host memory"};
+    memcpy(proof_bytes->data, ctx->h_proof, len);
+    proof_bytes->len = len;
     return SEZKP_OK;
   } catch (const Err& e) {
     set_err(err, err_len, e.msg);
@@ -758,6 +772,7 @@ int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max)
   if (!ctx || !ctx->have_times) return 0;
   int cnt = 0;
   for (int s = 0; s <= ST_NSTAGE && cnt < max; s++) out_ms[cnt++] = ctx->stage_ms[s];
+  for (int s = 0; s < 4 && cnt < max; s++) out_ms[cnt++] = ctx->host_ms[s];
   return cnt;
 }
 void* sezkp_ctx_stream(const sezkp_ctx* ctx) { return ctx ? (void*)ctx->st : nullptr; }

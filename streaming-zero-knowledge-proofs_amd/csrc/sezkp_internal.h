@@ -95,10 +95,44 @@ __host__ __device__ inline bool kind_has_leaf_table(uint32_t kind) { return kind
 // the block-boundary flags): committed from uniform-subtree hashes.
 __host__ __device__ inline bool kind_piecewise(uint32_t kind) { return kind == 1 || kind == 2 || kind >= 7; }
 
+// Dictionary (memoized subtree) commitment of dense small-range columns.
+constexpr int DICT_LEVELS = 5;          // tables T_0..T_4
+constexpr uint32_t DICT_CAP = 65536;    // entries per table level
+struct DictCol {
+  uint32_t col;
+  uint32_t pad;
+  uint64_t tab;  // node offset of this column's DICT_LEVELS x DICT_CAP tables
+};
+struct DictPlan {
+  int64_t min;
+  uint32_t R;    // range size (codes = raw - min < R)
+  int32_t K;     // table level used by the commit kernel; -1 = leaves computed
+  uint32_t pw[DICT_LEVELS];  // entries of T_k = R^(2^k) (0 above K)
+  uint32_t pad;
+};
+__host__ __device__ inline bool kind_dict(uint32_t kind) { return kind == 0 || (kind >= 3 && kind <= 6); }
+
 constexpr int LSTORE_FRI = 6;
 constexpr int COL_CHUNK_LOG2 = 10;
-constexpr int PATH_REC_WORDS = 264;   // FRI path record: 2 value + 2 pad + 32*8 siblings
-constexpr int OPEN_REC_WORDS = 352;   // column opening record
+// Device image of the bincode ProofV1 body (proof.rs:80-98) after the
+// column-root header: every record there is 8-byte aligned and fixed-size,
+// so the opening and path kernels write proof bytes in place.
+//   0                 u64 #queries
+//   8 + q*q_bytes     u64 row, u64 tau, then open_per_q openings of open_bytes
+//   fr_off            u64 k+1, (k+1) x 32 B FRI roots            (host)
+//   fq_off            u64 #queries
+//   fq_off+8+q*fq_bytes  u64 k+1, k+1 positions, u64 k, 2k path records
+//   tail_off          final value (8 B), manifest root (32 B)     (root: host)
+struct ProofLayout {
+  uint32_t* base;          // device pointer, 8-byte aligned
+  uint64_t open_bytes;     // 80 + 32*log2(n)
+  uint64_t q_bytes;        // 16 + open_per_q * open_bytes
+  uint64_t fr_off, fq_off, fq_bytes, tail_off, total;
+  uint32_t open_per_q;     // 9*tau + 3
+  uint32_t nq;             // queries (params.rs:31)
+  int k;                   // log2(N)
+  uint32_t tau;
+};
 
 // kernels launched by the host orchestrator (prover.cpp)
 hipError_t launch_expand(hipStream_t st, const TraceDev& T);
@@ -106,6 +140,9 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
                              int n_tab_cols, uint64_t tab_entries, uint32_t* tabs);
 hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_work,
                              int nwork, const uint32_t* tabs, uint32_t* outer_nodes, uint64_t outer_stride_nodes);
+hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
+                              int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
+                              uint64_t outer_stride_nodes);
 hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);
@@ -155,9 +192,9 @@ struct TailArgs {
 };
 hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a);
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
-                            uint32_t* d_out);
+                            const ProofLayout& P, const uint64_t* final_val);
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
-                           uint32_t* d_out);
+                           const ProofLayout& P);
 
 }  // namespace sezkp

@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
 __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                          const uint32_t* __restrict__ outer, uint64_t outer_stride,
                                                          int logChunks, const uint32_t* __restrict__ req,
-                                                         uint32_t* __restrict__ out) {
+                                                         ProofLayout P) {
   __shared__ uint32_t lds[8][1024];
   const uint32_t q = blockIdx.x;
   const int c = req[3 * q];
@@ -481,7 +481,21 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
   const uint64_t cl = n < 1024 ? n : 1024;
   int logcl = 0;
   while ((1ULL << logcl) < cl) logcl++;
-  uint32_t* o = out + (uint64_t)q * OPEN_REC_WORDS;
+  // Opening record (proof.rs:44-66): value, index, chunk_index, index_in_chunk,
+  // chunk_root, path_in_chunk (u64 len + siblings), path_to_chunk (u64 len + siblings)
+  const uint32_t qi = q / P.open_per_q, s = q % P.open_per_q;
+  uint32_t* qb = P.base + (8 + (uint64_t)qi * P.q_bytes) / 4;
+  uint32_t* o = qb + (16 + (uint64_t)s * P.open_bytes) / 4;
+  const uint64_t in = row - start;
+  if (tid == 0) {
+    if (q == 0) { P.base[0] = P.nq; P.base[1] = 0; }
+    if (s == 0) { qb[0] = (uint32_t)row; qb[1] = (uint32_t)(row >> 32); qb[2] = P.tau; qb[3] = 0; }
+    o[2] = (uint32_t)row; o[3] = (uint32_t)(row >> 32);
+    o[4] = (uint32_t)ch; o[5] = (uint32_t)(ch >> 32);
+    o[6] = (uint32_t)in; o[7] = 0;
+    o[16] = (uint32_t)logcl; o[17] = 0;
+    o[18 + 8 * logcl] = (uint32_t)logChunks; o[19 + 8 * logcl] = 0;
+  }
   for (uint64_t i = tid; i < cl; i += TR_THREADS) {
     uint32_t h[8];
     leaf_labeled_rt(ct, col_value(T, ct, start + i), h);
@@ -494,11 +508,10 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
     o[1] = (uint32_t)(v >> 32);
   }
   __syncthreads();
-  const uint64_t in = row - start;
   int cnt = (int)cl;
   for (int lvl = 0; lvl < logcl; lvl++) {
     const int sib = (int)((in >> lvl) ^ 1);
-    if (tid < 8) o[10 + 8 * lvl + tid] = lds[tid][sib];
+    if (tid < 8) o[18 + 8 * lvl + tid] = lds[tid][sib];
     const int half = cnt >> 1;
     uint32_t hh[2][8];
     int k = 0;
@@ -516,13 +529,317 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
     __syncthreads();
     cnt = half;
   }
-  if (tid < 8) o[2 + tid] = lds[tid][0];
+  if (tid < 8) o[8 + tid] = lds[tid][0];
   // path_to_chunk from the stored outer tree (all levels kept)
   const uint32_t* ob = outer + (uint64_t)c * outer_stride * 8;
+  uint32_t* op = o + 20 + 8 * logcl;
   for (int lvl = 0; lvl < logChunks; lvl++) {
     const uint64_t sib = (ch >> lvl) ^ 1;
-    if (tid < 8) o[90 + 8 * lvl + tid] = ob[8 * (tree_level_off(logChunks, 0, lvl) + sib) + tid];
+    if (tid < 8) op[8 * lvl + tid] = ob[8 * (tree_level_off(logChunks, 0, lvl) + sib) + tid];
   }
+}
+
+// ------------------------------------------------ dictionary commitments
+// Exact memoization for the dense columns (input_mv, mv, write_flag,
+// write_sym, head). Their raw integers lie in a small range [min, min+R) on
+// real traces (the AIR constrains mv/input_mv to {-1,0,1} and write_flag to
+// {0,1}; symbols come from a small alphabet; heads are block-relative walks).
+// The hash of an aligned 2^k-row subtree is a function of its k-tuple of
+// codes (raw - min), so tables T_k[e], e = sum_i code_i * R^i (row i of the
+// subtree), built level by level (T_0 = labelled leaves, T_{k+1} = H(T_k||T_k)),
+// replace the bottom K levels of every chunk tree. K is chosen per column on
+// the device from the measured range (cost = table entries + n / 2^K);
+// R^(2^K) <= DICT_CAP. Columns whose range is too wide use K = -1 (leaves
+// computed per row). The commitment is bit-identical either way.
+
+template <typename Key>
+__device__ __forceinline__ const Key* dict_keys(const TraceDev& T, const ColTemplate& ct) {
+  const uint64_t o = (uint64_t)ct.tape * T.n;
+  if constexpr (sizeof(Key) == 8) return reinterpret_cast<const Key*>(T.head + o);
+  else if constexpr (sizeof(Key) == 2) return reinterpret_cast<const Key*>(T.wsym + o);
+  else {
+    if (ct.kind == 0) return reinterpret_cast<const Key*>(T.input_mv);
+    if (ct.kind == 3) return reinterpret_cast<const Key*>(T.mv + o);
+    return reinterpret_cast<const Key*>(T.wflag + o);
+  }
+}
+// raw integer of a dense column at `row` (signed for i8 / i64 kinds)
+__device__ __forceinline__ int64_t dict_key_at(const TraceDev& T, const ColTemplate& ct, uint64_t row) {
+  const uint64_t o = (uint64_t)ct.tape * T.n + row;
+  switch (ct.kind) {
+    case 0: return T.input_mv[row];
+    case 3: return T.mv[o];
+    case 4: return T.wflag[o];
+    case 5: return T.wsym[o];
+    default: return T.head[o];
+  }
+}
+
+template <typename Key, int CNT>
+__device__ __forceinline__ void load_keys(const Key* __restrict__ p, int64_t (&k)[CNT]) {
+  constexpr int BYTES = CNT * (int)sizeof(Key);
+  if constexpr (BYTES >= 16) {
+    constexpr int PER = 16 / (int)sizeof(Key);
+#pragma unroll
+    for (int q = 0; q < BYTES / 16; q++) {
+      const uint4 w = reinterpret_cast<const uint4*>(p)[q];
+      const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int i = 0; i < PER; i++) {
+        const int bit = i * 8 * (int)sizeof(Key);
+        uint64_t raw;
+        if constexpr (sizeof(Key) == 8) raw = (uint64_t)ww[bit / 32] | ((uint64_t)ww[bit / 32 + 1] << 32);
+        else raw = (ww[bit / 32] >> (bit % 32)) & ((1u << (8 * sizeof(Key))) - 1u);
+        k[q * PER + i] = (int64_t)(Key)raw;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < CNT; i++) k[i] = (int64_t)p[i];
+  }
+}
+
+// Node providers for lane_tree: node j of the lane's 2^D nodes.
+template <typename Key, int K>
+struct DictNodes {
+  const Key* p;           // first row of the lane
+  const uint32_t* tab;    // T_K
+  int64_t mn;
+  uint32_t R;
+  __device__ __forceinline__ void get(int j, uint32_t (&h)[8]) const {
+    int64_t k[1 << K];
+    load_keys<Key, (1 << K)>(p + ((uint64_t)j << K), k);
+    uint32_t idx = 0;
+#pragma unroll
+    for (int i = (1 << K) - 1; i >= 0; i--) idx = idx * R + (uint32_t)(k[i] - mn);
+    node_load(tab + 8 * (uint64_t)idx, h);
+  }
+};
+template <typename Key>
+struct RawLeaves {
+  const Key* p;
+  const ColTemplate* ct;
+  __device__ __forceinline__ void get(int j, uint32_t (&h)[8]) const {
+    leaf_labeled_rt(*ct, gl_from_i64((int64_t)p[j]), h);
+  }
+};
+
+// Binary-counter Merkle reduction of 2^D consecutive nodes in a rolled loop:
+// the stack is indexed statically (merges unrolled per level, branch on the
+// uniform loop counter), so code size is D+1 compressions, not 2^(D+1).
+template <int D, class Prov>
+__device__ __forceinline__ void lane_tree(const Prov& P, uint32_t (&h)[8]) {
+  uint32_t s[D > 0 ? D : 1][8];
+  for (int j = 0; j < (1 << D); j++) {
+    uint32_t x[8];
+    P.get(j, x);
+    bool done = false;
+#pragma unroll
+    for (int l = 0; l < D; l++) {
+      if (!done) {
+        if ((j >> l) & 1) {
+          b3_parent(s[l], x, x);
+        } else {
+#pragma unroll
+          for (int w = 0; w < 8; w++) s[l][w] = x[w];
+          done = true;
+        }
+      }
+    }
+    if (!done) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) h[w] = x[w];
+    }
+  }
+}
+
+constexpr int DICT_LANE_LOG = 6;                                     // rows per lane
+constexpr int DICT_WG_ROWS = 64 << DICT_LANE_LOG;                    // 4096 rows per 64-lane WG
+constexpr int DICT_RANGE_ROWS = TR_THREADS * 16;                     // rows per range WG
+
+// per-(column, 4096 rows) min / max of the raw integers
+__global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                           const DictCol* __restrict__ dcols,
+                                                           int64_t* __restrict__ part, uint32_t nparts) {
+  __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
+  const ColTemplate ct = tmpl[dcols[blockIdx.y].col];
+  const int tid = threadIdx.x;
+  const uint64_t r0 = (uint64_t)blockIdx.x * DICT_RANGE_ROWS + (uint64_t)tid * 16;
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  if (r0 < T.n) {
+    int64_t k[16];
+    switch (ct.kind) {
+      case 0: case 3: load_keys<int8_t, 16>(dict_keys<int8_t>(T, ct) + r0, k); break;
+      case 4: load_keys<uint8_t, 16>(dict_keys<uint8_t>(T, ct) + r0, k); break;
+      case 5: load_keys<uint16_t, 16>(dict_keys<uint16_t>(T, ct) + r0, k); break;
+      default: load_keys<int64_t, 16>(dict_keys<int64_t>(T, ct) + r0, k); break;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      lo = k[i] < lo ? k[i] : lo;
+      hi = k[i] > hi ? k[i] : hi;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if ((tid & 63) == 0) { slo[tid >> 6] = lo; shi[tid >> 6] = hi; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < TR_THREADS / 64; w++) {
+      lo = slo[w] < lo ? slo[w] : lo;
+      hi = shi[w] > hi ? shi[w] : hi;
+    }
+    int64_t* o = part + 2 * ((uint64_t)blockIdx.y * nparts + blockIdx.x);
+    o[0] = lo;
+    o[1] = hi;
+  }
+}
+
+// one WG per dictionary column: reduce the partial ranges and choose K
+__global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restrict__ part, uint32_t nparts,
+                                                          uint64_t n, DictPlan* __restrict__ plans) {
+  __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
+  const int tid = threadIdx.x;
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  const int64_t* pp = part + 2 * (uint64_t)blockIdx.x * nparts;
+  for (uint32_t i = tid; i < nparts; i += TR_THREADS) {
+    lo = pp[2 * i] < lo ? pp[2 * i] : lo;
+    hi = pp[2 * i + 1] > hi ? pp[2 * i + 1] : hi;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if ((tid & 63) == 0) { slo[tid >> 6] = lo; shi[tid >> 6] = hi; }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int w = 1; w < TR_THREADS / 64; w++) {
+    lo = slo[w] < lo ? slo[w] : lo;
+    hi = shi[w] > hi ? shi[w] : hi;
+  }
+  DictPlan P{};
+  P.min = lo;
+  P.K = -1;
+  const uint64_t R = hi >= lo ? (uint64_t)hi - (uint64_t)lo + 1 : 1;
+  if (R <= DICT_CAP) {
+    P.R = (uint32_t)R;
+    uint64_t best = 2 * n, tabcost = 0, sz = R;  // K = -1: n leaves + n parents
+    for (int k = 0; k < DICT_LEVELS && (1ULL << k) <= n && sz <= DICT_CAP; k++) {
+      P.pw[k] = (uint32_t)sz;
+      tabcost += sz;
+      const uint64_t cost = tabcost + (n >> k);
+      if (cost < best) { best = cost; P.K = k; }
+      sz = sz * sz;
+    }
+    for (int k = P.K + 1; k < DICT_LEVELS; k++) P.pw[k] = 0;
+  }
+  plans[blockIdx.x] = P;
+}
+
+// table level `lvl` of every dictionary column (grid.y = column)
+__global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __restrict__ tmpl,
+                                                           const DictCol* __restrict__ dcols,
+                                                           const DictPlan* __restrict__ plans,
+                                                           uint32_t* __restrict__ tabs, int lvl) {
+  const DictPlan P = plans[blockIdx.y];
+  if (lvl > P.K) return;
+  const uint32_t e = blockIdx.x * TR_THREADS + threadIdx.x;
+  uint32_t size = 0, S = 0;  // static indices only (no scratch copy of P)
+#pragma unroll
+  for (int k = 0; k < DICT_LEVELS; k++) {
+    if (k == lvl) size = P.pw[k];
+    if (k + 1 == lvl) S = P.pw[k];
+  }
+  if (e >= size) return;
+  const DictCol dc = dcols[blockIdx.y];
+  uint32_t* tl = tabs + 8 * (dc.tab + (uint64_t)lvl * DICT_CAP);
+  uint32_t h[8];
+  if (lvl == 0) {
+    leaf_labeled_rt(tmpl[dc.col], gl_from_i64(P.min + (int64_t)e), h);
+  } else {
+    const uint32_t* tp = tl - 8 * (uint64_t)DICT_CAP;
+    uint32_t a[8], b[8];
+    node_load(tp + 8 * (uint64_t)(e % S), a);
+    node_load(tp + 8 * (uint64_t)(e / S), b);
+    b3_parent(a, b, h);
+  }
+  node_store(tl + 8 * (uint64_t)e, h);
+}
+
+template <typename Key>
+__device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const uint32_t* tab,
+                                          const ColTemplate* ct, uint32_t (&h)[8]) {
+  switch (P.K) {
+    case 0: lane_tree<6>(DictNodes<Key, 0>{p, tab, P.min, P.R}, h); break;
+    case 1: lane_tree<5>(DictNodes<Key, 1>{p, tab + 8 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 2: lane_tree<4>(DictNodes<Key, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 3: lane_tree<3>(DictNodes<Key, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 4: lane_tree<2>(DictNodes<Key, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    default: lane_tree<6>(RawLeaves<Key>{p, ct}, h); break;
+  }
+}
+
+// 64-lane WG = 4096 rows of one dictionary column (4 chunks): each lane folds
+// 64 rows to a level-6 node, 4 LDS levels give the 4 chunk roots, written as
+// leaves of the column's outer tree. Requires n >= 1024 (n % 64 == 0).
+__global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                        const DictCol* __restrict__ dcols,
+                                                        const DictPlan* __restrict__ plans,
+                                                        const uint32_t* __restrict__ tabs, uint32_t* __restrict__ outer,
+                                                        uint64_t outer_stride) {
+  __shared__ uint32_t lds[8][64];
+  const DictCol dc = dcols[blockIdx.y];
+  const ColTemplate* ctp = tmpl + dc.col;
+  const ColTemplate ct = *ctp;
+  const DictPlan P = plans[blockIdx.y];
+  const uint32_t* tab = tabs + 8 * dc.tab;
+  const int lane = threadIdx.x;
+  const uint64_t row0 = (uint64_t)blockIdx.x * DICT_WG_ROWS + ((uint64_t)lane << DICT_LANE_LOG);
+  const bool act = row0 < T.n;
+  if (act) {
+    uint32_t h[8];
+    switch (ct.kind) {
+      case 0: case 3: dict_lane<int8_t>(dict_keys<int8_t>(T, ct) + row0, P, tab, ctp, h); break;
+      case 4: dict_lane<uint8_t>(dict_keys<uint8_t>(T, ct) + row0, P, tab, ctp, h); break;
+      case 5: dict_lane<uint16_t>(dict_keys<uint16_t>(T, ct) + row0, P, tab, ctp, h); break;
+      default: dict_lane<int64_t>(dict_keys<int64_t>(T, ct) + row0, P, tab, ctp, h); break;
+    }
+#pragma unroll
+    for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
+  }
+  __syncthreads();
+  for (int cnt = 64; cnt > 4; cnt >>= 1) {  // levels 7..10
+    const int half = cnt >> 1;
+    uint32_t h[8];
+    const bool a2 = lane < half;
+    if (a2) {
+      uint32_t l[8], r[8];
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        const uint2 pr = *reinterpret_cast<const uint2*>(&lds[w][2 * lane]);
+        l[w] = pr.x;
+        r[w] = pr.y;
+      }
+      b3_parent(l, r, h);
+    }
+    __syncthreads();
+    if (a2) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
+    }
+    __syncthreads();
+  }
+  // chunk i of this WG: rows [blockIdx.x*4096 + 1024 i, +1024)
+  const uint64_t nch = T.n >> COL_CHUNK_LOG2;
+  const int q = lane >> 3, w = lane & 7;
+  const uint64_t ch = (uint64_t)blockIdx.x * 4 + q;
+  if (q < 4 && ch < nch) outer[(uint64_t)dc.col * outer_stride * 8 + ch * 8 + w] = lds[w][q];
 }
 
 // ------------------------------------------------------------------ host
@@ -538,6 +855,28 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
   hipLaunchKernelGGL(k_col_tables, dim3(gx, n_tab_cols), dim3(TR_THREADS), 0, st, T, d_tmpl, d_tab_cols, tabs);
   return hipGetLastError();
 }
+hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
+                              int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
+                              uint64_t outer_stride_nodes) {
+  if (ndict == 0) return hipSuccess;
+  if (T.n < (1ULL << COL_CHUNK_LOG2)) return hipErrorInvalidValue;
+  const uint32_t nparts = (uint32_t)((T.n + DICT_RANGE_ROWS - 1) / DICT_RANGE_ROWS);
+  hipLaunchKernelGGL(k_dict_range, dim3(nparts, ndict), dim3(TR_THREADS), 0, st, T, d_tmpl, d_dcols, d_part, nparts);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_plans);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  for (int l = 0; l < DICT_LEVELS; l++) {
+    hipLaunchKernelGGL(k_dict_level, dim3(DICT_CAP / TR_THREADS, ndict), dim3(TR_THREADS), 0, st, d_tmpl, d_dcols,
+                       d_plans, d_dtabs, l);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  const unsigned gx = (unsigned)((T.n + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
+  hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
+                     outer_nodes, outer_stride_nodes);
+  return hipGetLastError();
+}
+
 hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_work,
                              int nwork, const uint32_t* tabs, uint32_t* outer_nodes, uint64_t outer_stride_nodes) {
   if (nwork == 0) return hipSuccess;
@@ -564,10 +903,11 @@ hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, co
 }
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
-                           uint32_t* d_out) {
+                           const ProofLayout& P) {
   if (nreq == 0) return hipSuccess;
+  if ((uint64_t)nreq != (uint64_t)P.nq * P.open_per_q) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_col_open, dim3(nreq), dim3(TR_THREADS), 0, st, T, d_tmpl, outer_nodes, outer_stride_nodes,
-                     logChunks, d_req, d_out);
+                     logChunks, d_req, P);
   return hipGetLastError();
 }
 

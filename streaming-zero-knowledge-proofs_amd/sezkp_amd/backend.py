@@ -15,7 +15,9 @@ from ._lib import SEZKP_FLAG_STREAMING, Buf, SezkpError, check, lib, take_buf
 from .blocks import BlockSoA
 
 STAGES = ["expand", "col_commit", "col_outer", "compose", "intt", "lde_ntt", "deep", "layer0_tree",
-          "fri_fold_trees", "fri_paths", "col_openings", "total"]
+          "fri_fold_trees", "fri_paths", "col_openings", "total",
+          # host-side split of the same prove() call (wall clock)
+          "host_wall", "host_sync_wait", "host_final_wait", "host_serialize"]
 
 
 @dataclass
@@ -124,7 +126,7 @@ class ProverContext:
     def stage_times_ms(self) -> dict:
         buf = (C.c_double * 16)()
         n = lib.sezkp_ctx_stage_times(self._h, buf, 16)
-        return {STAGES[i]: buf[i] for i in range(n)}
+        return {STAGES[i]: buf[i] for i in range(min(n, len(STAGES)))}
 
     @property
     def stream(self) -> int:

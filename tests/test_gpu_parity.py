@@ -169,6 +169,32 @@ def test_prove_wide_values_bit_exact(gpu_ok, product, oracle):
     assert art.proof_bytes == oracle.prove_v1(blocks, mroot)
 
 
+def test_prove_dictionary_branches_bit_exact(gpu_ok, product, oracle, monkeypatch):
+    """Dense columns are committed through range dictionaries whose table level K
+    is chosen per column on the device; force every branch at T = 2^17 in one
+    block: head of tape 0 drifts by +1 per row (range 2^17 -> K = -1, computed
+    leaves), full u16 symbols on tape 0 (R = 65536 -> K = 0), 16 symbols on
+    tape 1 (K = 2), {-1,0,1} moves (K = 3), all-zero tape 2 (R = 1 -> K = 4).
+    The same bytes must come out with the dictionary path disabled."""
+    rng = np.random.default_rng(17)
+    T, tau = 1 << 17, 3
+    imv = rng.integers(-1, 2, T, dtype=np.int8)
+    mv = np.zeros((T, tau), np.int8)
+    mv[:, 0] = 1
+    mv[:, 1] = rng.integers(-1, 2, T, dtype=np.int8)
+    hw = np.zeros((T, tau), np.uint8)
+    hw[:, :2] = 1
+    ws = np.zeros((T, tau), np.uint16)
+    ws[:, 0] = rng.integers(0, 65536, T)
+    ws[:, 1] = rng.integers(0, 16, T)
+    blocks = product.partition(imv, mv, hw, ws, T)
+    mroot = blocks.manifest_root()
+    want = oracle.prove_v1(blocks, mroot)
+    assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
+    monkeypatch.setenv("SEZKP_NO_DICT", "1")
+    assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
+
+
 def test_prove_rejects_bad_shapes(gpu_ok, product):
     blocks = product.synthetic_blocks(96, 32, 2)  # n = 96, not a power of two
     with pytest.raises(product.SezkpError, match="power of two"):
