@@ -13,9 +13,16 @@ each proving its own copy of the workload (independent proofs, weak scaling,
 no data-path collective); the barrier / max-time reduction runs over RCCL.
 
 Extra objects on the JSON line:
-  roofline     — dominant kernel (column commitments) timed live with HIP
-                 events on the prover's stream; achieved = SURVEY §8(d)
-                 algorithmic bytes per launch / mean launch time.
+  roofline     — dominant kernel (k_layer16: the BLAKE3 Merkle tree over the
+                 2^24-point LDE, one launch per prove) timed live with HIP
+                 events bracketing exactly that launch on the prover's
+                 stream; achieved = SURVEY §8(d) algorithmic bytes per launch
+                 (72 B per leaf) / mean launch time. The kernel is VALU-bound
+                 (BLAKE3), so `valu` reports compressions/s against the
+                 CDNA4 integer-VALU ceiling next to the HBM fraction.
+  ntt_lde      — the HBM-bound LDE NTT (3 LDS passes) against SURVEY's
+                 9 B per LDE point compulsory traffic and against its own
+                 moved bytes.
   cpu_baseline — the C oracle (single-thread restatement of the reference's
                  compute path) timed on this host on a bounded sample.
 """
@@ -30,6 +37,10 @@ sys.path.insert(0, os.path.join(ROOT, "streaming-zero-knowledge-proofs_amd"))
 
 METRIC = "STARK prove field-elements/sec (NTT+FRI+Merkle), 2^24 domain, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# BLAKE3 compression = 7 rounds x 8 G x 12 VALU ops + finalisation ~ 690 ops;
+# 256 CU x 64 lanes x 2.4 GHz = 39.3 T int32 ops/s -> 57 G compressions/s
+# (tools/b3_ceiling.hip measures 57.4 G/s for 64-byte parent blocks).
+VALU_B3_PEAK = 57.0e9
 
 
 def alg_bytes(n: int, tau: int) -> dict:
@@ -131,13 +142,24 @@ def main():
 
     if rank == 0:
         ab = alg_bytes(T, args.tau)
-        t_commit = stages.get("col_commit", float("nan")) * 1e-3
-        achieved = ab["col_commit"] / t_commit / 1e9
-        roof = {"bound": "hbm", "kernel": "k_col_commit", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc("k_col_commit"),
-                "alg_bytes_per_launch": ab["col_commit"], "mean_launch_ms": t_commit * 1e3,
-                "note": "BLAKE3 column commitments (59 cols x 2^21 rows): VALU-bound; "
-                        "SURVEY 8(d) bytes = 72 B per column cell"}
+        t_l0 = stages.get("layer0_tree", float("nan")) * 1e-3
+        l0_bytes = 72 * N  # layer-0 Merkle = 8 B value + 64 B of nodes per leaf
+        achieved = l0_bytes / t_l0 / 1e9
+        roof = {"bound": "hbm", "kernel": "k_layer16", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc("k_layer16"),
+                "alg_bytes_per_launch": l0_bytes, "mean_launch_ms": t_l0 * 1e3,
+                "valu": {"compressions_per_launch": 2 * N - N // 4096,
+                         "achieved_per_s": (2 * N - N // 4096) / t_l0, "peak_per_s": VALU_B3_PEAK,
+                         "frac": (2 * N - N // 4096) / t_l0 / VALU_B3_PEAK},
+                "note": "layer-0 FRI Merkle tree over the LDE (2^24 leaves); BLAKE3 is VALU-bound on CDNA4, "
+                        "so the HBM fraction is structurally low (SURVEY 8(d) caveat); traffic = PMC "
+                        "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE per launch from profiles/pmc_summary.json"}
+        t_lde = stages.get("lde_ntt", float("nan")) * 1e-3
+        moved = 16 * N * 3 - 8 * (N - T)  # 3 passes read+write, the first reads only the n coefficients
+        ntt = {"kernel": "k_ntt_pass<DIT> x3 (coset LDE 2^%d)" % (N.bit_length() - 1),
+               "alg_bytes": 9 * N, "achieved_alg_GBs": 9 * N / t_lde / 1e9,
+               "moved_bytes": moved, "achieved_moved_GBs": moved / t_lde / 1e9,
+               "frac_moved": moved / t_lde / 1e9 / HBM_PEAK_GBS, "ms": t_lde * 1e3}
         whole = {"alg_bytes_per_step": ab["total"], "achieved_GBs": ab["total"] / (dt / args.steps) / 1e9}
         whole["frac"] = whole["achieved_GBs"] / (HBM_PEAK_GBS * world)
         out = {
@@ -148,7 +170,7 @@ def main():
                                    f"b={args.b}, tau={args.tau}, trace resident in HBM",
                        "T": T, "N": N, "tau": args.tau, "b": args.b, "proof_bytes": len(art.proof_bytes),
                        "parallelism": f"replicas x{world} (one independent proof per GPU)"},
-            "roofline": roof, "whole_prove_hbm": whole, "stages_ms": stages,
+            "roofline": roof, "ntt_lde": ntt, "whole_prove_hbm": whole, "stages_ms": stages,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(1 << args.cpu_sample_log_t, args.tau)

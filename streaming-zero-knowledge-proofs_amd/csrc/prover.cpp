@@ -31,8 +31,10 @@ namespace {
 
 constexpr int NUM_QUERIES = 30;  // params.rs:31
 constexpr int BLOWUP_LOG2 = 3;   // params.rs:28
-enum Stage { ST_EXPAND, ST_COMMIT, ST_OUTER, ST_COMPOSE, ST_INTT, ST_LDE, ST_DEEP, ST_L0TREE, ST_FRI, ST_PATHS,
-             ST_OPEN, ST_NSTAGE };
+// ST_L0TREE brackets exactly one launch (k_layer16 over the LDE) so bench.py
+// can quote that kernel's live duration; ST_L0UP holds its upper levels.
+enum Stage { ST_EXPAND, ST_COMMIT, ST_OUTER, ST_COMPOSE, ST_INTT, ST_LDE, ST_DEEP, ST_L0TREE, ST_L0UP, ST_FRI,
+             ST_PATHS, ST_OPEN, ST_NSTAGE };
 
 struct Err {
   int32_t code;
@@ -565,11 +567,13 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   rec(7);
   if (logN >= L16_LOG) {
     ok(launch_layer16(st, d_lde, nullptr, logN, 0, 0, trees[0]), "layer0_tree");
+    rec(ST_L0TREE + 1);
     for (auto& p : jobs0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_upper");
   } else {
     ok(launch_leaf_subtree(st, d_lde, nullptr, logN, 0, 0, trees[0]), "layer0_tree");
+    rec(ST_L0TREE + 1);
   }
-  rec(8);
+  rec(ST_L0UP + 1);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
   sync();
   std::vector<uint8_t> roots((size_t)(k + 1) * 32);
@@ -601,7 +605,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
   HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
   for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
-  rec(9);
+  rec(ST_FRI + 1);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
   sync();
   memcpy(roots.data(), h_small, (size_t)(k + 1) * 32);
@@ -657,10 +661,10 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   }
   HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (2 * max_fri_req + 3 * no) * 4, hipMemcpyHostToDevice, st));
   ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL, d_fri + (N - 2)), "fri_paths");
-  rec(10);
+  rec(ST_PATHS + 1);
   ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 2 * max_fri_req, (int)no, PL),
      "col_open");
-  rec(11);
+  rec(ST_OPEN + 1);
   HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.total, hipMemcpyDeviceToHost, st));
   sync();
   for (int s = 0; s < ST_NSTAGE; s++) {

@@ -343,8 +343,10 @@ __global__ void __launch_bounds__(PW_THREADS) k_col_commit_pw(TraceDev T, const 
   const int lane = threadIdx.x;
   const uint64_t item = (uint64_t)blockIdx.x * PW_THREADS + lane;
   if (item >= (uint64_t)n_pw * nchunks) return;
-  const uint32_t c = pw_cols[item % n_pw];
-  const uint64_t ch = chunks[item / n_pw];
+  // column-major items: a wave holds one column, so its lanes walk the same
+  // number of runs (flag columns cut every block into 2 runs, others do not)
+  const uint32_t c = pw_cols[item / nchunks];
+  const uint64_t ch = chunks[item % nchunks];
   const uint32_t kind = tmpl[c].kind;
   const uint32_t* U = tabs + 8 * tmpl[c].tab;
   const uint64_t n = T.n;
@@ -403,16 +405,19 @@ __global__ void __launch_bounds__(PW_THREADS) k_col_commit_pw(TraceDev T, const 
 __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, uint64_t m0, uint64_t m1, uint64_t m2,
                                                         uint64_t m3, NttTables tw, int logn, uint64_t* __restrict__ out) {
   const uint64_t n = T.n;
-  const uint64_t i0 = ((uint64_t)blockIdx.x * TR_THREADS + threadIdx.x) * 4;
+  // lane rows i0 + 256 j (j < 4): every load/store instruction covers 64
+  // consecutive rows (coalesced), row i+1 shares the neighbour's cache line
+  const uint64_t i0 = (uint64_t)blockIdx.x * TR_THREADS * 4 + threadIdx.x;
   if (i0 >= n) return;
-  // x = w_n^i0, then incremental
-  const uint64_t e0 = i0 << (tw.K - logn), e1 = 1ULL << (tw.K - logn);
+  // x = w_n^i0, then x *= w_n^256
+  const uint64_t e0 = i0 << (tw.K - logn), e1 = (uint64_t)TR_THREADS << (tw.K - logn);
   const uint64_t smask = (1ULL << tw.S) - 1;
   uint64_t x = gl_mul(tw.hi[e0 >> tw.S], tw.lo[e0 & smask]);
-  const uint64_t wn = gl_mul(tw.hi[e1 >> tw.S], tw.lo[e1 & smask]);
-  const int cnt = n - i0 < 4 ? (int)(n - i0) : 4;
-  for (int j = 0; j < cnt; j++) {
-    const uint64_t i = i0 + j;
+  const uint64_t e1m = e1 & ((tw.K >= 64) ? ~0ULL : ((1ULL << tw.K) - 1));
+  const uint64_t wn = gl_mul(tw.hi[e1m >> tw.S], tw.lo[e1m & smask]);
+  for (int j = 0; j < 4; j++) {
+    const uint64_t i = i0 + (uint64_t)j * TR_THREADS;
+    if (i >= n) break;
     const uint64_t ip1 = (i + 1) & (n - 1);
     const uint8_t fl = T.row_flags[i];
     const bool is_first = fl & 1, is_last = (fl >> 1) & 1;

@@ -15,7 +15,7 @@ from ._lib import SEZKP_FLAG_STREAMING, Buf, SezkpError, check, lib, take_buf
 from .blocks import BlockSoA
 
 STAGES = ["expand", "col_commit", "col_outer", "compose", "intt", "lde_ntt", "deep", "layer0_tree",
-          "fri_fold_trees", "fri_paths", "col_openings", "total",
+          "layer0_upper", "fri_fold_trees", "fri_paths", "col_openings", "total",
           # host-side split of the same prove() call (wall clock)
           "host_wall", "host_sync_wait", "host_final_wait", "host_serialize"]
 
@@ -124,8 +124,8 @@ class ProverContext:
         return ProofArtifact("stark", bytes(manifest_root), proof, _meta(proof, self.tau, streaming))
 
     def stage_times_ms(self) -> dict:
-        buf = (C.c_double * 16)()
-        n = lib.sezkp_ctx_stage_times(self._h, buf, 16)
+        buf = (C.c_double * 32)()
+        n = lib.sezkp_ctx_stage_times(self._h, buf, 32)
         return {STAGES[i]: buf[i] for i in range(min(n, len(STAGES)))}
 
     @property
