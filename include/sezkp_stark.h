@@ -94,11 +94,37 @@ int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_
                         char* err, size_t err_len);
 /* Per-stage device times (ms) of the last prove, measured with HIP events on
  * the context's stream. Order: expand, col_commit, col_outer, compose, intt,
- * lde_ntt, deep, layer0_tree, fri_fold_trees, fri_paths, col_openings, total.
- * Returns the number of stages written. */
+ * lde_ntt, deep, layer0_tree, layer0_upper, fri_fold_trees, fri_paths,
+ * col_openings, total, then host wall / sync-wait / final-wait / serialize.
+ * Returns the number of values written. */
 int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max);
 /* Device hipStream_t of the context (as void*), for external timing. */
 void* sezkp_ctx_stream(const sezkp_ctx* ctx);
+
+/* ------------------------------------------------ sharded proving (one proof, P GPUs)
+ * One process per GPU; every rank uploads the same blocks and calls prove()
+ * with the same manifest root; every rank returns the identical proof bytes.
+ * P must be a power of two <= 8 with n >= 4096 * P rows. The LDE domain is
+ * split into P cosets (no communication), one all-to-all moves it to a run
+ * layout (rank d owns indices i with (i mod 4096P) / 4096 == d), Merkle
+ * leaves are hashed per GPU and the tree caps are built from allgathered
+ * subtree roots. Replaces nothing in the reference (its prover
+ * is single-threaded); the ProvingBackend shim calls it when a communicator
+ * is configured. */
+/* ncclUniqueId of a new RCCL communicator (rank 0 creates, the caller broadcasts). */
+int32_t sezkp_comm_unique_id(uint8_t out[128], char* err, size_t err_len);
+sezkp_ctx* sezkp_ctx_create_sharded(int32_t device, int32_t rank, int32_t world, const uint8_t unique_id[128],
+                                    char* err, size_t err_len);
+/* The same over caller-provided host collectives (buffers are host memory;
+ * return 0 on success). */
+typedef struct sezkp_host_comm {
+  void* user;
+  int32_t (*allgather)(void* user, const void* send, void* recv, size_t bytes_per_rank);
+  int32_t (*alltoall)(void* user, const void* send, void* recv, size_t bytes_per_rank);
+  int32_t (*allreduce_sum_u8)(void* user, void* buf, size_t bytes);
+} sezkp_host_comm;
+sezkp_ctx* sezkp_ctx_create_sharded_host(int32_t device, int32_t rank, int32_t world, const sezkp_host_comm* comm,
+                                         char* err, size_t err_len);
 
 /* ------------------------------------------------ kernel-level entry points
  * Device pointers (u64 canonical Goldilocks, natural order), 32-byte digests,

@@ -1,0 +1,102 @@
+// comm.cpp — RCCL and host-callback implementations of sezkp::Comm.
+//
+// RCCL: one communicator per process (one process per GPU), collectives on
+// the prover's stream; with xGMI point-to-point links the exchanges are
+// ring/direct per-link bound, so the prover sends few, large messages
+// (one all-to-all of the LDE, one allgather per commitment step).
+#include "comm.h"
+
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <stdexcept>
+
+namespace sezkp {
+
+namespace {
+
+void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct RcclComm final : Comm {
+  ncclComm_t c = nullptr;
+  RcclComm(int r, int w, const uint8_t uid[128]) {
+    rank = r;
+    world = w;
+    ncclUniqueId id;
+    static_assert(sizeof(id.internal) == 128, "ncclUniqueId size");
+    memcpy(id.internal, uid, 128);
+    nccl_check(ncclCommInitRank(&c, w, id, r), "ncclCommInitRank");
+  }
+  ~RcclComm() override {
+    if (c) (void)ncclCommDestroy(c);
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    nccl_check(ncclAllGather(send, recv, bytes, ncclUint8, c, st), "ncclAllGather");
+  }
+  void alltoall(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    nccl_check(ncclAllToAll(send, recv, bytes, ncclUint8, c, st), "ncclAllToAll");
+  }
+  void allreduce_sum_u8(void* buf, size_t bytes, hipStream_t st) override {
+    nccl_check(ncclAllReduce(buf, buf, bytes, ncclUint8, ncclSum, c, st), "ncclAllReduce");
+  }
+  void group_start() override { nccl_check(ncclGroupStart(), "ncclGroupStart"); }
+  void group_end() override { nccl_check(ncclGroupEnd(), "ncclGroupEnd"); }
+  std::string name() const override { return "rccl"; }
+};
+
+// Device buffers are staged through host memory around each callback.
+struct HostComm final : Comm {
+  sezkp_host_comm cb;
+  std::vector<uint8_t> hs, hr;
+  HostComm(int r, int w, const sezkp_host_comm& c) : cb(c) {
+    rank = r;
+    world = w;
+    if (!cb.allgather || !cb.alltoall || !cb.allreduce_sum_u8) throw std::runtime_error("host comm: null callback");
+  }
+  void d2h(void* h, const void* d, size_t b, hipStream_t st) {
+    hip_check(hipMemcpyAsync(h, d, b, hipMemcpyDeviceToHost, st), "comm D2H");
+    hip_check(hipStreamSynchronize(st), "comm sync");
+  }
+  void h2d(void* d, const void* h, size_t b, hipStream_t st) {
+    hip_check(hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, st), "comm H2D");
+    hip_check(hipStreamSynchronize(st), "comm sync");
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    hs.resize(bytes);
+    hr.resize(bytes * world);
+    d2h(hs.data(), send, bytes, st);
+    if (cb.allgather(cb.user, hs.data(), hr.data(), bytes) != 0) throw std::runtime_error("host comm allgather failed");
+    h2d(recv, hr.data(), bytes * world, st);
+  }
+  void alltoall(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    hs.resize(bytes * world);
+    hr.resize(bytes * world);
+    d2h(hs.data(), send, bytes * world, st);
+    if (cb.alltoall(cb.user, hs.data(), hr.data(), bytes) != 0) throw std::runtime_error("host comm alltoall failed");
+    h2d(recv, hr.data(), bytes * world, st);
+  }
+  void allreduce_sum_u8(void* buf, size_t bytes, hipStream_t st) override {
+    hs.resize(bytes);
+    d2h(hs.data(), buf, bytes, st);
+    if (cb.allreduce_sum_u8(cb.user, hs.data(), bytes) != 0) throw std::runtime_error("host comm allreduce failed");
+    h2d(buf, hs.data(), bytes, st);
+  }
+  std::string name() const override { return "host"; }
+};
+
+}  // namespace
+
+Comm* make_rccl_comm(int rank, int world, const uint8_t unique_id[128]) { return new RcclComm(rank, world, unique_id); }
+Comm* make_host_comm(int rank, int world, const sezkp_host_comm& cb) { return new HostComm(rank, world, cb); }
+void rccl_unique_id(uint8_t out[128]) {
+  ncclUniqueId id;
+  nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  memcpy(out, id.internal, 128);
+}
+
+}  // namespace sezkp

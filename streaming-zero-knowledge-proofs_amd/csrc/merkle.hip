@@ -72,22 +72,23 @@ __device__ __forceinline__ void wg_reduce(uint32_t (*lds)[W], int cnt, int lvl, 
 // workgroup (4096 elements): wave prefix/suffix product scans + one Fermat
 // inversion in lane 0 of wave 0.
 constexpr int DEEP_PER = 16;
-__global__ void __launch_bounds__(MK_THREADS) k_deep(uint64_t* __restrict__ y, int logN, uint64_t z, NttTables T) {
+__global__ void __launch_bounds__(MK_THREADS) k_deep(uint64_t* __restrict__ y, int logN, uint64_t z, NttTables T,
+                                                     int logP, uint32_t g) {
   __shared__ uint64_t wtot[MK_THREADS / 64];
   __shared__ uint64_t s_inv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t i0 = ((uint64_t)blockIdx.x * MK_THREADS + tid) * DEEP_PER;
-  const uint64_t N = 1ULL << logN;
+  const uint64_t N = 1ULL << (logN - logP);  // local length
   const bool act = i0 < N;
   uint64_t d[DEEP_PER], a[DEEP_PER];
   uint64_t P = 1;
   if (act) {
-    // x_i = 3 * w_N^i ; first from the two-level table, then incremental
-    const uint64_t e = i0 << (T.K - logN);
+    // x_j = 3 * w_N^(g + P j) ; first from the two-level table, then incremental
+    const uint64_t e = ((uint64_t)g + (i0 << logP)) << (T.K - logN);
     uint64_t x = gl_mul(gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]), 3);
     uint64_t wN;
     {
-      const uint64_t e1 = 1ULL << (T.K - logN);
+      const uint64_t e1 = 1ULL << (T.K - logN + logP);
       wN = gl_mul(T.hi[e1 >> T.S], T.lo[e1 & ((1ULL << T.S) - 1)]);
     }
 #pragma unroll
@@ -411,56 +412,74 @@ __global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
   wg_reduce(lds, nact, lvl, 0, T);
 }
 
+// ------------------------------------------------ sharded layout changes
+// Rank g of P holds the coset values e[j] = f(3 w_N^(g + P j)), j < M = N/P.
+// Target (run) layout: rank d owns every index i with (i mod P*S) in
+// [d*S, (d+1)*S), S = 4096, stored as runs k1 = i / (P*S) of S consecutive
+// indices. Source j = k1*S + d*(S/P) + t (t < S/P) goes to rank d, slot
+// k1*(S/P) + t of the d-th send segment; on arrival from rank g it lands at
+// local k1*S + P*t + g. Both kernels are one coalesced pass (8 B read + write).
+constexpr uint64_t L16_TILE = 1ULL << L16_LOG;
+__global__ void __launch_bounds__(256) k_cyc_pack(const uint64_t* __restrict__ cyc, uint64_t* __restrict__ send,
+                                                  uint64_t M, int logP) {
+  const uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // send index
+  if (o >= M) return;
+  const int lsp = L16_LOG - logP;                               // log2(S/P)
+  const uint64_t d = o / (M >> logP), r = o % (M >> logP);
+  const uint64_t k1 = r >> lsp, t = r & ((1ULL << lsp) - 1);
+  send[o] = cyc[(k1 << L16_LOG) + (d << lsp) + t];
+}
+__global__ void __launch_bounds__(256) k_cyc_unpack(const uint64_t* __restrict__ recv, uint64_t* __restrict__ local,
+                                                    uint64_t M, int logP) {
+  const uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // recv index
+  if (o >= M) return;
+  const int lsp = L16_LOG - logP;
+  const uint64_t g = o / (M >> logP), r = o % (M >> logP);
+  const uint64_t k1 = r >> lsp, t = r & ((1ULL << lsp) - 1);
+  local[(k1 << L16_LOG) + (t << logP) + g] = recv[o];
+}
+// run roots allgathered as [rank d][run k1] -> cap level L16_LOG node k1*P + d
+__global__ void __launch_bounds__(256) k_runroots_scatter(const uint32_t* __restrict__ gathered, TreeDev cap,
+                                                          uint64_t nrun, int logP) {
+  const uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (o >= (nrun << logP)) return;
+  const uint64_t d = o / nrun, k1 = o % nrun;
+  uint32_t h[8];
+  node_load(gathered + 8 * o, h);
+  store_level(cap, L16_LOG, (k1 << logP) + d, h);
+}
+
 // ---------------------------------------------------------- path extraction
 // One 64-lane workgroup per (layer, index): recompute the 64-leaf group that
 // holds the index (levels < lstore), then read stored siblings above.
 __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict__ layers, const uint32_t* __restrict__ req,
-                                                  ProofLayout P, const uint64_t* __restrict__ final_val) {
+                                                  ProofLayout P) {
   __shared__ uint32_t lds[8][64];
   const int lane = threadIdx.x;
-  const uint32_t q = blockIdx.x;
-  const uint32_t r = req[2 * q];
-  const uint64_t idx = req[2 * q + 1];
+  const uint32_t r = req[3 * blockIdx.x];
+  const uint64_t idx = req[3 * blockIdx.x + 1];
+  const uint32_t ord = req[3 * blockIdx.x + 2];  // q*2k + 2r + side
   const FriLayerDev Ly = layers[r];
   const TreeDev& T = Ly.tree;
-  const int L = T.logLen;
+  const TreeDev& C = Ly.cap;
+  const int L = C.logLen;  // global layer length 2^L
+  // local position of the global index (identity when unsharded)
+  const uint64_t li = Ly.sharded ? (((idx >> (L16_LOG + Ly.logP)) << L16_LOG) | (idx & (L16_TILE - 1))) : idx;
   const int glog = L < T.lstore ? L : T.lstore;
   const uint64_t g = 1ULL << glog;
-  const uint64_t base = idx & ~(g - 1);
-  // FriQuery (proof.rs:68-78): positions then k pairs of (value, path) records
+  const uint64_t base = li & ~(g - 1);
+  // FriQuery (proof.rs:68-78): record = value, u64 path length, siblings
   const int k = P.k;
-  const uint32_t qi = q / (2 * k), side = q & 1;
+  const uint32_t qi = ord / (2 * k), side = ord & 1;
   uint32_t* fq = P.base + (P.fq_off + 8 + (uint64_t)qi * P.fq_bytes) / 4;
   const uint64_t off_r = 2 * (16 * (uint64_t)r + 32 * ((uint64_t)r * k - (uint64_t)r * (r - 1) / 2));
   uint32_t* o = fq + (8 + 8 * (uint64_t)(k + 1) + 8 + off_r + side * (16 + 32 * (uint64_t)L)) / 4;
   if (lane == 0) {
-    const uint64_t v = Ly.vals[idx];
+    const uint64_t v = Ly.vals[li];
     o[0] = (uint32_t)v;
     o[1] = (uint32_t)(v >> 32);
     o[2] = (uint32_t)L;
     o[3] = 0;
-    if (r == 0 && side == 0) {  // query header: k+1 positions (prover.rs:390-393)
-      fq[0] = (uint32_t)(k + 1);
-      fq[1] = 0;
-      uint64_t p = idx, len = 1ULL << k;
-      for (int j = 0; j <= k; j++) {
-        fq[2 + 2 * j] = (uint32_t)p;
-        fq[3 + 2 * j] = (uint32_t)(p >> 32);
-        len >>= 1;
-        if (len) p %= len;
-      }
-      fq[2 + 2 * (k + 1)] = (uint32_t)k;
-      fq[3 + 2 * (k + 1)] = 0;
-    }
-    if (q == 0) {
-      uint32_t* f0 = P.base + P.fq_off / 4;
-      f0[0] = P.nq;
-      f0[1] = 0;
-      uint32_t* t = P.base + P.tail_off / 4;
-      const uint64_t fv = *final_val;
-      t[0] = (uint32_t)fv;
-      t[1] = (uint32_t)(fv >> 32);
-    }
   }
   if (lane < (int)g) {
     uint32_t h[8];
@@ -470,7 +489,7 @@ __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict_
   __syncthreads();
   int cnt = (int)g;
   for (int lvl = 0; lvl < glog; lvl++) {
-    const int sib = (int)(((idx - base) >> lvl) ^ 1);
+    const int sib = (int)(((li - base) >> lvl) ^ 1);
     if (lane < 8) o[4 + 8 * lvl + lane] = lds[lane][sib];
     const int half = cnt >> 1;
     uint32_t h[8];
@@ -486,17 +505,43 @@ __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict_
     cnt = half;
   }
   for (int lvl = glog; lvl < L; lvl++) {
-    const uint64_t sib = (idx >> lvl) ^ 1;
-    if (lane < 8) o[4 + 8 * lvl + lane] = T.nodes[8 * (tree_level_off(L, T.lstore, lvl) + sib) + lane];
+    uint32_t s;
+    if (lvl < C.lstore) {  // inside this rank's run subtree (local tree)
+      const uint64_t sib = (li >> lvl) ^ 1;
+      s = T.nodes[8 * (tree_level_off(T.logLen, T.lstore, lvl) + sib) + (lane & 7)];
+    } else {               // cap levels (global indices)
+      const uint64_t sib = (idx >> lvl) ^ 1;
+      s = C.nodes[8 * (tree_level_off(C.logLen, C.lstore, lvl) + sib) + (lane & 7)];
+    }
+    if (lane < 8) o[4 + 8 * lvl + lane] = s;
   }
 }
 
 // ------------------------------------------------------------------ host
-hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw) {
-  const uint64_t N = 1ULL << logN;
+hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw, int logP, uint32_t g) {
+  if (logP > logN) return hipErrorInvalidValue;
+  const uint64_t N = 1ULL << (logN - logP);
   const uint64_t per_wg = (uint64_t)MK_THREADS * DEEP_PER;
   const unsigned grid = (unsigned)((N + per_wg - 1) / per_wg);
-  hipLaunchKernelGGL(k_deep, dim3(grid), dim3(MK_THREADS), 0, st, y, logN, z, tw);
+  hipLaunchKernelGGL(k_deep, dim3(grid), dim3(MK_THREADS), 0, st, y, logN, z, tw, logP, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_cyc_pack(hipStream_t st, const uint64_t* cyc, uint64_t* send, uint64_t M, int logP) {
+  if (M % L16_TILE || (1 << logP) > (int)L16_TILE) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cyc_pack, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, cyc, send, M, logP);
+  return hipGetLastError();
+}
+hipError_t launch_cyc_unpack(hipStream_t st, const uint64_t* recv, uint64_t* local, uint64_t M, int logP) {
+  if (M % L16_TILE || (1 << logP) > (int)L16_TILE) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cyc_unpack, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, recv, local, M, logP);
+  return hipGetLastError();
+}
+hipError_t launch_runroots_scatter(hipStream_t st, const uint32_t* gathered, TreeDev cap, uint64_t nrun_per_rank,
+                                   int logP) {
+  const uint64_t total = nrun_per_rank << logP;
+  hipLaunchKernelGGL(k_runroots_scatter, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, gathered, cap,
+                     nrun_per_rank, logP);
   return hipGetLastError();
 }
 
@@ -594,10 +639,10 @@ hipError_t launch_tree_upper(hipStream_t st, TreeDev* trees, int ntrees, uint64_
 }
 
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
-                            const ProofLayout& P, const uint64_t* final_val) {
+                            const ProofLayout& P) {
   if (nreq == 0) return hipSuccess;
-  if ((uint64_t)nreq != (uint64_t)P.nq * 2 * P.k) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_fri_paths, dim3(nreq), dim3(64), 0, st, d_layers, d_req, P, final_val);
+  if ((uint64_t)nreq > (uint64_t)P.nq * 2 * P.k) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fri_paths, dim3(nreq), dim3(64), 0, st, d_layers, d_req, P);
   return hipGetLastError();
 }
 

@@ -70,10 +70,11 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(NttPassArgs P) {
       pos = tile * (uint64_t)nel + q;
     }
     uint64_t v;
-    if (P.src) {  // LDE replicated load: B[8k+s] = A[k] * n^-1 * 3^bitrev(k)
-      uint64_t k = pos >> 3;
+    if (P.src) {  // LDE replicated load: B[2^skip k + s] = A[k] * n^-1 * (3 w^g)^bitrev(k)
+      uint64_t k = pos >> P.skip;
       uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;
       v = gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk));
+      if (P.coset_e) v = gl_mul(v, tw_pow(T, ((uint64_t)rk * P.coset_e) & ((1ULL << T.K) - 1), false));
     } else {
       v = P.a[pos];
     }
@@ -192,18 +193,18 @@ hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
 // replicated, scaled coefficients (LDE) and skips the 3 stages replication
 // makes trivial (blowup 8).
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
-                   const uint64_t* src, int log_src, uint64_t inv_n) {
+                   const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e) {
   if (logN == 0) return hipSuccess;
   int ms[8], np;
   plan_passes(logN, src ? 3 : 1, ms, &np);
   // DIT order: smallest strides first; ensure the first pass holds >= 3 stages for the LDE skip
-  if (src && ms[0] < 3) return hipErrorInvalidValue;
+  if (src && ms[0] < logN - log_src) return hipErrorInvalidValue;
   int sL = 0;
   for (int i = 0; i < np; i++) {
     NttPassArgs P{};
     P.a = a; P.tw = T; P.m = ms[i]; P.sL = sL; P.inverse = inverse ? 1 : 0;
     P.src = (i == 0) ? src : nullptr;
-    P.log_src = log_src; P.inv_n = inv_n;
+    P.log_src = log_src; P.inv_n = inv_n; P.coset_e = (i == 0) ? coset_e : 0;
     P.skip = (i == 0 && src) ? (logN - log_src) : 0;
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
     uint64_t tiles = (1ULL << logN) >> (P.m + logC);

@@ -22,6 +22,7 @@
 
 #include "../../include/sezkp_stark.h"
 #include "codec.h"
+#include "comm.h"
 #include "host_crypto.h"
 #include "sezkp_internal.h"
 
@@ -169,8 +170,23 @@ struct sezkp_ctx {
   uint64_t* d_base = nullptr;
   uint64_t* d_lde = nullptr;
   uint64_t* d_fri = nullptr;
-  std::vector<TreeDev> trees;
   uint32_t* d_roots = nullptr;
+  // ---- sharding: one proof over `world` GPUs (world == 1: the whole prover
+  // on this device; every sharded quantity below degenerates to it)
+  int rank = 0, world = 1, logP = 0;
+  std::unique_ptr<Comm> comm;
+  uint64_t M = 0;                       // local LDE length N / P
+  int logM = 0;
+  int rR = -1;                          // run layers 0..rR (len >= 4096 P), the rest replicated
+  uint64_t ch_lo = 0, ch_hi = 0;        // this rank's column chunks
+  uint64_t* d_cyc = nullptr;            // P > 1: coset values f(3 w^(rank + P j))
+  uint64_t* d_xbuf = nullptr;           // P > 1: all-to-all send buffer
+  uint64_t* d_rep = nullptr;            // replicated layers (P > 1: first the whole layer rR)
+  std::vector<uint64_t*> lvals;         // per FRI layer: this rank's values
+  std::vector<TreeDev> ltrees, caps;    // per FRI layer: local tree, cap (== local tree unless sharded)
+  std::vector<uint32_t*> rr_gather;     // P > 1, per run layer: allgathered run roots [P][runs]
+  std::vector<int> rep16;               // replicated layers with >= 4096 leaves (P > 1)
+  int tail_first = 1;                   // first layer of the small-layer tail kernel
   FriLayerDev* d_layers = nullptr;
   ForestLayer* d_forest = nullptr;
   int n_forest = 0;
@@ -350,6 +366,17 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   // chunks whose rows cross few block boundaries go to the piecewise kernel;
   // the rest (many short blocks) are committed densely for every column
   const uint64_t nchunks = 1ULL << logChunks, chunk_rows = n < 1024 ? n : 1024;
+  // sharded: this rank commits chunks [ch_lo, ch_hi) of every column
+  if (world > 1) {
+    if (logn < 12 + logP || logP > 3)
+      throw Err{SEZKP_E_INVALID, "sharded proving needs n >= 4096 * P rows and P <= 8 (n = " + std::to_string(n) +
+                                     ", P = " + std::to_string(world) + ")"};
+    ch_lo = (nchunks >> logP) * rank;
+    ch_hi = ch_lo + (nchunks >> logP);
+  } else {
+    ch_lo = 0;
+    ch_hi = nchunks;
+  }
   std::vector<uint32_t> work, pw_chunks;
   std::vector<uint8_t> dense_chunk(nchunks, 0);
   {
@@ -360,6 +387,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
       int inside = 0;
       for (uint32_t j = k; j < nblk && v.step_start[j] < c1; j++)
         if (j == 0 || v.step_start[j] != v.step_start[j - 1]) inside++;
+      if (ch < ch_lo || ch >= ch_hi) continue;
       if (inside <= 16) pw_chunks.push_back((uint32_t)ch);
       else dense_chunk[ch] = 1;
     }
@@ -367,7 +395,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   for (int c = 0; c < ncols; c++) {
     if (use_dict && kind_dict(tm[c].kind)) continue;
     const bool pw = kind_piecewise(tm[c].kind);
-    for (uint64_t ch = 0; ch < nchunks; ch++)
+    for (uint64_t ch = ch_lo; ch < ch_hi; ch++)
       if (!pw || dense_chunk[ch]) { work.push_back((uint32_t)c); work.push_back((uint32_t)ch); }
   }
   d_tmpl = dalloc<ColTemplate>(ncols);
@@ -398,47 +426,92 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   d_colroots = dalloc<uint32_t>((size_t)ncols * 8);
 
   // ---- LDE / FRI workspace
-  d_base = dalloc<uint64_t>(n);
-  d_lde = dalloc<uint64_t>(N);
-  d_fri = dalloc<uint64_t>(N);
+  // Layer r has 2^(k-r) leaves. Run layers (r <= rR, >= 4096 P leaves) are
+  // held as this rank's runs of 4096 (all of it when P = 1); the remaining
+  // small layers are replicated on every rank.
   const int k = logN;
-  trees.assign(k + 1, TreeDev{});
+  const uint64_t S = 1ULL << L16_LOG;
+  d_base = dalloc<uint64_t>(n);
+  M = N >> logP;
+  logM = logN - logP;
+  rR = world > 1 ? k - L16_LOG - logP : (k >= L16_LOG ? k - L16_LOG : -1);
+  d_lde = dalloc<uint64_t>(M);
+  if (world > 1) {
+    d_cyc = dalloc<uint64_t>(M);
+    d_xbuf = dalloc<uint64_t>(M);
+  }
+  lvals.assign(k + 1, nullptr);
+  ltrees.assign(k + 1, TreeDev{});
+  caps.assign(k + 1, TreeDev{});
+  rr_gather.assign(k + 1, nullptr);
+  uint64_t run_vals = 0, rep_vals = world > 1 ? (S << logP) : 0;
+  for (int r = 1; r <= k; r++) {
+    if (r <= rR) run_vals += (N >> r) >> logP;
+    else rep_vals += N >> r;
+  }
+  d_fri = dalloc<uint64_t>(run_vals + 1);
+  d_rep = dalloc<uint64_t>(rep_vals + 1);
+  d_roots = dalloc<uint32_t>((size_t)(k + 2) * 8);
+  uint32_t* root_dummy = d_roots + 8 * (k + 1);
   uint64_t total_nodes = 0;
-  for (int r = 0; r <= k; r++) total_nodes += tree_stored_nodes(k - r, LSTORE_FRI);
-  uint32_t* d_nodes = dalloc<uint32_t>(total_nodes * 8 + 8);
-  d_roots = dalloc<uint32_t>((size_t)(k + 1) * 8);
-  std::vector<FriLayerDev> ly(k + 1);
-  uint64_t off = 0;
   for (int r = 0; r <= k; r++) {
-    trees[r].nodes = d_nodes + off * 8;
-    trees[r].root = d_roots + 8 * r;
-    trees[r].logLen = k - r;
-    trees[r].lstore = LSTORE_FRI;
-    off += tree_stored_nodes(k - r, LSTORE_FRI);
-    ly[r].vals = r == 0 ? d_lde : d_fri + (N - (N >> (r - 1)));
-    ly[r].tree = trees[r];
+    const int ll = r <= rR ? k - r - logP : k - r;
+    total_nodes += tree_stored_nodes(ll, LSTORE_FRI);
+    if (world > 1 && r <= rR) total_nodes += tree_stored_nodes(k - r, L16_LOG) + ((N >> r) >> L16_LOG);
+  }
+  uint32_t* d_nodes = dalloc<uint32_t>(total_nodes * 8 + 8);
+  uint64_t off = 0, voff = 0, roff = world > 1 ? (S << logP) : 0;
+  std::vector<FriLayerDev> ly(k + 1);
+  for (int r = 0; r <= k; r++) {
+    const bool run = r <= rR;
+    if (r == 0) lvals[r] = d_lde;
+    else if (run) { lvals[r] = d_fri + voff; voff += (N >> r) >> logP; }
+    else { lvals[r] = d_rep + roff; roff += N >> r; }
+    TreeDev& t = ltrees[r];
+    t.nodes = d_nodes + off * 8;
+    t.logLen = run ? k - r - logP : k - r;
+    t.lstore = LSTORE_FRI;
+    t.root = (run && world > 1) ? root_dummy : d_roots + 8 * r;
+    off += tree_stored_nodes(t.logLen, LSTORE_FRI);
+    caps[r] = t;
+    if (run && world > 1) {
+      TreeDev& c = caps[r];
+      c.nodes = d_nodes + off * 8;
+      c.logLen = k - r;
+      c.lstore = L16_LOG;
+      c.root = d_roots + 8 * r;
+      off += tree_stored_nodes(k - r, L16_LOG);
+      rr_gather[r] = d_nodes + off * 8;
+      off += (N >> r) >> L16_LOG;
+    }
+    ly[r] = FriLayerDev{lvals[r], ltrees[r], caps[r], (uint32_t)(run && world > 1), (uint32_t)logP};
   }
   d_layers = dalloc<FriLayerDev>(k + 1);
   up(d_layers, ly.data(), ly.size());
-  // forest of fold-layer trees with >= 4096 leaves (layers 1 .. k-12)
+  // replicated layers of >= 4096 leaves (P > 1), then the small-layer tail
+  rep16.clear();
+  tail_first = rR + 1 > 1 ? rR + 1 : 1;
+  while (tail_first <= k && k - tail_first >= L16_LOG) rep16.push_back(tail_first++);
+  // forest of the run layers 1..rR (local runs of 4096 leaves per WG)
   {
     std::vector<ForestLayer> fl;
     uint32_t wgs = 0;
-    for (int r = 1; r <= k && k - r >= L16_LOG; r++) {
-      fl.push_back(ForestLayer{ly[r].vals, trees[r], wgs, 0});
-      wgs += (uint32_t)(1ULL << (k - r - L16_LOG));
+    for (int r = 1; r <= rR; r++) {
+      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, 0});
+      wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
     }
     n_forest = (int)fl.size();
     forest_wgs = wgs;
     d_forest = dalloc<ForestLayer>(fl.size() + 1);
     if (!fl.empty()) up(d_forest, fl.data(), fl.size());
   }
-  // upper levels (> 12) of the layers built by the 16-leaves-per-lane kernel
+  // upper levels (> 12): layer 0's cap, then every other cap / replicated tree
   {
     std::vector<std::vector<UpperJob>> p0, pF;
-    if (k > L16_LOG) plan_upper_jobs(trees[0], L16_LOG, p0);
+    if (rR >= 0 && caps[0].logLen > L16_LOG) plan_upper_jobs(caps[0], L16_LOG, p0);
     for (int r = 1; r <= k; r++)
-      if (k - r > L16_LOG) plan_upper_jobs(trees[r], L16_LOG, pF);
+      if ((r <= rR || std::find(rep16.begin(), rep16.end(), r) != rep16.end()) && caps[r].logLen > L16_LOG)
+        plan_upper_jobs(caps[r], L16_LOG, pF);
     std::vector<UpperJob> all;
     jobs0.clear();
     jobsF.clear();
@@ -449,8 +522,8 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   }
   max_fri_req = (size_t)NUM_QUERIES * 2 * k;
   max_open_req = (size_t)NUM_QUERIES * (3 + 9 * tau);
-  d_req = dalloc<uint32_t>(max_fri_req * 2 + max_open_req * 3);
-  h_req = halloc<uint32_t>(max_fri_req * 2 + max_open_req * 3);
+  d_req = dalloc<uint32_t>(max_fri_req * 3 + max_open_req * 4);
+  h_req = halloc<uint32_t>(max_fri_req * 3 + max_open_req * 4);
   // ---- proof layout (proof.rs:80-98, bincode fixint LE)
   {
     BinWriter w;
@@ -506,16 +579,31 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     if (e != hipSuccess) throw Err{SEZKP_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
   };
 
+  const bool sharded = world > 1;
+  const uint64_t S = 1ULL << L16_LOG;
   rec(0);
-  // ---- column commitments (openings.rs:306-398)
+  // ---- column commitments (openings.rs:306-398): this rank's chunks, then
+  // every rank gathers all chunk roots and builds the outer trees
   ok(launch_expand(st, T), "expand");
   rec(1);
-  ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride),
+  const uint64_t row_lo = n >= 1024 ? ch_lo << COL_CHUNK_LOG2 : 0;
+  const uint64_t row_hi = n >= 1024 ? ch_hi << COL_CHUNK_LOG2 : n;
+  ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
+                        row_hi - row_lo),
      "col_commit_dict");
   ok(launch_col_tables(st, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs), "col_tables");
   ok(launch_col_commit(st, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
   ok(launch_col_commit_pw(st, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
                           outer_stride, d_err), "col_commit_pw");
+  if (sharded) {
+    const size_t bytes = (size_t)(ch_hi - ch_lo) * 32;
+    comm->group_start();
+    for (int c = 0; c < ncols; c++) {
+      uint32_t* lvl0 = d_outer + (size_t)c * outer_stride * 8;
+      comm->allgather(lvl0 + ch_lo * 8, lvl0, bytes, st);
+    }
+    comm->group_end();
+  }
   rec(2);
   TreeDev outer0{d_outer, d_colroots, logChunks, 0};
   ok(launch_tree_upper(st, &outer0, ncols, outer_stride, 8, 0), "col_outer");
@@ -527,7 +615,8 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   std::vector<uint8_t> colroots((uint8_t*)h_small, (uint8_t*)h_small + (size_t)ncols * 32);
   for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
 
-  // ---- transcript prelude + column roots (prover.rs:67-81)
+  // ---- transcript prelude + column roots (prover.rs:67-81); every rank
+  // replays the same transcript, so challenges need no broadcast
   Transcript tr("sezkp-stark/v1");
   tr.absorb("manifest_root", mroot, 32);
   tr.absorb_u64("n", n);
@@ -555,22 +644,39 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     z = hgl_add(z, 1);
   }
 
-  // ---- composition + LDE + DEEP + layer-0 tree (prover.rs:137-189, lde.rs:42-97)
-  ok(launch_compose(st, T, A, mask, tw, logn, d_base), "compose");
+  // ---- composition (this rank's rows, then allgather) + INTT (replicated)
+  ok(launch_compose(st, T, A, mask, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
+  if (sharded) comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st);
   rec(4);
   ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
   rec(5);
+  // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on
+  // 3 w_N^g <w_M> (M = N/P), no communication
   const uint64_t inv_n = hgl_inv(n % GL_P_HOST);
-  ok(ntt_dit(st, d_lde, logN, false, tw, d_base, logn, inv_n), "lde_ntt");
+  uint64_t* lde_out = sharded ? d_cyc : d_lde;
+  const uint64_t coset_e = sharded ? ((uint64_t)rank << (tw.K - logN)) : 0;
+  ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e), "lde_ntt");
   rec(6);
-  ok(launch_deep(st, d_lde, logN, z, tw), "deep");
+  ok(launch_deep(st, lde_out, logN, z, tw, logP, (uint32_t)rank), "deep");
+  if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI
+    ok(launch_cyc_pack(st, d_cyc, d_xbuf, M, logP), "cyc_pack");
+    comm->alltoall(d_xbuf, d_cyc, (size_t)(M >> logP) * 8, st);
+    ok(launch_cyc_unpack(st, d_cyc, d_lde, M, logP), "cyc_unpack");
+  }
   rec(7);
-  if (logN >= L16_LOG) {
-    ok(launch_layer16(st, d_lde, nullptr, logN, 0, 0, trees[0]), "layer0_tree");
+  // ---- layer-0 tree: local runs, then the cap from allgathered run roots
+  if (rR >= 0) {
+    ok(launch_layer16(st, d_lde, nullptr, ltrees[0].logLen, 0, 0, ltrees[0]), "layer0_tree");
     rec(ST_L0TREE + 1);
+    if (sharded) {
+      const uint64_t nrun = M >> L16_LOG;
+      const uint32_t* lv12 = ltrees[0].nodes + 8 * tree_level_off(ltrees[0].logLen, LSTORE_FRI, L16_LOG);
+      comm->allgather(lv12, rr_gather[0], (size_t)nrun * 32, st);
+      ok(launch_runroots_scatter(st, rr_gather[0], caps[0], nrun, logP), "runroots0");
+    }
     for (auto& p : jobs0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_upper");
   } else {
-    ok(launch_leaf_subtree(st, d_lde, nullptr, logN, 0, 0, trees[0]), "layer0_tree");
+    ok(launch_leaf_subtree(st, d_lde, nullptr, logN, 0, 0, ltrees[0]), "layer0_tree");
     rec(ST_L0TREE + 1);
   }
   rec(ST_L0UP + 1);
@@ -580,31 +686,52 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   memcpy(roots.data(), h_small, 32);
   tr.absorb("fri_layer_root", roots.data(), 32);
 
-  // ---- FRI folds + layer trees (prover.rs:192-239)
+  // ---- FRI folds + layer trees (prover.rs:192-239). Folds of run layers are
+  // rank-local (i and i + len/2 share i mod 4096P).
   auto bb = tr.challenge("fri_betas", 8 * (size_t)k);
-  auto layer_vals = [&](int r) { return r == 0 ? d_lde : d_fri + (N - (N >> (r - 1))); };
-  const int r1 = k > L16_LOG ? k - L16_LOG : 0;  // first fold producing a layer of <= 2^11 leaves
-  for (int r = 0; r < r1; r++) {  // fold chain of the big layers (values only)
-    const uint64_t beta = rd64(bb.data() + 8 * r) % GL_P_HOST;
-    ok(launch_fold(st, layer_vals(r), layer_vals(r + 1), logN - r - 1, beta), "fri_fold");
-  }
-  {  // layers of <= 2^11 leaves on the side stream, concurrent with the forest
+  auto beta_of = [&](int r) { return rd64(bb.data() + 8 * r) % GL_P_HOST; };
+  // layers of <= 2^11 leaves: one launch on the side stream, overlapping the
+  // forest / upper levels (its source is the last fold-chain output)
+  auto launch_tail = [&](const uint64_t* src_vals) {
+    if (tail_first > k) return;
     TailArgs ta{};
-    ta.src = layer_vals(r1);
-    ta.Ls = logN - r1 - 1;
+    ta.src = src_vals;
+    ta.Ls = k - tail_first;
     for (int j = 0; j <= ta.Ls; j++) {
-      ta.beta[j] = rd64(bb.data() + 8 * (r1 + j)) % GL_P_HOST;
-      ta.vals[j] = layer_vals(r1 + 1 + j);
-      ta.tree[j] = trees[r1 + 1 + j];
+      ta.beta[j] = beta_of(tail_first - 1 + j);
+      ta.vals[j] = lvals[tail_first + j];
+      ta.tree[j] = ltrees[tail_first + j];
     }
     HIP_OR_THROW(hipEventRecord(ev_fold, st));
     HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
     ok(launch_fri_tail(st2, ta), "fri_tail");
     HIP_OR_THROW(hipEventRecord(ev_tail, st2));
-  }
+  };
+  for (int r = 0; r < rR; r++)
+    ok(launch_fold(st, lvals[r], lvals[r + 1], ltrees[r + 1].logLen, beta_of(r)), "fri_fold");
+  const uint64_t* rep_src = rR >= 0 ? lvals[rR] : d_lde;  // full values of the layer above the replicated ones
+  if (!sharded) launch_tail(rep_src);
   ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
-  HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
+  if (sharded) {  // run roots of layers 1..rR + the whole of layer rR
+    comm->group_start();
+    for (int r = 1; r <= rR; r++) {
+      const uint64_t nrun = (N >> r) >> (L16_LOG + logP);
+      const uint32_t* lv12 = ltrees[r].nodes + 8 * tree_level_off(ltrees[r].logLen, LSTORE_FRI, L16_LOG);
+      comm->allgather(lv12, rr_gather[r], (size_t)nrun * 32, st);
+    }
+    comm->allgather(lvals[rR], d_rep, (size_t)S * 8, st);
+    comm->group_end();
+    for (int r = 1; r <= rR; r++)
+      ok(launch_runroots_scatter(st, rr_gather[r], caps[r], (N >> r) >> (L16_LOG + logP), logP), "runroots");
+    rep_src = d_rep;
+  }
+  for (int r : rep16) {  // replicated layers with >= 4096 leaves: fold + subtrees
+    ok(launch_layer16(st, rep_src, lvals[r], k - r, 1, beta_of(r - 1), ltrees[r]), "fri_rep16");
+    rep_src = lvals[r];
+  }
+  if (sharded) launch_tail(rep_src);
   for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
+  if (tail_first <= k) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
   rec(ST_FRI + 1);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
   sync();
@@ -618,7 +745,8 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   auto fb = tr.challenge("row_queries", 8 * NUM_QUERIES);
   for (int i = 0; i < NUM_QUERIES; i++) frows[i] = rd64(fb.data() + 8 * i) % N;
 
-  // FRI path requests: per query, per layer r < k: (r, i), (r, i ^ half)
+  // FRI path requests (layer, index, ordinal) for the records this rank owns:
+  // run layers by run owner, replicated layers on rank 0
   std::vector<uint64_t> pos((size_t)NUM_QUERIES * (k + 1));
   size_t nf = 0;
   for (int q = 0; q < NUM_QUERIES; q++) {
@@ -627,20 +755,31 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     uint64_t len = N;
     for (int r = 0; r < k; r++) {
       const uint64_t half = len / 2;
-      h_req[2 * nf] = r; h_req[2 * nf + 1] = (uint32_t)p[r]; nf++;
-      h_req[2 * nf] = r; h_req[2 * nf + 1] = (uint32_t)(p[r] ^ half); nf++;
+      for (int side = 0; side < 2; side++) {
+        const uint64_t idx = side ? (p[r] ^ half) : p[r];
+        const int owner = (sharded && r <= rR) ? (int)((idx >> L16_LOG) & (uint64_t)(world - 1)) : 0;
+        if (owner != rank) continue;
+        h_req[3 * nf] = (uint32_t)r;
+        h_req[3 * nf + 1] = (uint32_t)idx;
+        h_req[3 * nf + 2] = (uint32_t)(q * 2 * k + 2 * r + side);
+        nf++;
+      }
       p[r + 1] = p[r] % half;
       len = half;
     }
   }
-  // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66)
-  uint32_t* oreq = h_req + 2 * max_fri_req;
-  size_t no = 0;
+  // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66), rank 0
+  uint32_t* oreq = h_req + 3 * max_fri_req;
+  size_t no = 0, ord = 0;
   auto push_open = [&](int c, uint64_t row) {
-    oreq[3 * no] = (uint32_t)c;
-    oreq[3 * no + 1] = (uint32_t)row;
-    oreq[3 * no + 2] = (uint32_t)(row >> 32);
-    no++;
+    if (rank == 0) {
+      oreq[4 * no] = (uint32_t)c;
+      oreq[4 * no + 1] = (uint32_t)row;
+      oreq[4 * no + 2] = (uint32_t)(row >> 32);
+      oreq[4 * no + 3] = (uint32_t)ord;
+      no++;
+    }
+    ord++;
   };
   for (int q = 0; q < NUM_QUERIES; q++) {
     const uint64_t row = rows[q], ip1 = row + 1 < n ? row + 1 : 0;  // next_wrap
@@ -659,13 +798,16 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     push_open(2, row);  // is_last
     push_open(0, row);  // input_mv
   }
-  HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (2 * max_fri_req + 3 * no) * 4, hipMemcpyHostToDevice, st));
-  ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL, d_fri + (N - 2)), "fri_paths");
+  HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (3 * max_fri_req + 4 * no) * 4, hipMemcpyHostToDevice, st));
+  if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
+  ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL), "fri_paths");
   rec(ST_PATHS + 1);
-  ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 2 * max_fri_req, (int)no, PL),
+  ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 3 * max_fri_req, (int)no, PL),
      "col_open");
+  if (sharded) comm->allreduce_sum_u8(PL.base, PL.total, st);
   rec(ST_OPEN + 1);
   HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.total, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), lvals[k], 8, hipMemcpyDeviceToHost, st));
   sync();
   for (int s = 0; s < ST_NSTAGE; s++) {
     float ms = 0;
@@ -676,12 +818,26 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   stage_ms[ST_NSTAGE] = tot;
   have_times = true;
 
-  // ---- host-known parts of the body: FRI roots, manifest root
+  // ---- host-known parts of the body: counts, query headers, FRI roots,
+  // positions, final value (prover.rs:242-243), manifest root
   const auto t_ser = clk::now();
   uint8_t* body = h_proof + hdr_bytes;
-  const uint64_t kr = (uint64_t)k + 1;
-  memcpy(body + PL.fr_off, &kr, 8);
+  auto put64 = [&](uint64_t at, uint64_t v) { memcpy(body + at, &v, 8); };
+  put64(0, NUM_QUERIES);
+  for (int q = 0; q < NUM_QUERIES; q++) {
+    put64(8 + q * PL.q_bytes, rows[q]);
+    put64(8 + q * PL.q_bytes + 8, tau);
+  }
+  put64(PL.fr_off, (uint64_t)k + 1);
   memcpy(body + PL.fr_off + 8, roots.data(), roots.size());
+  put64(PL.fq_off, NUM_QUERIES);
+  for (int q = 0; q < NUM_QUERIES; q++) {
+    const uint64_t at = PL.fq_off + 8 + q * PL.fq_bytes;
+    put64(at, (uint64_t)k + 1);
+    for (int r = 0; r <= k; r++) put64(at + 8 + 8 * r, pos[(size_t)q * (k + 1) + r]);
+    put64(at + 8 + 8 * (uint64_t)(k + 1), (uint64_t)k);
+  }
+  memcpy(body + PL.tail_off, h_small + 8 * (k + 1), 8);
   memcpy(body + PL.tail_off + 8, mroot, 32);
   const size_t out = hdr_bytes + PL.total;
   const auto t_end = clk::now();
@@ -714,10 +870,16 @@ static void to_buf(const std::vector<uint8_t>& v, sezkp_buf* out) {
 }
 static void to_buf(const std::string& s, sezkp_buf* out) { to_buf(std::vector<uint8_t>(s.begin(), s.end()), out); }
 
-sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len) {
+static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const uint8_t* uid,
+                             const sezkp_host_comm* hc, char* err, size_t err_len) {
   try {
+    if (world < 1 || world > 8 || (world & (world - 1)) || rank < 0 || rank >= world)
+      throw Err{SEZKP_E_INVALID, "world must be a power of two <= 8 and 0 <= rank < world"};
     std::unique_ptr<sezkp_ctx> c(new sezkp_ctx());
     c->device = device;
+    c->rank = rank;
+    c->world = world;
+    c->logP = ilog2((uint64_t)world);
     int cnt = 0;
     HIP_OR_THROW(hipGetDeviceCount(&cnt));
     if (device < 0 || device >= cnt) throw Err{SEZKP_E_DEVICE, "no such HIP device " + std::to_string(device)};
@@ -728,6 +890,13 @@ sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len) {
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     c->tw = tables_for_device(device);
+    if (world > 1) {
+      try {
+        c->comm.reset(hc ? make_host_comm(rank, world, *hc) : make_rccl_comm(rank, world, uid));
+      } catch (const std::exception& e) {
+        throw Err{SEZKP_E_DEVICE, e.what()};
+      }
+    }
     return c.release();
   } catch (const Err& e) {
     set_err(err, err_len, e.msg);
@@ -735,6 +904,35 @@ sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len) {
     set_err(err, err_len, e.what());
   }
   return nullptr;
+}
+
+sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len) {
+  return ctx_create(device, 0, 1, nullptr, nullptr, err, err_len);
+}
+sezkp_ctx* sezkp_ctx_create_sharded(int32_t device, int32_t rank, int32_t world, const uint8_t unique_id[128],
+                                    char* err, size_t err_len) {
+  if (!unique_id && world > 1) {
+    set_err(err, err_len, "null unique id");
+    return nullptr;
+  }
+  return ctx_create(device, rank, world, unique_id, nullptr, err, err_len);
+}
+sezkp_ctx* sezkp_ctx_create_sharded_host(int32_t device, int32_t rank, int32_t world, const sezkp_host_comm* comm,
+                                         char* err, size_t err_len) {
+  if (!comm) {
+    set_err(err, err_len, "null host comm");
+    return nullptr;
+  }
+  return ctx_create(device, rank, world, nullptr, comm, err, err_len);
+}
+int32_t sezkp_comm_unique_id(uint8_t out[128], char* err, size_t err_len) {
+  try {
+    rccl_unique_id(out);
+    return SEZKP_OK;
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+    return SEZKP_E_DEVICE;
+  }
 }
 void sezkp_ctx_destroy(sezkp_ctx* ctx) { delete ctx; }
 

@@ -24,12 +24,13 @@ struct NttPassArgs {
   const uint64_t* src;  // replicated LDE load source (bit-reversed coeffs), or null
   NttTables tw;
   uint64_t inv_n;
+  uint64_t coset_e;  // LDE load: extra factor w_{2^K}^(coset_e * bitrev(k)) (sharded coset), 0 = none
   int m, sL, logC, inverse, skip, log_src;
 };
 
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
-                   const uint64_t* src, int log_src, uint64_t inv_n);
+                   const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e = 0);
 hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale,
                           bool do_scale);
 
@@ -140,22 +141,40 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
                              int n_tab_cols, uint64_t tab_entries, uint32_t* tabs);
 hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_work,
                              int nwork, const uint32_t* tabs, uint32_t* outer_nodes, uint64_t outer_stride_nodes);
+// rows [row0, row0 + nrows) of every dictionary column (row0, nrows multiples of 4096 or the whole trace)
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes);
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows);
 hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);
+// rows [row0, row0 + nrows) (nrows = n for the whole trace)
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
-                          const NttTables& tw, int logn, uint64_t* out);
-hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw);
+                          const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows);
+// DEEP divide of y[j] at x = 3 * w_{2^logN}^(g + (j << logP)) (logP = 0, g = 0: natural layout)
+hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw, int logP = 0,
+                       uint32_t g = 0);
+// Sharded LDE layout change (see prover.cpp, prove_sharded): cyclic coset
+// values of rank g (index g + P*j) <-> runs of S = 2^12 consecutive indices.
+hipError_t launch_cyc_pack(hipStream_t st, const uint64_t* cyc, uint64_t* send, uint64_t M, int logP);
+hipError_t launch_cyc_unpack(hipStream_t st, const uint64_t* recv, uint64_t* local, uint64_t M, int logP);
+// gathered[d][k1] (run roots of rank d) -> level-12 node k1*P + d of `cap`
+hipError_t launch_runroots_scatter(hipStream_t st, const uint32_t* gathered, TreeDev cap, uint64_t nrun_per_rank,
+                                   int logP);
 hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold,
                                uint64_t beta, TreeDev tree);
 hipError_t launch_tree_upper(hipStream_t st, TreeDev* trees, int ntrees_same_shape, uint64_t tree_stride_nodes,
                              uint64_t root_stride_words, int from_level);
+// A FRI layer as seen by the path kernel. Unsharded: vals/tree hold the
+// whole layer and cap == tree. Sharded run layers: vals/tree are this rank's
+// runs (global index i -> local ((i >> (12+logP)) << 12) | (i & 4095), tree
+// levels < 12 valid) and cap holds levels >= 12 with global indices.
 struct FriLayerDev {
   const uint64_t* vals;
   TreeDev tree;
+  TreeDev cap;
+  uint32_t sharded;
+  uint32_t logP;
 };
 // Upper-level reduction job: one WG reduces <= 1024 stored nodes of `tree`
 // from level `from` (WG index wg within that level).
@@ -191,8 +210,10 @@ struct TailArgs {
   TreeDev tree[TAIL_MAX];
 };
 hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a);
+// requests: (layer, index, ordinal in the proof's FRI records) triples
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
-                            const ProofLayout& P, const uint64_t* final_val);
+                            const ProofLayout& P);
+// requests: (column, row lo, row hi, ordinal in the proof's openings) quadruples
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
                            const ProofLayout& P);

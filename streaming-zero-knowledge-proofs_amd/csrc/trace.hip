@@ -403,12 +403,13 @@ __global__ void __launch_bounds__(PW_THREADS) k_col_commit_pw(TraceDev T, const 
 // alpha*flg*sum(b(b-1)) term is identically zero and is skipped; the bit
 // reconstructions equal x & 0xFFFF / x & 0xF of the canonical value.
 __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, uint64_t m0, uint64_t m1, uint64_t m2,
-                                                        uint64_t m3, NttTables tw, int logn, uint64_t* __restrict__ out) {
+                                                        uint64_t m3, NttTables tw, int logn, uint64_t* __restrict__ out,
+                                                        uint64_t row0, uint64_t row_end) {
   const uint64_t n = T.n;
   // lane rows i0 + 256 j (j < 4): every load/store instruction covers 64
   // consecutive rows (coalesced), row i+1 shares the neighbour's cache line
-  const uint64_t i0 = (uint64_t)blockIdx.x * TR_THREADS * 4 + threadIdx.x;
-  if (i0 >= n) return;
+  const uint64_t i0 = row0 + (uint64_t)blockIdx.x * TR_THREADS * 4 + threadIdx.x;
+  if (i0 >= row_end) return;
   // x = w_n^i0, then x *= w_n^256
   const uint64_t e0 = i0 << (tw.K - logn), e1 = (uint64_t)TR_THREADS << (tw.K - logn);
   const uint64_t smask = (1ULL << tw.S) - 1;
@@ -417,7 +418,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
   const uint64_t wn = gl_mul(tw.hi[e1m >> tw.S], tw.lo[e1m & smask]);
   for (int j = 0; j < 4; j++) {
     const uint64_t i = i0 + (uint64_t)j * TR_THREADS;
-    if (i >= n) break;
+    if (i >= row_end) break;
     const uint64_t ip1 = (i + 1) & (n - 1);
     const uint8_t fl = T.row_flags[i];
     const bool is_first = fl & 1, is_last = (fl >> 1) & 1;
@@ -475,9 +476,10 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
                                                          int logChunks, const uint32_t* __restrict__ req,
                                                          ProofLayout P) {
   __shared__ uint32_t lds[8][1024];
-  const uint32_t q = blockIdx.x;
-  const int c = req[3 * q];
-  const uint64_t row = (uint64_t)req[3 * q + 1] | ((uint64_t)req[3 * q + 2] << 32);
+  const uint32_t* rq = req + 4 * (uint64_t)blockIdx.x;
+  const int c = rq[0];
+  const uint64_t row = (uint64_t)rq[1] | ((uint64_t)rq[2] << 32);
+  const uint32_t q = rq[3];  // ordinal of this opening in the proof
   const ColTemplate ct = tmpl[c];
   const int tid = threadIdx.x;
   const uint64_t n = T.n;
@@ -493,8 +495,6 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
   uint32_t* o = qb + (16 + (uint64_t)s * P.open_bytes) / 4;
   const uint64_t in = row - start;
   if (tid == 0) {
-    if (q == 0) { P.base[0] = P.nq; P.base[1] = 0; }
-    if (s == 0) { qb[0] = (uint32_t)row; qb[1] = (uint32_t)(row >> 32); qb[2] = P.tau; qb[3] = 0; }
     o[2] = (uint32_t)row; o[3] = (uint32_t)(row >> 32);
     o[4] = (uint32_t)ch; o[5] = (uint32_t)(ch >> 32);
     o[6] = (uint32_t)in; o[7] = 0;
@@ -665,13 +665,14 @@ constexpr int DICT_RANGE_ROWS = TR_THREADS * 16;                     // rows per
 // per-(column, 4096 rows) min / max of the raw integers
 __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                            const DictCol* __restrict__ dcols,
-                                                           int64_t* __restrict__ part, uint32_t nparts) {
+                                                           int64_t* __restrict__ part, uint32_t nparts,
+                                                           uint64_t row0, uint64_t row_end) {
   __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
   const ColTemplate ct = tmpl[dcols[blockIdx.y].col];
   const int tid = threadIdx.x;
-  const uint64_t r0 = (uint64_t)blockIdx.x * DICT_RANGE_ROWS + (uint64_t)tid * 16;
+  const uint64_t r0 = row0 + (uint64_t)blockIdx.x * DICT_RANGE_ROWS + (uint64_t)tid * 16;
   int64_t lo = INT64_MAX, hi = INT64_MIN;
-  if (r0 < T.n) {
+  if (r0 < row_end) {
     int64_t k[16];
     switch (ct.kind) {
       case 0: case 3: load_keys<int8_t, 16>(dict_keys<int8_t>(T, ct) + r0, k); break;
@@ -797,7 +798,7 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
                                                         const DictCol* __restrict__ dcols,
                                                         const DictPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ tabs, uint32_t* __restrict__ outer,
-                                                        uint64_t outer_stride) {
+                                                        uint64_t outer_stride, uint64_t row0) {
   __shared__ uint32_t lds[8][64];
   const DictCol dc = dcols[blockIdx.y];
   const ColTemplate* ctp = tmpl + dc.col;
@@ -805,15 +806,16 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
   const DictPlan P = plans[blockIdx.y];
   const uint32_t* tab = tabs + 8 * dc.tab;
   const int lane = threadIdx.x;
-  const uint64_t row0 = (uint64_t)blockIdx.x * DICT_WG_ROWS + ((uint64_t)lane << DICT_LANE_LOG);
-  const bool act = row0 < T.n;
+  const uint64_t wg_row = row0 + (uint64_t)blockIdx.x * DICT_WG_ROWS;
+  const uint64_t lrow = wg_row + ((uint64_t)lane << DICT_LANE_LOG);
+  const bool act = lrow < T.n;
   if (act) {
     uint32_t h[8];
     switch (ct.kind) {
-      case 0: case 3: dict_lane<int8_t>(dict_keys<int8_t>(T, ct) + row0, P, tab, ctp, h); break;
-      case 4: dict_lane<uint8_t>(dict_keys<uint8_t>(T, ct) + row0, P, tab, ctp, h); break;
-      case 5: dict_lane<uint16_t>(dict_keys<uint16_t>(T, ct) + row0, P, tab, ctp, h); break;
-      default: dict_lane<int64_t>(dict_keys<int64_t>(T, ct) + row0, P, tab, ctp, h); break;
+      case 0: case 3: dict_lane<int8_t>(dict_keys<int8_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      case 4: dict_lane<uint8_t>(dict_keys<uint8_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      case 5: dict_lane<uint16_t>(dict_keys<uint16_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      default: dict_lane<int64_t>(dict_keys<int64_t>(T, ct) + lrow, P, tab, ctp, h); break;
     }
 #pragma unroll
     for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
@@ -843,7 +845,7 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
   // chunk i of this WG: rows [blockIdx.x*4096 + 1024 i, +1024)
   const uint64_t nch = T.n >> COL_CHUNK_LOG2;
   const int q = lane >> 3, w = lane & 7;
-  const uint64_t ch = (uint64_t)blockIdx.x * 4 + q;
+  const uint64_t ch = (wg_row >> COL_CHUNK_LOG2) + q;
   if (q < 4 && ch < nch) outer[(uint64_t)dc.col * outer_stride * 8 + ch * 8 + w] = lds[w][q];
 }
 
@@ -862,11 +864,13 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
 }
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes) {
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows) {
   if (ndict == 0) return hipSuccess;
   if (T.n < (1ULL << COL_CHUNK_LOG2)) return hipErrorInvalidValue;
-  const uint32_t nparts = (uint32_t)((T.n + DICT_RANGE_ROWS - 1) / DICT_RANGE_ROWS);
-  hipLaunchKernelGGL(k_dict_range, dim3(nparts, ndict), dim3(TR_THREADS), 0, st, T, d_tmpl, d_dcols, d_part, nparts);
+  if (row0 + nrows > T.n || (nrows != T.n && (row0 % DICT_WG_ROWS || nrows % DICT_WG_ROWS))) return hipErrorInvalidValue;
+  const uint32_t nparts = (uint32_t)((nrows + DICT_RANGE_ROWS - 1) / DICT_RANGE_ROWS);
+  hipLaunchKernelGGL(k_dict_range, dim3(nparts, ndict), dim3(TR_THREADS), 0, st, T, d_tmpl, d_dcols, d_part, nparts,
+                     row0, row0 + nrows);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_plans);
@@ -876,9 +880,9 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
                        d_plans, d_dtabs, l);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  const unsigned gx = (unsigned)((T.n + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
+  const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
   hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
-                     outer_nodes, outer_stride_nodes);
+                     outer_nodes, outer_stride_nodes, row0);
   return hipGetLastError();
 }
 
@@ -899,18 +903,20 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
   return hipGetLastError();
 }
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
-                          const NttTables& tw, int logn, uint64_t* out) {
-  const uint64_t thr = (T.n + 3) / 4;
+                          const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows) {
+  if (row0 + nrows > T.n) return hipErrorInvalidValue;
+  const uint64_t thr = (nrows + 3) / 4;
   const unsigned grid = (unsigned)((thr + TR_THREADS - 1) / TR_THREADS);
+  if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(k_compose, dim3(grid), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3], tw,
-                     logn, out);
+                     logn, out, row0, row0 + nrows);
   return hipGetLastError();
 }
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
                            const ProofLayout& P) {
   if (nreq == 0) return hipSuccess;
-  if ((uint64_t)nreq != (uint64_t)P.nq * P.open_per_q) return hipErrorInvalidValue;
+  if ((uint64_t)nreq > (uint64_t)P.nq * P.open_per_q) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_col_open, dim3(nreq), dim3(TR_THREADS), 0, st, T, d_tmpl, outer_nodes, outer_stride_nodes,
                      logChunks, d_req, P);
   return hipGetLastError();

@@ -5,8 +5,8 @@ C ABI in include/sezkp_stark.h. All compute runs in lib/libsezkp_stark.so
 (HIP kernels for gfx950); importing fails loudly when it is not built.
 """
 from ._lib import LIB_PATH, SezkpError, lib  # noqa: F401  (raises ImportError if the .so is missing)
-from .backend import STAGES, ProofArtifact, ProverContext, StarkV1  # noqa: F401
+from .backend import STAGES, ProofArtifact, ProverContext, ShardedProverContext, StarkV1  # noqa: F401
 from .blocks import BlockSoA, partition, simulate, synthetic_blocks  # noqa: F401
 
-__all__ = ["StarkV1", "ProverContext", "ProofArtifact", "BlockSoA", "SezkpError", "simulate", "partition",
+__all__ = ["StarkV1", "ProverContext", "ShardedProverContext", "ProofArtifact", "BlockSoA", "SezkpError", "simulate", "partition",
            "synthetic_blocks", "STAGES", "LIB_PATH", "lib"]

@@ -26,6 +26,7 @@ EXPORTS = [
     "sezkp_ctx_upload", "sezkp_ctx_prove", "sezkp_ctx_stage_times", "sezkp_ctx_stream", "sezkp_gl_ntt",
     "sezkp_gl_coset_lde_deep", "sezkp_fri_fold_commit", "sezkp_merkle_root_u64", "sezkp_manifest_root",
     "sezkp_blocks_decode_cbor", "sezkp_blocks_view", "sezkp_blocks_free", "sezkp_blake3",
+    "sezkp_comm_unique_id", "sezkp_ctx_create_sharded", "sezkp_ctx_create_sharded_host",
 ]
 
 
@@ -46,6 +47,17 @@ VIEW_FIELDS = [
     ("step_start", C.c_uint64), ("input_mv", C.c_int8), ("mv", C.c_int8), ("has_write", C.c_uint8),
     ("wsym", C.c_uint16),
 ]
+
+
+# host collectives for sezkp_ctx_create_sharded_host (buffers are host memory)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+ALLTOALL_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_void_p, C.c_size_t)
+
+
+class HostComm(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("allgather", ALLGATHER_FN), ("alltoall", ALLTOALL_FN),
+                ("allreduce_sum_u8", ALLREDUCE_FN)]
 
 
 class BlockView(C.Structure):
@@ -81,6 +93,11 @@ def _load():
     L.sezkp_blocks_view.argtypes = [C.c_void_p]
     L.sezkp_blocks_free.argtypes = [C.c_void_p]
     L.sezkp_blake3.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+    L.sezkp_comm_unique_id.argtypes = [C.c_char_p] + E
+    L.sezkp_ctx_create_sharded.restype = C.c_void_p
+    L.sezkp_ctx_create_sharded.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_char_p] + E
+    L.sezkp_ctx_create_sharded_host.restype = C.c_void_p
+    L.sezkp_ctx_create_sharded_host.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.POINTER(HostComm)] + E
     return L
 
 

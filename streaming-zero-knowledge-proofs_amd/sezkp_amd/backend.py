@@ -109,6 +109,7 @@ class ProverContext:
         if not self._h:
             raise SezkpError(-2, err.value.decode())
         self.tau = 0
+        self.rank, self.world = 0, 1
 
     def upload(self, blocks: BlockSoA) -> None:
         err = C.create_string_buffer(1024)
@@ -142,3 +143,39 @@ class ProverContext:
             self.close()
         except Exception:
             pass
+
+
+class ShardedProverContext(ProverContext):
+    """One STARK v1 proof over `world` GPUs (one process per GPU).
+
+    Every rank uploads the same blocks and calls prove() with the same root;
+    every rank gets the identical proof bytes. comm="rccl": the exchanges run
+    over RCCL (xGMI) inside the library; the communicator id is created on
+    rank 0 and broadcast over the torch.distributed `group`. comm="host":
+    the exchanges are staged through host memory and run over the (gloo)
+    `group` by `sezkp_amd.dist.HostCollectives` — for tests on one GPU.
+    """
+
+    def __init__(self, rank: int, world: int, device: int = 0, comm: str = "rccl", group=None):
+        import torch.distributed as dist
+        err = C.create_string_buffer(1024)
+        self.tau = 0
+        self.rank, self.world = rank, world
+        self._hc = None
+        if comm == "rccl":
+            uid = C.create_string_buffer(128)
+            if rank == 0:
+                check(lib.sezkp_comm_unique_id(uid, err, 1024), err)
+            obj = [bytes(uid.raw)]
+            if world > 1:
+                dist.broadcast_object_list(obj, src=0, group=group)
+            self._h = lib.sezkp_ctx_create_sharded(device, rank, world, obj[0], err, 1024)
+        elif comm == "host":
+            from .dist import HostCollectives
+            self._coll = HostCollectives(group)
+            self._hc = self._coll.c_struct()
+            self._h = lib.sezkp_ctx_create_sharded_host(device, rank, world, C.byref(self._hc), err, 1024)
+        else:
+            raise ValueError(f"unknown comm {comm!r}")
+        if not self._h:
+            raise SezkpError(-2, err.value.decode())
