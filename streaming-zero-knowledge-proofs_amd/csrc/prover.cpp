@@ -174,7 +174,8 @@ struct sezkp_ctx {
   // ---- sharding: one proof over `world` GPUs (world == 1: the whole prover
   // on this device; every sharded quantity below degenerates to it)
   int rank = 0, world = 1, logP = 0;
-  std::unique_ptr<Comm> comm;
+  std::unique_ptr<Comm> comm;            // non-null: the sharded algorithm (also at P = 1, see ctx_create)
+  bool sharded() const { return comm != nullptr; }
   uint64_t M = 0;                       // local LDE length N / P
   int logM = 0;
   int rR = -1;                          // run layers 0..rR (len >= 4096 P), the rest replicated
@@ -367,7 +368,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   // the rest (many short blocks) are committed densely for every column
   const uint64_t nchunks = 1ULL << logChunks, chunk_rows = n < 1024 ? n : 1024;
   // sharded: this rank commits chunks [ch_lo, ch_hi) of every column
-  if (world > 1) {
+  if (sharded()) {
     if (logn < 12 + logP || logP > 3)
       throw Err{SEZKP_E_INVALID, "sharded proving needs n >= 4096 * P rows and P <= 8 (n = " + std::to_string(n) +
                                      ", P = " + std::to_string(world) + ")"};
@@ -434,9 +435,9 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   d_base = dalloc<uint64_t>(n);
   M = N >> logP;
   logM = logN - logP;
-  rR = world > 1 ? k - L16_LOG - logP : (k >= L16_LOG ? k - L16_LOG : -1);
+  rR = sharded() ? k - L16_LOG - logP : (k >= L16_LOG ? k - L16_LOG : -1);
   d_lde = dalloc<uint64_t>(M);
-  if (world > 1) {
+  if (sharded()) {
     d_cyc = dalloc<uint64_t>(M);
     d_xbuf = dalloc<uint64_t>(M);
   }
@@ -444,7 +445,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   ltrees.assign(k + 1, TreeDev{});
   caps.assign(k + 1, TreeDev{});
   rr_gather.assign(k + 1, nullptr);
-  uint64_t run_vals = 0, rep_vals = world > 1 ? (S << logP) : 0;
+  uint64_t run_vals = 0, rep_vals = sharded() ? (S << logP) : 0;
   for (int r = 1; r <= k; r++) {
     if (r <= rR) run_vals += (N >> r) >> logP;
     else rep_vals += N >> r;
@@ -457,10 +458,10 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   for (int r = 0; r <= k; r++) {
     const int ll = r <= rR ? k - r - logP : k - r;
     total_nodes += tree_stored_nodes(ll, LSTORE_FRI);
-    if (world > 1 && r <= rR) total_nodes += tree_stored_nodes(k - r, L16_LOG) + ((N >> r) >> L16_LOG);
+    if (sharded() && r <= rR) total_nodes += tree_stored_nodes(k - r, L16_LOG) + ((N >> r) >> L16_LOG);
   }
   uint32_t* d_nodes = dalloc<uint32_t>(total_nodes * 8 + 8);
-  uint64_t off = 0, voff = 0, roff = world > 1 ? (S << logP) : 0;
+  uint64_t off = 0, voff = 0, roff = sharded() ? (S << logP) : 0;
   std::vector<FriLayerDev> ly(k + 1);
   for (int r = 0; r <= k; r++) {
     const bool run = r <= rR;
@@ -471,10 +472,10 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     t.nodes = d_nodes + off * 8;
     t.logLen = run ? k - r - logP : k - r;
     t.lstore = LSTORE_FRI;
-    t.root = (run && world > 1) ? root_dummy : d_roots + 8 * r;
+    t.root = (run && sharded()) ? root_dummy : d_roots + 8 * r;
     off += tree_stored_nodes(t.logLen, LSTORE_FRI);
     caps[r] = t;
-    if (run && world > 1) {
+    if (run && sharded()) {
       TreeDev& c = caps[r];
       c.nodes = d_nodes + off * 8;
       c.logLen = k - r;
@@ -484,7 +485,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
       rr_gather[r] = d_nodes + off * 8;
       off += (N >> r) >> L16_LOG;
     }
-    ly[r] = FriLayerDev{lvals[r], ltrees[r], caps[r], (uint32_t)(run && world > 1), (uint32_t)logP};
+    ly[r] = FriLayerDev{lvals[r], ltrees[r], caps[r], (uint32_t)(run && sharded()), (uint32_t)logP};
   }
   d_layers = dalloc<FriLayerDev>(k + 1);
   up(d_layers, ly.data(), ly.size());
@@ -579,7 +580,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     if (e != hipSuccess) throw Err{SEZKP_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
   };
 
-  const bool sharded = world > 1;
+  const bool sharded = this->sharded();
   const uint64_t S = 1ULL << L16_LOG;
   rec(0);
   // ---- column commitments (openings.rs:306-398): this rank's chunks, then
@@ -890,7 +891,10 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     c->tw = tables_for_device(device);
-    if (world > 1) {
+    // SEZKP_FORCE_SHARDED=1 runs the sharded algorithm (and its RCCL calls)
+    // with a one-rank communicator: tests it on a single GPU
+    const bool force = uid && getenv("SEZKP_FORCE_SHARDED") != nullptr;
+    if (world > 1 || force) {
       try {
         c->comm.reset(hc ? make_host_comm(rank, world, *hc) : make_rccl_comm(rank, world, uid));
       } catch (const std::exception& e) {

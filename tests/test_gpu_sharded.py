@@ -1,0 +1,115 @@
+"""GPU parity of the sharded (one proof over P GPUs) prover, SURVEY 8(e).
+
+The box has one GPU, so P ranks share it and exchange through
+`HostCollectives` (gloo, host-staged) instead of RCCL; the data path,
+layouts and kernels are the production ones. Every rank must return the
+oracle's proof bytes.
+"""
+import hashlib
+import os
+import socket
+import sys
+
+import pytest
+
+from conftest import ORACLE, PKG
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, T, b, tau, seed, q):
+    sys.path[:0] = [PKG, ORACLE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sezkp_amd
+        blocks = sezkp_amd.synthetic_blocks(T, b, tau, seed)
+        ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
+        ctx.upload(blocks)
+        root = blocks.manifest_root()
+        p1 = ctx.prove(root).proof_bytes
+        p2 = ctx.prove(root).proof_bytes
+        calls = dict(ctx._coll.calls)
+        ctx.close()
+        q.put((rank, hashlib.sha256(p1).hexdigest(), p1 == p2, calls))
+    except Exception as e:
+        q.put((rank, f"ERR {type(e).__name__}: {e}", False, {}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, T, b, tau, seed):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, T, b, tau, seed, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("world,T,b,tau,seed", [
+    (2, 1 << 13, 512, 2, 42),   # smallest legal shard (n = 4096 P)
+    (4, 1 << 14, 512, 3, 7),
+    (2, 1 << 15, 100, 8, 9),    # ragged blocks crossing rank boundaries, tau = 8
+])
+def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau, seed):
+    blocks = product.synthetic_blocks(T, b, tau, seed)
+    want = hashlib.sha256(oracle.prove_v1(blocks, blocks.manifest_root())).hexdigest()
+    res = _run(world, T, b, tau, seed)
+    for rank, digest, repeat_ok, calls in res:
+        assert digest == want, f"rank {rank}: {digest}"
+        assert repeat_ok
+        # per prove: one all-to-all (LDE), one byte-sum (proof body), allgathers
+        assert calls["alltoall"] == 2 and calls["allreduce"] == 2 and calls["allgather"] > 0
+
+
+def test_sharded_context_world1_is_single_gpu(gpu_ok, product, oracle):
+    blocks = product.synthetic_blocks(1 << 12, 512, 2, 3)
+    root = blocks.manifest_root()
+    ctx = product.ShardedProverContext(0, 1, device=0, comm="rccl")
+    ctx.upload(blocks)
+    assert ctx.prove(root).proof_bytes == oracle.prove_v1(blocks, root)
+    ctx.close()
+
+
+def test_sharded_rejects_small_trace(gpu_ok, product):
+    from sezkp_amd.dist import HostCollectives
+    import sezkp_amd._lib as L
+    import ctypes as C
+    hc = HostCollectives(None).c_struct()  # never called: upload fails first
+    err = C.create_string_buffer(1024)
+    h = L.lib.sezkp_ctx_create_sharded_host(0, 0, 2, C.byref(hc), err, 1024)
+    assert h
+    blocks = product.synthetic_blocks(1 << 12, 512, 2, 3)  # n = 4096 < 4096 * 2
+    rc = L.lib.sezkp_ctx_upload(h, C.byref(blocks.view()), err, 1024)
+    L.lib.sezkp_ctx_destroy(h)
+    assert rc == L.SEZKP_E_INVALID and b"n >= 4096 * P" in err.value
+    assert not L.lib.sezkp_ctx_create_sharded_host(0, 0, 3, C.byref(hc), err, 1024)  # world not a power of two
+
+
+@pytest.mark.parametrize("T,b,tau", [(1 << 12, 512, 2), (1 << 15, 200, 8)])
+def test_sharded_algorithm_over_rccl_one_rank(gpu_ok, product, oracle, monkeypatch, T, b, tau):
+    """SEZKP_FORCE_SHARDED runs the sharded algorithm with a one-rank RCCL
+    communicator: every RCCL call (allgather, all-to-all, allreduce) and the
+    run/cap layouts execute on the device, bit-exact with the oracle."""
+    monkeypatch.setenv("SEZKP_FORCE_SHARDED", "1")
+    blocks = product.synthetic_blocks(T, b, tau, 11)
+    root = blocks.manifest_root()
+    ctx = product.ShardedProverContext(0, 1, device=0, comm="rccl")
+    ctx.upload(blocks)
+    assert ctx.prove(root).proof_bytes == oracle.prove_v1(blocks, root)
+    ctx.close()

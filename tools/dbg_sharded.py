@@ -31,7 +31,7 @@ def worker(rank, world, port, args, q):
     try:
         blocks = sezkp_amd.synthetic_blocks(1 << args.log_t, args.b, args.tau, args.seed)
         root = blocks.manifest_root()
-        dev = rank if args.comm == "rccl" else 0
+        dev = rank if (args.comm == "rccl" and not args.same_device) else 0
         ctx = sezkp_amd.ShardedProverContext(rank, world, device=dev, comm=args.comm)
         ctx.upload(blocks)
         t0 = time.perf_counter()
@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--comm", default="host")
     ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("--same-device", action="store_true", help="all ranks on GPU 0 (RCCL may refuse)")
     args = ap.parse_args()
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
