@@ -92,6 +92,10 @@ void sezkp_ctx_destroy(sezkp_ctx* ctx);
 int32_t sezkp_ctx_upload(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len);
 int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, sezkp_buf* proof_bytes,
                         char* err, size_t err_len);
+/* Same proof, borrowed: *data points into the context's pinned host buffer
+ * (valid until the next prove/upload/destroy of this context); no copy. */
+int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags,
+                               const uint8_t** data, size_t* len, char* err, size_t err_len);
 /* Per-stage device times (ms) of the last prove, measured with HIP events on
  * the context's stream. Order: expand, col_commit, col_outer, compose, intt,
  * lde_ntt, deep, layer0_tree, layer0_upper, fri_fold_trees, fri_paths,

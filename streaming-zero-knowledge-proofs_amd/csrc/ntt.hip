@@ -15,6 +15,8 @@
 //   DIF: natural -> bit-reversed order.   DIT: bit-reversed -> natural order.
 // Twiddles: w_{2^K}^e = tw_hi[e >> S] * tw_lo[e & (2^S-1)] (two small tables,
 // L2-resident), inverse uses e -> 2^K - e.
+#include <stdlib.h>
+
 #include "dev_common.h"
 #include "sezkp_internal.h"
 
@@ -129,6 +131,248 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(NttPassArgs P) {
   }
 }
 
+// ------------------------------------------------ four-step register passes
+// A pass of m = M1 + M2 stages as ONE exchange through LDS instead of m
+// LDS round trips: two register-resident radix-2^M FFTs (<= 16 points) whose
+// internal twiddles are powers of w_16 = 2^156 (w_16^-1 = 2^36), i.e. shifts
+// plus one 128->64 reduction instead of general products, and one general
+// twiddle w_{2^m}^(j1*k2) between them (LDS table). Same tile geometry and
+// per-pass twiddle as k_ntt_pass; the two kernels are interchangeable per pass.
+//   DIT (bit-reversed in, natural out): position F1*u + r holds a[j1 + F2*j2],
+//     j1 = rev_M2(u), j2 = rev_M1(r). Step 1 (thread per u): F1-point DIT over
+//     j2 -> Y[j1][k2]; * w^(j1 k2); step 2 (thread per k2): F2-point DIT over
+//     j1 (slot u holds j1 = rev(u)) -> X[k2 + F1*k1].
+//   DIF (natural in, bit-reversed out): step 1 (thread per r): F2-point DIF
+//     over x[F1*u + r] -> slot q holds k_lo = rev_M2(q); * w^(r k_lo);
+//     step 2 (thread per q): F1-point DIF over r -> X[k_lo + F2*k_hi] lands at
+//     position q*F1 + q' (k_hi = rev_M1(q')).
+__device__ __forceinline__ uint64_t gl_neg(uint64_t x) { return x ? GL_P - x : 0; }
+__device__ __forceinline__ uint64_t gl_shl(uint64_t x, int e) {  // x * 2^e mod p, 0 < e < 64
+  return gl_reduce128(x << e, x >> (64 - e));
+}
+// x * 2^e mod p, 0 <= e < 192 (2^96 = -1); e is a compile-time constant after unrolling
+__device__ __forceinline__ uint64_t gl_mul_pow2(uint64_t x, int e) {
+  const bool neg = e >= 96;
+  if (neg) e -= 96;
+  uint64_t r = x;
+  if (e >= 64) {
+    r = gl_shl(r, e / 2);
+    e -= e / 2;
+  }
+  if (e > 0) r = gl_shl(r, e);
+  return neg ? gl_neg(r) : r;
+}
+// x * w_{2h}^j for 2h <= 16
+template <bool INV>
+__device__ __forceinline__ uint64_t tw_small(uint64_t x, int j, int h) {
+  return gl_mul_pow2(x, ((INV ? 36 : 156) * j * (8 / h)) % 192);
+}
+template <int LOGF, bool INV, int SKIP>
+__device__ __forceinline__ void fft_dit_regs(uint64_t (&x)[1 << LOGF]) {
+#pragma unroll
+  for (int s = SKIP; s < LOGF; s++) {
+    const int h = 1 << s;
+#pragma unroll
+    for (int t0 = 0; t0 < (1 << LOGF); t0++) {
+      if (!(t0 & h)) {
+        const int j = t0 & (h - 1);
+        const uint64_t y = j ? tw_small<INV>(x[t0 + h], j, h) : x[t0 + h];
+        const uint64_t a = x[t0];
+        x[t0] = gl_add(a, y);
+        x[t0 + h] = gl_sub(a, y);
+      }
+    }
+  }
+}
+template <int LOGF, bool INV>
+__device__ __forceinline__ void fft_dif_regs(uint64_t (&x)[1 << LOGF]) {
+#pragma unroll
+  for (int s = LOGF - 1; s >= 0; s--) {
+    const int h = 1 << s;
+#pragma unroll
+    for (int t0 = 0; t0 < (1 << LOGF); t0++) {
+      if (!(t0 & h)) {
+        const int j = t0 & (h - 1);
+        const uint64_t a = x[t0], b = x[t0 + h];
+        x[t0] = gl_add(a, b);
+        const uint64_t d = gl_sub(a, b);
+        x[t0 + h] = j ? tw_small<INV>(d, j, h) : d;
+      }
+    }
+  }
+}
+template <int M>
+__device__ __forceinline__ constexpr int rev(int x) {
+  int r = 0;
+  for (int i = 0; i < M; i++) r |= ((x >> i) & 1) << (M - 1 - i);
+  return r;
+}
+
+struct Tile {
+  uint64_t blk_base, low0, tile;
+  int sL, m;
+  bool wide;
+};
+// global position of (sub-transform row t, tile column c); low = its `low` index
+__device__ __forceinline__ uint64_t tile_pos(const Tile& G, int t, int c, uint64_t& low) {
+  if (G.wide) {
+    low = G.low0 + c;
+    return G.blk_base + low + ((uint64_t)t << G.sL);
+  }
+  low = (uint64_t)c & ((1ULL << G.sL) - 1);
+  const uint64_t cb = (uint64_t)c >> G.sL;
+  return G.tile * ((uint64_t)NTT_CMAX << G.m) + (cb << (G.sL + G.m)) + ((uint64_t)t << G.sL) + low;
+}
+
+template <bool DIF, bool INV, int M1, int M2, int SKIP>
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt4(NttPassArgs P) {
+  constexpr int F1 = 1 << M1, F2 = 1 << M2, m = M1 + M2, R = 1 << m;
+  __shared__ uint64_t sh[R * NTT_PADC];
+  __shared__ uint64_t W[R];
+  const int tid = threadIdx.x;
+  const NttTables& T = P.tw;
+  for (int x = tid; x < R; x += NTT_THREADS) W[x] = tw_pow(T, (uint64_t)x << (T.K - m), INV);
+  Tile G;
+  G.sL = P.sL;
+  G.m = m;
+  G.tile = blockIdx.x;
+  G.wide = (1ULL << G.sL) >= (uint64_t)NTT_CMAX;
+  G.blk_base = 0;
+  G.low0 = 0;
+  if (G.wide) {
+    const uint64_t tiles_per_blk = (1ULL << G.sL) / NTT_CMAX;
+    G.blk_base = (G.tile / tiles_per_blk) * ((uint64_t)R << G.sL);
+    G.low0 = (G.tile % tiles_per_blk) * NTT_CMAX;
+  }
+  const int tw_shift = T.K - m - G.sL;
+  const int c = tid & (NTT_CMAX - 1), g = tid / NTT_CMAX;
+  __syncthreads();
+  if constexpr (!DIF) {
+    if (g < F2) {  // step 1: thread (c, u), registers r
+      const int u = g;
+      uint64_t x[F1];
+      uint64_t low = 0;
+      if (P.src) {  // LDE replicated load (first pass, sL = 0, low = 0)
+        const uint64_t p0 = tile_pos(G, F1 * u, c, low);
+#pragma unroll
+        for (int r = 0; r < F1; r += (1 << SKIP)) {
+          const uint64_t k = (p0 + r) >> P.skip;
+          const uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;
+          uint64_t v = gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk));
+          if (P.coset_e) v = gl_mul(v, tw_pow(T, ((uint64_t)rk * P.coset_e) & ((1ULL << T.K) - 1), false));
+#pragma unroll
+          for (int s = 0; s < (1 << SKIP); s++) x[r + s] = v;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < F1; r++) x[r] = P.a[tile_pos(G, F1 * u + r, c, low)];
+        if (low != 0) {  // pre-twiddle w^(low * (j1 + F2 j2)), j2 = rev(r)
+          const int j1 = rev<M2>(u);
+          uint64_t t = tw_pow(T, (low * (uint64_t)j1) << tw_shift, INV);
+          const uint64_t s1 = tw_pow(T, (low * (uint64_t)F2) << tw_shift, INV);
+          uint64_t tw[F1];
+#pragma unroll
+          for (int q = 0; q < F1; q++) {
+            tw[q] = t;
+            t = gl_mul(t, s1);
+          }
+#pragma unroll
+          for (int r = 0; r < F1; r++) x[r] = gl_mul(x[r], tw[rev<M1>(r)]);
+        }
+      }
+      fft_dit_regs<M1, INV, SKIP>(x);
+      const int j1 = rev<M2>(u);
+#pragma unroll
+      for (int k2 = 0; k2 < F1; k2++) {
+        const uint64_t v = k2 && j1 ? gl_mul(x[k2], W[j1 * k2]) : x[k2];
+        sh[(u * F1 + k2) * NTT_PADC + c] = v;
+      }
+    }
+    __syncthreads();
+    if (g < F1) {  // step 2: thread (c, k2), registers u
+      const int k2 = g;
+      uint64_t y[F2];
+#pragma unroll
+      for (int u = 0; u < F2; u++) y[u] = sh[(u * F1 + k2) * NTT_PADC + c];
+      fft_dit_regs<M2, INV, 0>(y);
+      uint64_t low;
+#pragma unroll
+      for (int k1 = 0; k1 < F2; k1++) P.a[tile_pos(G, k2 + F1 * k1, c, low)] = y[k1];
+    }
+  } else {
+    if (g < F1) {  // step 1: thread (c, r), registers u (natural)
+      const int r = g;
+      uint64_t x[F2];
+      uint64_t low;
+#pragma unroll
+      for (int u = 0; u < F2; u++) x[u] = P.a[tile_pos(G, F1 * u + r, c, low)];
+      fft_dif_regs<M2, INV>(x);
+#pragma unroll
+      for (int q = 0; q < F2; q++) {
+        const int klo = rev<M2>(q);
+        const uint64_t v = klo && r ? gl_mul(x[q], W[r * klo]) : x[q];
+        sh[(q * F1 + r) * NTT_PADC + c] = v;
+      }
+    }
+    __syncthreads();
+    if (g < F2) {  // step 2: thread (c, q), registers r
+      const int q = g;
+      uint64_t y[F1];
+#pragma unroll
+      for (int r = 0; r < F1; r++) y[r] = sh[(q * F1 + r) * NTT_PADC + c];
+      fft_dif_regs<M1, INV>(y);
+      uint64_t low;
+      (void)tile_pos(G, q * F1, c, low);
+      if (low != 0) {  // post-twiddle w^(low * (k_lo + F2 k_hi)), k_hi = rev(q')
+        uint64_t t = tw_pow(T, (low * (uint64_t)rev<M2>(q)) << tw_shift, INV);
+        const uint64_t s1 = tw_pow(T, (low * (uint64_t)F2) << tw_shift, INV);
+        uint64_t tw[F1];
+#pragma unroll
+        for (int kh = 0; kh < F1; kh++) {
+          tw[kh] = t;
+          t = gl_mul(t, s1);
+        }
+#pragma unroll
+        for (int qq = 0; qq < F1; qq++) y[qq] = gl_mul(y[qq], tw[rev<M1>(qq)]);
+      }
+#pragma unroll
+      for (int qq = 0; qq < F1; qq++) P.a[tile_pos(G, q * F1 + qq, c, low)] = y[qq];
+    }
+  }
+}
+
+// launch one pass with the register kernel when its shape allows, else false
+template <bool DIF, bool INV>
+static bool launch_ntt4(hipStream_t st, const NttPassArgs& P, unsigned tiles) {
+  if (P.logC != 4) return false;
+  const int skip = P.src ? P.skip : 0;
+  if (DIF && skip) return false;
+#define SEZKP_NTT4(M1, M2, SK) \
+  hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, SK>), dim3(tiles), dim3(NTT_THREADS), 0, st, P)
+  switch (P.m * 4 + skip) {
+    case 8 * 4 + 0: SEZKP_NTT4(4, 4, 0); return true;
+    case 7 * 4 + 0: SEZKP_NTT4(4, 3, 0); return true;
+    case 6 * 4 + 0: SEZKP_NTT4(3, 3, 0); return true;
+    default: break;
+  }
+  if constexpr (!DIF) {
+    switch (P.m * 4 + skip) {
+      case 8 * 4 + 1: SEZKP_NTT4(4, 4, 1); return true;
+      case 8 * 4 + 2: SEZKP_NTT4(4, 4, 2); return true;
+      case 8 * 4 + 3: SEZKP_NTT4(4, 4, 3); return true;
+      case 7 * 4 + 1: SEZKP_NTT4(4, 3, 1); return true;
+      case 7 * 4 + 2: SEZKP_NTT4(4, 3, 2); return true;
+      case 7 * 4 + 3: SEZKP_NTT4(4, 3, 3); return true;
+      case 6 * 4 + 1: SEZKP_NTT4(3, 3, 1); return true;
+      case 6 * 4 + 2: SEZKP_NTT4(3, 3, 2); return true;
+      case 6 * 4 + 3: SEZKP_NTT4(3, 3, 3); return true;
+      default: break;
+    }
+  }
+#undef SEZKP_NTT4
+  return false;
+}
+
 // Out-of-place bit-reversal permutation (optionally scaled), tiled so both the
 // read and the write are 16-element (128-B) row segments:
 // p = x*2^(a+b) + y*2^a + z  ->  rev(z)*2^(a+b) + rev(y)*2^a + rev(x), a = 4.
@@ -164,6 +408,11 @@ __global__ void k_bitrev_permute_small(const uint64_t* __restrict__ in, uint64_t
 }
 
 // ------------------------------------------------------------------ host side
+// SEZKP_NTT_RADIX2=1 forces the radix-2 LDS passes (A/B comparison)
+static bool ntt4_disabled() {
+  static const bool off = getenv("SEZKP_NTT_RADIX2") != nullptr;
+  return off;
+}
 static void plan_passes(int logN, int first_min, int* ms, int* np) {
   int passes = (logN + NTT_MMAX - 1) / NTT_MMAX;
   if (passes < 1) passes = 1;
@@ -184,7 +433,10 @@ hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     P.inverse = inverse ? 1 : 0; P.skip = 0;
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
     uint64_t tiles = (1ULL << logN) >> (P.m + logC);
-    hipLaunchKernelGGL(k_ntt_pass<true>, dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
+    const bool fast = !ntt4_disabled() &&
+                      (inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
+                               : launch_ntt4<true, false>(st, P, (unsigned)tiles));
+    if (!fast) hipLaunchKernelGGL(k_ntt_pass<true>, dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
   }
   return hipGetLastError();
 }
@@ -208,7 +460,10 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     P.skip = (i == 0 && src) ? (logN - log_src) : 0;
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
     uint64_t tiles = (1ULL << logN) >> (P.m + logC);
-    hipLaunchKernelGGL(k_ntt_pass<false>, dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
+    const bool fast = !ntt4_disabled() &&
+                      (inverse ? launch_ntt4<false, true>(st, P, (unsigned)tiles)
+                               : launch_ntt4<false, false>(st, P, (unsigned)tiles));
+    if (!fast) hipLaunchKernelGGL(k_ntt_pass<false>, dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
     sL += ms[i];
   }
   return hipGetLastError();

@@ -974,6 +974,23 @@ int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_
   }
 }
 
+int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, const uint8_t** data,
+                               size_t* len, char* err, size_t err_len) {
+  (void)flags;
+  try {
+    if (!ctx || !manifest_root || !data || !len) throw Err{SEZKP_E_INVALID, "null argument"};
+    *len = ctx->prove(manifest_root);
+    *data = ctx->h_proof;
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+    return SEZKP_E_NOMEM;
+  }
+}
+
 int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max) {
   if (!ctx || !ctx->have_times) return 0;
   int cnt = 0;

@@ -26,7 +26,7 @@ EXPORTS = [
     "sezkp_ctx_upload", "sezkp_ctx_prove", "sezkp_ctx_stage_times", "sezkp_ctx_stream", "sezkp_gl_ntt",
     "sezkp_gl_coset_lde_deep", "sezkp_fri_fold_commit", "sezkp_merkle_root_u64", "sezkp_manifest_root",
     "sezkp_blocks_decode_cbor", "sezkp_blocks_view", "sezkp_blocks_free", "sezkp_blake3",
-    "sezkp_comm_unique_id", "sezkp_ctx_create_sharded", "sezkp_ctx_create_sharded_host",
+    "sezkp_comm_unique_id", "sezkp_ctx_create_sharded", "sezkp_ctx_create_sharded_host", "sezkp_ctx_prove_borrow",
 ]
 
 
@@ -80,6 +80,8 @@ def _load():
     L.sezkp_ctx_destroy.argtypes = [C.c_void_p]
     L.sezkp_ctx_upload.argtypes = [C.c_void_p, C.POINTER(BlockView)] + E
     L.sezkp_ctx_prove.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.POINTER(Buf)] + E
+    L.sezkp_ctx_prove_borrow.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.POINTER(C.POINTER(C.c_uint8)),
+                                         C.POINTER(C.c_size_t)] + E
     L.sezkp_ctx_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int32]
     L.sezkp_ctx_stream.restype = C.c_void_p
     L.sezkp_ctx_stream.argtypes = [C.c_void_p]

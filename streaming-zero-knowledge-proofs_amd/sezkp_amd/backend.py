@@ -124,6 +124,15 @@ class ProverContext:
         proof = take_buf(pb)
         return ProofArtifact("stark", bytes(manifest_root), proof, _meta(proof, self.tau, streaming))
 
+    def prove_view(self, manifest_root: bytes) -> memoryview:
+        """The proof bytes as a read-only view of the context's pinned host
+        buffer (no copy); valid until the next prove/upload/close."""
+        ptr = C.POINTER(C.c_uint8)()
+        n = C.c_size_t()
+        err = C.create_string_buffer(1024)
+        check(lib.sezkp_ctx_prove_borrow(self._h, bytes(manifest_root), 0, C.byref(ptr), C.byref(n), err, 1024), err)
+        return memoryview((C.c_uint8 * n.value).from_address(C.addressof(ptr.contents))).cast("B").toreadonly()
+
     def stage_times_ms(self) -> dict:
         buf = (C.c_double * 32)()
         n = lib.sezkp_ctx_stage_times(self._h, buf, 32)

@@ -215,6 +215,8 @@ def test_prove_full_size_config3(gpu_ok, product, oracle):
     assert art.proof_bytes == oracle.prove_v1(blocks, mroot)
     again = ctx.prove(mroot)  # resident inputs: repeated proofs are deterministic
     assert again.proof_bytes == art.proof_bytes
+    view = ctx.prove_view(mroot)  # borrowed pinned buffer, same bytes
+    assert view.readonly and bytes(view) == art.proof_bytes
 
 
 def test_streaming_meta_and_verify(gpu_ok, product, oracle):
