@@ -423,41 +423,48 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
     const uint8_t fl = T.row_flags[i];
     const bool is_first = fl & 1, is_last = (fl >> 1) & 1;
     const uint32_t blk = T.row_blk[i];
-    uint64_t acc = 0;
+    // Each constraint type shares one alpha across tapes (air.rs:49-136), so
+    // its per-tape terms are summed first (exactly, as integers where they are
+    // small) and multiplied once: sum_r a*t_r = a * sum_r t_r in the field.
+    int64_t s_c2 = 0, s_c3 = 0, s_sy = 0;
+    uint64_t s_hr = 0, s_sl = 0, s_bf = 0, s_bl = 0;
     for (int r = 0; r < T.tau; r++) {
       const uint64_t o = (uint64_t)r * n;
       const int64_t mv = T.mv[o + i];
       const int64_t head = T.head[o + i];
       const uint64_t head_f = gl_from_i64(head);
-      const uint64_t mv_f = gl_from_i64(mv);
       // C2: mv(mv-1)(mv+1) = mv^3 - mv  (|mv| <= 128: exact in i64)
-      const int64_t c2 = mv * mv * mv - mv;
-      if (c2) acc = gl_add(acc, gl_mul(A.mv_domain, gl_from_i64(c2)));
-      // C3: (1 - is_last) * (head' - head - mv')
-      if (!is_last) {
-        const int64_t d = T.head[o + ip1] - head - (int64_t)T.mv[o + ip1];
-        if (d) acc = gl_add(acc, gl_mul(A.head_update, gl_from_i64(d)));
-      }
+      s_c2 += mv * mv * mv - mv;
+      // C3: (1 - is_last) * (head' - head - mv'), |head| <= 128 n
+      if (!is_last) s_c3 += T.head[o + ip1] - head - (int64_t)T.mv[o + ip1];
       if (T.wflag[o + i]) {
         // head - sum(head_bits * 2^k)
-        acc = gl_add(acc, gl_mul(A.head_reconstruct, gl_sub(head_f, head_f & 0xFFFF)));
+        s_hr = gl_add(s_hr, gl_sub(head_f, head_f & 0xFFFF));
         // slack = (win_len - 1) - head, reconstructed from 16 bits
         const uint64_t winlen = T.blk_winlen[(uint64_t)r * T.nblk + blk];
         const uint64_t slack = gl_sub(gl_sub(winlen, 1), head_f);
-        acc = gl_add(acc, gl_mul(A.slack_reconstruct, gl_sub(slack, slack & 0xFFFF)));
+        s_sl = gl_add(s_sl, gl_sub(slack, slack & 0xFFFF));
         // symbol 4-bit decomposition
-        const uint64_t sym = T.wsym[o + i];
-        acc = gl_add(acc, gl_mul(A.sym_reconstruct, sym - (sym & 0xF)));
+        const int64_t sym = T.wsym[o + i];
+        s_sy += sym - (sym & 0xF);
       }
       if (is_first) {
         const uint64_t offin = T.blk_offin[(uint64_t)r * T.nblk + blk];
-        acc = gl_add(acc, gl_mul(A.boundary_first, gl_sub(gl_sub(head_f, mv_f), offin)));
+        s_bf = gl_add(s_bf, gl_sub(gl_sub(head_f, gl_from_i64(mv)), offin));
       }
       if (is_last) {
         const uint64_t offout = T.blk_offout[(uint64_t)r * T.nblk + blk];
-        acc = gl_add(acc, gl_mul(A.boundary_last, gl_sub(head_f, offout)));
+        s_bl = gl_add(s_bl, gl_sub(head_f, offout));
       }
     }
+    uint64_t acc = 0;
+    if (s_c2) acc = gl_mul(A.mv_domain, gl_from_i64(s_c2));
+    if (s_c3) acc = gl_add(acc, gl_mul(A.head_update, gl_from_i64(s_c3)));
+    if (s_hr) acc = gl_add(acc, gl_mul(A.head_reconstruct, s_hr));
+    if (s_sl) acc = gl_add(acc, gl_mul(A.slack_reconstruct, s_sl));
+    if (s_sy) acc = gl_add(acc, gl_mul(A.sym_reconstruct, (uint64_t)s_sy));
+    if (is_first) acc = gl_add(acc, gl_mul(A.boundary_first, s_bf));
+    if (is_last) acc = gl_add(acc, gl_mul(A.boundary_last, s_bl));
     // mask R(x) = m0 + m1 x + m2 x^2 + m3 x^3 (Horner)
     uint64_t R = gl_add(gl_mul(gl_add(gl_mul(gl_add(gl_mul(m3, x), m2), x), m1), x), m0);
     out[i] = gl_add(acc, R);
@@ -755,27 +762,28 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __
                                                            uint32_t* __restrict__ tabs, int lvl) {
   const DictPlan P = plans[blockIdx.y];
   if (lvl > P.K) return;
-  const uint32_t e = blockIdx.x * TR_THREADS + threadIdx.x;
   uint32_t size = 0, S = 0;  // static indices only (no scratch copy of P)
 #pragma unroll
   for (int k = 0; k < DICT_LEVELS; k++) {
     if (k == lvl) size = P.pw[k];
     if (k + 1 == lvl) S = P.pw[k];
   }
-  if (e >= size) return;
   const DictCol dc = dcols[blockIdx.y];
   uint32_t* tl = tabs + 8 * (dc.tab + (uint64_t)lvl * DICT_CAP);
-  uint32_t h[8];
-  if (lvl == 0) {
-    leaf_labeled_rt(tmpl[dc.col], gl_from_i64(P.min + (int64_t)e), h);
-  } else {
-    const uint32_t* tp = tl - 8 * (uint64_t)DICT_CAP;
-    uint32_t a[8], b[8];
-    node_load(tp + 8 * (uint64_t)(e % S), a);
-    node_load(tp + 8 * (uint64_t)(e / S), b);
-    b3_parent(a, b, h);
+  const ColTemplate ct = tmpl[dc.col];
+  for (uint32_t e = blockIdx.x * TR_THREADS + threadIdx.x; e < size; e += gridDim.x * TR_THREADS) {
+    uint32_t h[8];
+    if (lvl == 0) {
+      leaf_labeled_rt(ct, gl_from_i64(P.min + (int64_t)e), h);
+    } else {
+      const uint32_t* tp = tl - 8 * (uint64_t)DICT_CAP;
+      uint32_t a[8], b[8];
+      node_load(tp + 8 * (uint64_t)(e % S), a);
+      node_load(tp + 8 * (uint64_t)(e / S), b);
+      b3_parent(a, b, h);
+    }
+    node_store(tl + 8 * (uint64_t)e, h);
   }
-  node_store(tl + 8 * (uint64_t)e, h);
 }
 
 template <typename Key>
@@ -876,8 +884,9 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
   hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_plans);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   for (int l = 0; l < DICT_LEVELS; l++) {
-    hipLaunchKernelGGL(k_dict_level, dim3(DICT_CAP / TR_THREADS, ndict), dim3(TR_THREADS), 0, st, d_tmpl, d_dcols,
-                       d_plans, d_dtabs, l);
+    // grid-stride: most (column, level) pairs are empty or tiny; 64 WGs per
+    // column still spread a full 65536-entry level over every CU
+    hipLaunchKernelGGL(k_dict_level, dim3(64, ndict), dim3(TR_THREADS), 0, st, d_tmpl, d_dcols, d_plans, d_dtabs, l);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
