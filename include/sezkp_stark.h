@@ -156,8 +156,17 @@ int32_t sezkp_manifest_root(const sezkp_block_view* blocks, uint8_t out[32]);
  * arrays a view points to; free with sezkp_blocks_free. */
 typedef struct sezkp_blocks sezkp_blocks;
 int32_t sezkp_blocks_decode_cbor(const uint8_t* data, size_t len, sezkp_blocks** out, char* err, size_t err_len);
+/* JSON Lines, one BlockSummary per line (crates/sezkp-core/src/io_jsonl.rs:43-84;
+ * an empty line is an error naming its line number), and its writer
+ * (write_block_summaries_jsonl, io_jsonl.rs:93-106). */
+int32_t sezkp_blocks_decode_jsonl(const uint8_t* data, size_t len, sezkp_blocks** out, char* err, size_t err_len);
+int32_t sezkp_blocks_encode_jsonl(const sezkp_block_view* blocks, sezkp_buf* out);
 const sezkp_block_view* sezkp_blocks_view(const sezkp_blocks* b);
 void sezkp_blocks_free(sezkp_blocks* b);
+/* Decode a manifest file (sezkp-merkle commit output: {root: [32], n_leaves}),
+ * CBOR or JSON (is_json != 0). */
+int32_t sezkp_manifest_decode(const uint8_t* data, size_t len, int32_t is_json, uint8_t root[32],
+                              uint32_t* n_leaves, char* err, size_t err_len);
 /* BLAKE3 hash with extendable output (host). */
 void sezkp_blake3(const uint8_t* data, size_t len, uint8_t* out, size_t out_len);
 

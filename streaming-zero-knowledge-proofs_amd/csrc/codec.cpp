@@ -314,6 +314,8 @@ void decode_block(P& d, BlockStore& s, BlockShape& sh) {
   s.step_start.push_back(s.step_start.back() + (s.input_mv.size() - steps_before));
 }
 
+void finish_blocks(BlockStore& s, const BlockShape& sh);
+
 template <class P>
 void decode_blocks(P& d, BlockStore& s) {
   s.step_start.assign(1, 0);
@@ -321,6 +323,10 @@ void decode_blocks(P& d, BlockStore& s) {
   int64_t r = d.begin_array();
   while (d.more(r)) decode_block(d, s, sh);
   if (!d.done()) throw DecodeError("trailing bytes after block array");
+  finish_blocks(s, sh);
+}
+
+void finish_blocks(BlockStore& s, const BlockShape& sh) {
   // The prover reads tau = blocks[0].windows.len() and indexes every per-block
   // vector and every step's tapes by r < tau (openings.rs:195, columns.rs:258).
   s.tau = sh.nwin.empty() ? 0 : sh.nwin[0];
@@ -403,6 +409,90 @@ bool decode_blocks_json(const char* data, size_t len, BlockStore& out, std::stri
     return false;
   }
 }
+// JSON Lines: one BlockSummary object per line (io_jsonl.rs:43-84); a
+// trailing "\r" is trimmed, an empty line is an error naming its line number.
+bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::string& err) {
+  size_t line_no = 0;
+  try {
+    out.step_start.assign(1, 0);
+    BlockShape sh;
+    const char* p = data;
+    const char* e = data + len;
+    while (p < e) {
+      const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(e - p)));
+      const char* end = nl ? nl : e;
+      line_no++;
+      const char* le = end;
+      if (le > p && le[-1] == '\r') le--;
+      if (le == p) throw DecodeError("empty line");
+      Json d(p, (size_t)(le - p));
+      decode_block(d, out, sh);
+      if (!d.done()) throw DecodeError("trailing bytes after the block object");
+      p = nl ? nl + 1 : e;
+    }
+    line_no = 0;
+    finish_blocks(out, sh);
+    return true;
+  } catch (const std::exception& ex) {
+    err = line_no ? "parse jsonl line " + std::to_string(line_no) + ": " + ex.what()
+                  : std::string("deserialize JSONL block summaries: ") + ex.what();
+    return false;
+  }
+}
+
+// write_block_summaries_jsonl (io_jsonl.rs:93-106): serde field order, tags zeroed
+std::string encode_blocks_jsonl(const sezkp_block_view& v) {
+  std::string o;
+  const uint32_t tau = v.tau;
+  o.reserve((size_t)v.step_start[v.n_blocks] * (40 + 28 * tau) + (size_t)v.n_blocks * 400);
+  std::string tag = "[";
+  for (int i = 0; i < 16; i++) tag += i ? ",0" : "0";
+  tag += "]";
+  auto num = [&](long long x) { o += std::to_string(x); };
+  for (uint32_t k = 0; k < v.n_blocks; k++) {
+    o += "{\"version\":"; num(v.version[k]);
+    o += ",\"block_id\":"; num(v.block_id[k]);
+    o += ",\"step_lo\":"; o += std::to_string(v.step_lo[k]);
+    o += ",\"step_hi\":"; o += std::to_string(v.step_hi[k]);
+    o += ",\"ctrl_in\":"; num(v.ctrl_in[k]);
+    o += ",\"ctrl_out\":"; num(v.ctrl_out[k]);
+    o += ",\"in_head_in\":"; num(v.in_head_in[k]);
+    o += ",\"in_head_out\":"; num(v.in_head_out[k]);
+    o += ",\"windows\":[";
+    for (uint32_t r = 0; r < tau; r++) {
+      if (r) o += ",";
+      o += "{\"left\":"; num(v.win_left[(size_t)k * tau + r]);
+      o += ",\"right\":"; num(v.win_right[(size_t)k * tau + r]);
+      o += "}";
+    }
+    o += "],\"head_in_offsets\":[";
+    for (uint32_t r = 0; r < tau; r++) { if (r) o += ","; num(v.off_in[(size_t)k * tau + r]); }
+    o += "],\"head_out_offsets\":[";
+    for (uint32_t r = 0; r < tau; r++) { if (r) o += ","; num(v.off_out[(size_t)k * tau + r]); }
+    o += "],\"movement_log\":{\"steps\":[";
+    for (uint64_t s = v.step_start[k]; s < v.step_start[k + 1]; s++) {
+      if (s != v.step_start[k]) o += ",";
+      o += "{\"input_mv\":"; num(v.input_mv[s]);
+      o += ",\"tapes\":[";
+      for (uint32_t r = 0; r < tau; r++) {
+        const size_t i = (size_t)s * tau + r;
+        if (r) o += ",";
+        o += "{\"write\":";
+        if (v.has_write[i]) num(v.wsym[i]); else o += "null";
+        o += ",\"mv\":"; num(v.mv[i]);
+        o += "}";
+      }
+      o += "]}";
+    }
+    o += "]},\"pre_tags\":[";
+    for (uint32_t r = 0; r < tau; r++) { if (r) o += ","; o += tag; }
+    o += "],\"post_tags\":[";
+    for (uint32_t r = 0; r < tau; r++) { if (r) o += ","; o += tag; }
+    o += "]}\n";
+  }
+  return o;
+}
+
 bool decode_manifest_cbor(const uint8_t* data, size_t len, uint8_t root[32], uint32_t* n_leaves, std::string& err) {
   try {
     Cbor d(data, len);

@@ -27,6 +27,8 @@ struct BlockStore {
 };
 bool decode_blocks_cbor(const uint8_t* data, size_t len, BlockStore& out, std::string& err);
 bool decode_blocks_json(const char* data, size_t len, BlockStore& out, std::string& err);
+bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::string& err);
+std::string encode_blocks_jsonl(const sezkp_block_view& v);
 bool decode_manifest_cbor(const uint8_t* data, size_t len, uint8_t root[32], uint32_t* n_leaves, std::string& err);
 bool decode_manifest_json(const char* data, size_t len, uint8_t root[32], uint32_t* n_leaves, std::string& err);
 

@@ -1134,6 +1134,39 @@ int32_t sezkp_blocks_decode_cbor(const uint8_t* data, size_t len, sezkp_blocks**
   *out = b.release();
   return SEZKP_OK;
 }
+int32_t sezkp_blocks_decode_jsonl(const uint8_t* data, size_t len, sezkp_blocks** out, char* err, size_t err_len) {
+  std::unique_ptr<sezkp_blocks> b(new sezkp_blocks());
+  std::string e;
+  if (!decode_blocks_jsonl(reinterpret_cast<const char*>(data), len, b->s, e)) {
+    set_err(err, err_len, e);
+    return SEZKP_E_DECODE;
+  }
+  *out = b.release();
+  return SEZKP_OK;
+}
+int32_t sezkp_blocks_encode_jsonl(const sezkp_block_view* blocks, sezkp_buf* out) {
+  try {
+    if (!blocks || !out) return SEZKP_E_INVALID;
+    to_buf(encode_blocks_jsonl(*blocks), out);
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    return e.code;
+  } catch (const std::exception&) {
+    return SEZKP_E_NOMEM;
+  }
+}
+int32_t sezkp_manifest_decode(const uint8_t* data, size_t len, int32_t is_json, uint8_t root[32],
+                              uint32_t* n_leaves, char* err, size_t err_len) {
+  if (!data || !root) return SEZKP_E_INVALID;
+  std::string e;
+  const bool ok = is_json ? decode_manifest_json(reinterpret_cast<const char*>(data), len, root, n_leaves, e)
+                          : decode_manifest_cbor(data, len, root, n_leaves, e);
+  if (!ok) {
+    set_err(err, err_len, e);
+    return SEZKP_E_DECODE;
+  }
+  return SEZKP_OK;
+}
 const sezkp_block_view* sezkp_blocks_view(const sezkp_blocks* b) { return b ? &b->s.view : nullptr; }
 void sezkp_blocks_free(sezkp_blocks* b) { delete b; }
 void sezkp_blake3(const uint8_t* data, size_t len, uint8_t* out, size_t out_len) {

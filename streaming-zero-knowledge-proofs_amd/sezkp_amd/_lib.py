@@ -27,6 +27,7 @@ EXPORTS = [
     "sezkp_gl_coset_lde_deep", "sezkp_fri_fold_commit", "sezkp_merkle_root_u64", "sezkp_manifest_root",
     "sezkp_blocks_decode_cbor", "sezkp_blocks_view", "sezkp_blocks_free", "sezkp_blake3",
     "sezkp_comm_unique_id", "sezkp_ctx_create_sharded", "sezkp_ctx_create_sharded_host", "sezkp_ctx_prove_borrow",
+    "sezkp_blocks_decode_jsonl", "sezkp_blocks_encode_jsonl", "sezkp_manifest_decode",
 ]
 
 
@@ -91,6 +92,9 @@ def _load():
     L.sezkp_merkle_root_u64.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p, C.c_void_p]
     L.sezkp_manifest_root.argtypes = [C.POINTER(BlockView), C.c_char_p]
     L.sezkp_blocks_decode_cbor.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p)] + E
+    L.sezkp_blocks_decode_jsonl.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p)] + E
+    L.sezkp_blocks_encode_jsonl.argtypes = [C.POINTER(BlockView), C.POINTER(Buf)]
+    L.sezkp_manifest_decode.argtypes = [C.c_char_p, C.c_size_t, C.c_int32, C.c_char_p, C.POINTER(C.c_uint32)] + E
     L.sezkp_blocks_view.restype = C.POINTER(BlockView)
     L.sezkp_blocks_view.argtypes = [C.c_void_p]
     L.sezkp_blocks_free.argtypes = [C.c_void_p]

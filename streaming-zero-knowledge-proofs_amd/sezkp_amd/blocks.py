@@ -14,7 +14,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import VIEW_FIELDS, BlockView, SezkpError, lib
+from ._lib import VIEW_FIELDS, BlockView, Buf, SezkpError, lib, take_buf
 
 _NP = {C.c_uint16: np.uint16, C.c_uint32: np.uint32, C.c_uint64: np.uint64, C.c_int64: np.int64,
        C.c_int8: np.int8, C.c_uint8: np.uint8}
@@ -56,9 +56,37 @@ class BlockSoA:
     @classmethod
     def from_cbor(cls, data: bytes) -> "BlockSoA":
         """Decode CBOR Vec<BlockSummary> (crates/sezkp-core/src/io.rs:57-65) via the C ABI."""
+        return cls._decode(lib.sezkp_blocks_decode_cbor, data)
+
+    @classmethod
+    def from_jsonl(cls, data: bytes) -> "BlockSoA":
+        """Decode JSON Lines, one BlockSummary per line (io_jsonl.rs:43-84)."""
+        return cls._decode(lib.sezkp_blocks_decode_jsonl, data)
+
+    @classmethod
+    def from_file(cls, path: str) -> "BlockSoA":
+        """.cbor / .jsonl / .ndjson block files (by extension)."""
+        data = open(path, "rb").read()
+        ext = path.rsplit(".", 1)[-1].lower() if "." in path else ""
+        if ext == "cbor":
+            return cls.from_cbor(data)
+        if ext in ("jsonl", "ndjson"):
+            return cls.from_jsonl(data)
+        raise SezkpError(-1, f"unsupported blocks extension: {ext or '(none)'} (supported: .cbor, .jsonl, .ndjson)")
+
+    def to_jsonl(self) -> bytes:
+        """write_block_summaries_jsonl (io_jsonl.rs:93-106) via the C ABI."""
+        b = Buf()
+        rc = lib.sezkp_blocks_encode_jsonl(C.byref(self.view()), C.byref(b))
+        if rc != 0:
+            raise SezkpError(rc, "encode jsonl")
+        return take_buf(b)
+
+    @classmethod
+    def _decode(cls, fn, data: bytes) -> "BlockSoA":
         h = C.c_void_p()
         err = C.create_string_buffer(512)
-        rc = lib.sezkp_blocks_decode_cbor(data, len(data), C.byref(h), err, 512)
+        rc = fn(data, len(data), C.byref(h), err, 512)
         if rc != 0:
             raise SezkpError(rc, err.value.decode())
         try:

@@ -1,0 +1,133 @@
+"""Multi-GPU `prove` launcher (BASELINE config 5: a streaming prove from a
+blocks.jsonl sharded over the GPUs of one node).
+
+    python -m sezkp_amd.launch prove --blocks blocks.jsonl --manifest manifest.cbor \\
+        --out proof.cbor [--stream] [--gpus 8] [--comm rccl|host] [--assume-committed]
+
+Mirrors `sezkp-cli prove --backend stark` (crates/sezkp-cli/src/main.rs:429-527):
+the manifest precheck (main.rs:454-457) unless --assume-committed, then ONE
+proof over all GPUs (`ShardedProverContext`: one process per GPU, RCCL over
+xGMI inside the library), written by rank 0 as the CBOR ProofArtifact
+(io.rs:176-183). Unlike the reference's stark path (io.rs:78-88), .jsonl/.ndjson
+block files are accepted (io_jsonl.rs:43-84), as config 5 requires.
+--gpus 1 runs the single-GPU context. --comm host runs every rank on GPU 0
+with host-staged collectives (tests).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _read_manifest_root(path: str) -> bytes:
+    """Manifest file {root: [32 uints], n_leaves} (sezkp-merkle commit output), .cbor or .json."""
+    import ctypes as C
+    from ._lib import check, lib
+    raw = open(path, "rb").read()
+    root = C.create_string_buffer(32)
+    n = C.c_uint32()
+    err = C.create_string_buffer(512)
+    check(lib.sezkp_manifest_decode(raw, len(raw), int(path.lower().endswith(".json")), root, C.byref(n), err, 512),
+          err)
+    return root.raw
+
+
+def _worker(rank: int, world: int, port: int, args, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from . import ShardedProverContext
+        from .blocks import BlockSoA
+        t0 = time.perf_counter()
+        blocks = BlockSoA.from_file(args.blocks)
+        t_load = time.perf_counter() - t0
+        root = _read_manifest_root(args.manifest)
+        if not args.assume_committed and blocks.manifest_root() != root:
+            raise RuntimeError("manifest root mismatch: blocks do not match the committed manifest")
+        dev = 0 if args.comm == "host" else rank
+        ctx = ShardedProverContext(rank, world, device=dev, comm=args.comm)
+        ctx.upload(blocks)
+        t1 = time.perf_counter()
+        art = ctx.prove(root, streaming=args.stream)
+        t_prove = time.perf_counter() - t1
+        if rank == 0:
+            with open(args.out, "wb") as f:
+                f.write(art.to_cbor())
+        ctx.close()
+        q.put((rank, None, len(art.proof_bytes), t_load, t_prove))
+    except Exception as e:  # reported by the parent
+        q.put((rank, f"{type(e).__name__}: {e}", 0, 0.0, 0.0))
+    finally:
+        dist.destroy_process_group()
+
+
+def prove(args) -> int:
+    if not args.out.lower().endswith(".cbor"):
+        print("error: --out must be a .cbor artifact", file=sys.stderr)
+        return 2
+    if args.gpus == 1 and args.comm == "rccl":
+        from . import ProverContext
+        from .blocks import BlockSoA
+        blocks = BlockSoA.from_file(args.blocks)
+        root = _read_manifest_root(args.manifest)
+        if not args.assume_committed and blocks.manifest_root() != root:
+            print("error: manifest root mismatch", file=sys.stderr)
+            return 1
+        ctx = ProverContext(0)
+        ctx.upload(blocks)
+        art = ctx.prove(root, streaming=args.stream)
+        open(args.out, "wb").write(art.to_cbor())
+        print(json.dumps({"gpus": 1, "proof_bytes": len(art.proof_bytes)}))
+        return 0
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, args.gpus, port, args, q)) for r in range(args.gpus)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=args.timeout) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    errs = [(r, e) for r, e, *_ in res if e]
+    if errs:
+        for r, e in errs:
+            print(f"error: rank {r}: {e}", file=sys.stderr)
+        return 1
+    print(json.dumps({"gpus": args.gpus, "comm": args.comm, "proof_bytes": res[0][2],
+                      "load_s": [round(x[3], 3) for x in res], "prove_s": [round(x[4], 4) for x in res]}))
+    return 0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m sezkp_amd.launch")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("prove")
+    p.add_argument("--backend", default="stark", choices=["stark"])
+    p.add_argument("--blocks", required=True)
+    p.add_argument("--manifest", required=True)
+    p.add_argument("--out", required=True)
+    p.add_argument("--stream", action="store_true")
+    p.add_argument("--assume-committed", action="store_true")
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--comm", default="rccl", choices=["rccl", "host"])
+    p.add_argument("--timeout", type=float, default=1800.0)
+    args = ap.parse_args(argv)
+    return prove(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

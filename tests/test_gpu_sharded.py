@@ -113,3 +113,32 @@ def test_sharded_algorithm_over_rccl_one_rank(gpu_ok, product, oracle, monkeypat
     ctx.upload(blocks)
     assert ctx.prove(root).proof_bytes == oracle.prove_v1(blocks, root)
     ctx.close()
+
+
+@pytest.mark.parametrize("gpus,stream", [(2, False), (1, True)])
+def test_launcher_jsonl_artifact_matches_oracle(gpu_ok, product, oracle, tmp_path, gpus, stream):
+    """Config 5 path: blocks.jsonl -> `python -m sezkp_amd.launch prove` (manifest
+    precheck, one proof over `gpus` ranks) -> CBOR artifact == the oracle's."""
+    import subprocess
+    import cbor_min
+    T, tau = 1 << 13, 2
+    blocks = product.synthetic_blocks(T, 512, tau, 21)
+    root = blocks.manifest_root()
+    (tmp_path / "b.jsonl").write_bytes(blocks.to_jsonl())
+    (tmp_path / "m.cbor").write_bytes(cbor_min.dumps({"root": list(root), "n_leaves": int(blocks.block_id.size)}))
+    cmd = [sys.executable, "-m", "sezkp_amd.launch", "prove", "--blocks", str(tmp_path / "b.jsonl"),
+           "--manifest", str(tmp_path / "m.cbor"), "--out", str(tmp_path / "p.cbor"), "--gpus", str(gpus),
+           "--comm", "host" if gpus > 1 else "rccl"] + (["--stream"] if stream else [])
+    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    meta = {"proto": "stark-v1", "domain_n": 8 * T, "tau": tau}
+    if stream:
+        meta["mode"] = "streaming"
+    want = cbor_min.proof_artifact_cbor("stark", root, oracle.prove_v1(blocks, root), meta)
+    assert (tmp_path / "p.cbor").read_bytes() == want
+    # a manifest that does not match the blocks is refused before proving
+    (tmp_path / "bad.cbor").write_bytes(cbor_min.dumps({"root": [0] * 32, "n_leaves": 1}))
+    bad = cmd[:]
+    bad[bad.index(str(tmp_path / "m.cbor"))] = str(tmp_path / "bad.cbor")
+    r = subprocess.run(bad, cwd=PKG, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 1 and "manifest root mismatch" in r.stderr
