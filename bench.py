@@ -62,8 +62,10 @@ def load_pmc(kernel: str):
         return None
 
 
-def cpu_baseline(T_sample: int, tau: int):
-    """Oracle compute-once prover, 1 thread, on a bounded sample (T_sample rows)."""
+def cpu_baseline(T_sample: int, tau: int, T_mt: int):
+    """The C oracle's compute-once prover on this host: the
+    OpenMP build on the host's cores (`value`, the fair multi-core baseline)
+    and the single-thread build, each on a bounded sample of the workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as O
     from sezkp_amd import synthetic_blocks
@@ -77,11 +79,24 @@ def cpu_baseline(T_sample: int, tau: int):
     # reference-faithful structure repeats the layer-0 LDE pass 1 + 2*30*k times
     t_pass = O.time_lde_pass(blocks, root)
     k = N.bit_length() - 1
-    return {"value": N / dt, "unit": "field-elements/s", "cores": 1, "kind": "port",
-            "sample": f"oracle compute-once prove_v1 (C restatement, 1 thread), T=2^{T_sample.bit_length()-1} "
-                      f"(N=2^{k}), tau={tau}; {dt:.2f} s",
+    single = {"value": N / dt, "cores": 1,
+              "sample": f"oracle compute-once prove_v1, 1 thread, T=2^{T_sample.bit_length()-1} (N=2^{k}), "
+                        f"tau={tau}; {dt:.2f} s"}
+    threads = min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1))
+    used = O.use_mt(threads)
+    bl = synthetic_blocks(T_mt, 512, tau, 42)
+    r = bl.manifest_root()
+    t1 = time.perf_counter()
+    O.prove_v1(bl, r)
+    dt_mt = time.perf_counter() - t1
+    Nm = 8 * T_mt
+    return {"value": Nm / dt_mt, "unit": "field-elements/s", "cores": used, "kind": "port",
+            "sample": f"oracle compute-once prove_v1 (C restatement, OpenMP, {used} threads), "
+                      f"T=2^{T_mt.bit_length()-1} (N=2^{Nm.bit_length()-1}), tau={tau}; {dt_mt:.2f} s",
+            "single_thread": single,
             "reference_faithful_est_elems_per_s": N / (dt + 60 * k * t_pass),
-            "reference_faithful_note": f"+{60*k} layer-0 LDE passes of {t_pass:.3f} s each (prover.rs:312-398)"}
+            "reference_faithful_note": f"1 thread, +{60*k} layer-0 LDE passes of {t_pass:.3f} s each "
+                                       f"(prover.rs:312-398), as the reference runs"}
 
 
 def main():
@@ -93,6 +108,7 @@ def main():
     ap.add_argument("--tau", type=int, default=8)
     ap.add_argument("--b", type=int, default=512)
     ap.add_argument("--cpu-sample-log-t", type=int, default=18)
+    ap.add_argument("--cpu-mt-log-t", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sharded", action="store_true",
                     help="N>1: skip the extra sharded (one proof over all GPUs) measurement")
@@ -192,7 +208,7 @@ def main():
                                        "workspace allocation + trace image over PCIe) + prove; not `value`"},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(1 << args.cpu_sample_log_t, args.tau)
+            out["cpu_baseline"] = cpu_baseline(1 << args.cpu_sample_log_t, args.tau, 1 << args.cpu_mt_log_t)
     ctx.close()
     if world > 1 and not args.no_sharded:
         # ONE proof over all ranks (weak: 2^log_t rows per GPU),

@@ -38,6 +38,18 @@ def build():
     _lib = None
 
 
+def use_mt(threads: int) -> int:
+    """Switch to the OpenMP build of the same source (multi-core compute-once
+    CPU baseline); returns the thread count in use."""
+    global LIB_PATH, _lib
+    LIB_PATH = os.path.join(HERE, "_build", "libsezkp_oracle_mt.so")
+    _lib = None
+    L = lib()
+    L.orc_set_threads.restype = C.c_int
+    L.orc_set_threads.argtypes = [C.c_int]
+    return L.orc_set_threads(threads)
+
+
 _lib = None
 
 

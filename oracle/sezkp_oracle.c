@@ -83,18 +83,20 @@ static void ntt_core(uint64_t *a, size_t n, int inverse) {
         if (inverse) w_len = gl_inv(w_len);          /* ntt.rs:59-74 */
         uint64_t w = 1;
         for (size_t i = 0; i < half; i++) { ws[i] = w; w = gl_mul(w, w_len); }
-        for (size_t j = 0; j < n; j += len) {
-            for (size_t i = 0; i < half; i++) {
-                uint64_t u = a[j + i];
-                uint64_t v = gl_mul(a[j + i + half], ws[i]);
-                a[j + i] = gl_add(u, v);
-                a[j + i + half] = gl_sub(u, v);
-            }
+        /* butterflies of one stage are independent (OpenMP build: cpu_baseline) */
+        #pragma omp parallel for schedule(static) if (n >= 4096)
+        for (size_t t = 0; t < n / 2; t++) {
+            size_t j = (t / half) * len, i = t % half;
+            uint64_t u = a[j + i];
+            uint64_t v = gl_mul(a[j + i + half], ws[i]);
+            a[j + i] = gl_add(u, v);
+            a[j + i + half] = gl_sub(u, v);
         }
     }
     free(ws);
     if (inverse) { /* ntt.rs:151-154 */
         uint64_t inv_n = gl_inv(gl_from_u64((uint64_t)n));
+        #pragma omp parallel for schedule(static) if (n >= 4096)
         for (size_t i = 0; i < n; i++) a[i] = gl_mul(a[i], inv_n);
     }
 }
@@ -105,9 +107,12 @@ void orc_ntt_inverse(uint64_t *a, size_t n) { ntt_core(a, n, 1); }
 void orc_coset_lde(const uint64_t *coeffs, size_t m, uint32_t k_log2, uint64_t shift, uint64_t *out) {
     size_t n = (size_t)1 << k_log2;
     memset(out, 0, n * sizeof(uint64_t));
-    uint64_t pw = 1;
     if (m > n) m = n;
-    for (size_t j = 0; j < m; j++) { out[j] = gl_mul(coeffs[j], pw); pw = gl_mul(pw, shift); }
+    #pragma omp parallel for schedule(static) if (m >= 4096)
+    for (size_t c0 = 0; c0 < m; c0 += 1024) {  /* chunks restart shift^j from shift^c0 */
+        uint64_t pw = gl_pow(shift, c0);
+        for (size_t j = c0; j < m && j < c0 + 1024; j++) { out[j] = gl_mul(coeffs[j], pw); pw = gl_mul(pw, shift); }
+    }
     ntt_core(out, n, 0);
 }
 
@@ -391,6 +396,7 @@ static void mtree_build(mtree *t, const uint8_t *leaves, size_t n) {
         size_t o = po + pl, nl = (pl + 1) / 2;
         t->lvl_off[l] = o;
         t->lvl_len[l] = nl;
+        #pragma omp parallel for schedule(static) if (pl >= 2048)
         for (size_t i = 0; i < pl; i += 2) {
             if (i + 1 < pl) hash2(t->nodes + 32 * (po + i), t->nodes + 32 * (po + i + 1), t->nodes + 32 * (o + i / 2));
             else memcpy(t->nodes + 32 * (o + i / 2), t->nodes + 32 * (po + i), 32);
@@ -817,12 +823,16 @@ static uint64_t *lde_deep(const uint64_t *base_vals, size_t n, unsigned blow_log
     uint64_t *y = (uint64_t *)malloc(N * sizeof(uint64_t));
     orc_coset_lde(coeffs, n, k, shift, y);           /* evaluate_on_coset_pow2 */
     free(coeffs);
-    uint64_t w = gl_root_2exp(k), wp = 1;
-    for (size_t i = 0; i < N; i++) {                 /* lde.rs:80-93 */
-        uint64_t x = gl_mul(shift, wp);
-        uint64_t d = gl_sub(x, z);
-        y[i] = gl_mul(y[i], gl_inv(d));
-        wp = gl_mul(wp, w);
+    uint64_t w = gl_root_2exp(k);
+    #pragma omp parallel for schedule(static) if (N >= 4096)
+    for (size_t c0 = 0; c0 < N; c0 += 1024) {        /* lde.rs:80-93, chunks restart w^i */
+        uint64_t wp = gl_pow(w, c0);
+        for (size_t i = c0; i < N && i < c0 + 1024; i++) {
+            uint64_t x = gl_mul(shift, wp);
+            uint64_t d = gl_sub(x, z);
+            y[i] = gl_mul(y[i], gl_inv(d));
+            wp = gl_mul(wp, w);
+        }
     }
     return y;
 }
@@ -874,6 +884,7 @@ static int prove_front(const orc_blocks *b, const uint8_t mroot[32], prove_state
     tr_absorb_u64(&ps->tr, "tau", tc->tau);
     /* column commitments (prover.rs:75-81) */
     ps->cc = (col_commit *)calloc(tc->ncols, sizeof(col_commit));
+    #pragma omp parallel for schedule(dynamic)
     for (size_t c = 0; c < tc->ncols; c++) commit_column(tc, c, &ps->cc[c]);
     tr_absorb_u64(&ps->tr, "n_cols", tc->ncols);
     for (size_t c = 0; c < tc->ncols; c++) tr_absorb(&ps->tr, "col_root", ps->cc[c].root, 32);
@@ -912,14 +923,18 @@ static int prove_front(const orc_blocks *b, const uint8_t mroot[32], prove_state
     }
     ps->z = z;
     /* base evaluations C(i) + R(ω^i) (prover.rs:142-158) */
-    uint64_t w_base = gl_root_2exp(base_log2), xp = 1;
+    uint64_t w_base = gl_root_2exp(base_log2);
     ps->base_vals = (uint64_t *)malloc(n * sizeof(uint64_t));
-    for (size_t i = 0; i < n; i++) {
-        uint64_t comp = gl_add(compose_row(tc, i, &ps->al), compose_boundary(tc, i, &ps->al));
-        uint64_t m = 0; /* eval_mask_at, Horner (masking.rs:86-92) */
-        for (int j = 3; j >= 0; j--) m = gl_add(gl_mul(m, xp), ps->mask[j]);
-        ps->base_vals[i] = gl_add(comp, gl_add(0, m));
-        xp = gl_mul(xp, w_base);
+    #pragma omp parallel for schedule(static) if (n >= 4096)
+    for (size_t c0 = 0; c0 < n; c0 += 1024) {  /* chunks restart w^i */
+        uint64_t xp = gl_pow(w_base, c0);
+        for (size_t i = c0; i < n && i < c0 + 1024; i++) {
+            uint64_t comp = gl_add(compose_row(tc, i, &ps->al), compose_boundary(tc, i, &ps->al));
+            uint64_t m = 0; /* eval_mask_at, Horner (masking.rs:86-92) */
+            for (int j = 3; j >= 0; j--) m = gl_add(gl_mul(m, xp), ps->mask[j]);
+            ps->base_vals[i] = gl_add(comp, gl_add(0, m));
+            xp = gl_mul(xp, w_base);
+        }
     }
     ps->lde = lde_deep(ps->base_vals, n, 3, 3, z);
     return 0;
@@ -967,11 +982,22 @@ static int prove_impl(const orc_blocks *b, const uint8_t mroot[32], int mode,
     unsigned k = ps.k;
     /* layer-0 root via StreamingLayerBuilder (prover.rs:139-189) */
     uint8_t *leaves0 = (uint8_t *)malloc(32 * N);
-    slb s;
-    slb_init(&s);
-    for (size_t i = 0; i < N; i++) { orc_hash_leaf_u64(ps.lde[i], leaves0 + 32 * i); slb_absorb_leaf(&s, leaves0 + 32 * i); }
+    #pragma omp parallel for schedule(static) if (N >= 4096)
+    for (size_t i = 0; i < N; i++) orc_hash_leaf_u64(ps.lde[i], leaves0 + 32 * i);
     uint8_t *roots = (uint8_t *)malloc(32 * (k + 1));
-    slb_finalize(&s, roots);
+    mtree t0;
+    mtree_build(&t0, leaves0, N);
+    if (mode == 1) {  /* the reference's streaming builder (fri_stream.rs:55-121) */
+        slb s;
+        slb_init(&s);
+        for (size_t i = 0; i < N; i++) slb_absorb_leaf(&s, leaves0 + 32 * i);
+        slb_finalize(&s, roots);
+    } else {          /* compute-once: the same root from the stored tree (a
+                       * power-of-two MerkleTree root equals the streaming
+                       * builder's) */
+        memcpy(roots, mtree_root(&t0), 32);
+    }
+    free(leaves0);
     tr_absorb(&ps.tr, "fri_layer_root", roots, 32);
     /* betas (prover.rs:192-198) */
     size_t n_folds = k;
@@ -984,16 +1010,17 @@ static int prove_impl(const orc_blocks *b, const uint8_t mroot[32], int mode,
     uint64_t **layers = (uint64_t **)calloc(k + 1, sizeof(uint64_t *));
     mtree *trees = (mtree *)calloc(k + 1, sizeof(mtree));
     layers[0] = ps.lde;
-    mtree_build(&trees[0], leaves0, N);
-    free(leaves0);
+    trees[0] = t0;
     size_t cur = N;
     for (size_t r = 0; r < n_folds; r++) {
         size_t half = cur / 2;
         layers[r + 1] = (uint64_t *)malloc(8 * half);
+        #pragma omp parallel for schedule(static) if (half >= 4096)
         for (size_t i = 0; i < half; i++)
             layers[r + 1][i] = gl_add(layers[r][i], gl_mul(betas[r], layers[r][i + half]));
         cur = half;
         uint8_t *lv = (uint8_t *)malloc(32 * cur);
+        #pragma omp parallel for schedule(static) if (cur >= 4096)
         for (size_t i = 0; i < cur; i++) orc_hash_leaf_u64(layers[r + 1][i], lv + 32 * i);
         mtree_build(&trees[r + 1], lv, cur);
         free(lv);
@@ -1123,6 +1150,12 @@ int orc_prove_v1_debug(const orc_blocks *b, const uint8_t mroot[32], uint8_t *co
 }
 
 void orc_free(void *p) { free(p); }
+#ifdef _OPENMP
+#include <omp.h>
+int orc_set_threads(int n) { if (n > 0) omp_set_num_threads(n); return omp_get_max_threads(); }
+#else
+int orc_set_threads(int n) { (void)n; return 1; }
+#endif
 
 double orc_time_lde_pass(const orc_blocks *b, const uint8_t mroot[32]) {
     prove_state ps;

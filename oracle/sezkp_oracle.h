@@ -98,6 +98,8 @@ int orc_prove_v1_debug(const orc_blocks *b, const uint8_t manifest_root[32],
                        uint8_t *col_roots, uint64_t *base_evals, uint64_t *lde_vals,
                        uint8_t *fri_roots, char *err, size_t err_len);
 void orc_free(void *p);
+/* OpenMP threads of the compute-once path (libsezkp_oracle_mt.so); returns the count in use (1 without OpenMP) */
+int orc_set_threads(int n);
 
 /* Time one reference-faithful LDE+layer-0 pass (the unit the reference
  * repeats 1+60k times, prover.rs:312-398); returns seconds. */

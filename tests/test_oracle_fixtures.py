@@ -18,7 +18,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, ROOT
 
 P = 0xFFFFFFFF00000001
 SETS = {"root_blocks": ("ref_blocks.cbor", "ref_manifest.cbor", "ref_proof_stark_v0.cbor"),
@@ -160,3 +160,27 @@ def test_roots_of_unity(oracle):  # lib.rs:268-275
     for k in range(1, 33):
         w = oracle.lib().orc_gl_root_2exp(k)
         assert pow(w, 1 << k, P) == 1 and pow(w, 1 << (k - 1), P) != 1
+
+
+def test_openmp_oracle_matches_single_thread(oracle):
+    """The multi-core CPU baseline (same C source built with OpenMP) emits the
+    single-thread oracle's bytes."""
+    import importlib
+    import subprocess
+    import sys
+    code = ("import sys; sys.path[:0]=[%r,%r]\n"
+            "import hashlib, oracle_ctypes as O, sezkp_amd as S\n"
+            "O.use_mt(4)\n"
+            "for T,b,tau in ((4096,512,8),(8192,100,3)):\n"
+            "    bl=S.synthetic_blocks(T,b,tau,3); print(hashlib.sha256(O.prove_v1(bl, bl.manifest_root())).hexdigest())\n"
+            % (os.path.join(ROOT, "streaming-zero-knowledge-proofs_amd"), os.path.join(ROOT, "oracle")))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-1500:]
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "streaming-zero-knowledge-proofs_amd"))
+    import sezkp_amd as S
+    want = []
+    for T, b, tau in ((4096, 512, 8), (8192, 100, 3)):
+        bl = S.synthetic_blocks(T, b, tau, 3)
+        want.append(hashlib.sha256(oracle.prove_v1(bl, bl.manifest_root())).hexdigest())
+    assert r.stdout.split() == want
