@@ -180,6 +180,7 @@ struct sezkp_ctx {
   int logM = 0;
   int rR = -1;                          // run layers 0..rR (len >= 4096 P), the rest replicated
   uint64_t ch_lo = 0, ch_hi = 0;        // this rank's column chunks
+  uint32_t blk_lo = 0, blk_cnt = 0;     // blocks overlapping this rank's rows (+ the next row)
   uint64_t* d_cyc = nullptr;            // P > 1: coset values f(3 w^(rank + P j))
   uint64_t* d_xbuf = nullptr;           // P > 1: all-to-all send buffer
   uint64_t* d_rep = nullptr;            // replicated layers (P > 1: first the whole layer rR)
@@ -377,6 +378,15 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   } else {
     ch_lo = 0;
     ch_hi = nchunks;
+  }
+  {  // blocks holding rows [ch_lo * 1024, ch_hi * 1024] (the extra row: compose and
+     // next_* openings read row i + 1)
+    const uint64_t r0 = ch_lo * chunk_rows, r1 = std::min<uint64_t>(ch_hi * chunk_rows, n - 1);
+    auto block_of = [&](uint64_t row) {
+      return (uint32_t)(std::upper_bound(v.step_start, v.step_start + nblk + 1, row) - v.step_start - 1);
+    };
+    blk_lo = block_of(r0);
+    blk_cnt = block_of(r1) - blk_lo + 1;
   }
   std::vector<uint32_t> work, pw_chunks;
   std::vector<uint8_t> dense_chunk(nchunks, 0);
@@ -585,14 +595,14 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   rec(0);
   // ---- column commitments (openings.rs:306-398): this rank's chunks, then
   // every rank gathers all chunk roots and builds the outer trees
-  ok(launch_expand(st, T), "expand");
+  ok(launch_expand(st, T, blk_lo, blk_cnt), "expand");
   rec(1);
   const uint64_t row_lo = n >= 1024 ? ch_lo << COL_CHUNK_LOG2 : 0;
   const uint64_t row_hi = n >= 1024 ? ch_hi << COL_CHUNK_LOG2 : n;
   ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
                         row_hi - row_lo),
      "col_commit_dict");
-  ok(launch_col_tables(st, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs), "col_tables");
+  ok(launch_col_tables(st, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
   ok(launch_col_commit(st, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
   ok(launch_col_commit_pw(st, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
                           outer_stride, d_err), "col_commit_pw");
@@ -769,11 +779,13 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
       len = half;
     }
   }
-  // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66), rank 0
+  // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66),
+  // each by the rank owning the row's chunk
   uint32_t* oreq = h_req + 3 * max_fri_req;
   size_t no = 0, ord = 0;
   auto push_open = [&](int c, uint64_t row) {
-    if (rank == 0) {
+    const uint64_t ch = n >= 1024 ? row >> COL_CHUNK_LOG2 : 0;
+    if (ch >= ch_lo && ch < ch_hi) {
       oreq[4 * no] = (uint32_t)c;
       oreq[4 * no + 1] = (uint32_t)row;
       oreq[4 * no + 2] = (uint32_t)(row >> 32);

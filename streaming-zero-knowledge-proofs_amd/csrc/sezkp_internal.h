@@ -136,9 +136,10 @@ struct ProofLayout {
 };
 
 // kernels launched by the host orchestrator (prover.cpp)
-hipError_t launch_expand(hipStream_t st, const TraceDev& T);
+// blocks [blk_lo, blk_lo + blk_cnt) only (a sharded rank's rows + one row of halo)
+hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt);
 hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_tab_cols,
-                             int n_tab_cols, uint64_t tab_entries, uint32_t* tabs);
+                             int n_tab_cols, uint64_t tab_entries, uint32_t* tabs, uint32_t blk_lo, uint32_t blk_cnt);
 hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_work,
                              int nwork, const uint32_t* tabs, uint32_t* outer_nodes, uint64_t outer_stride_nodes);
 // rows [row0, row0 + nrows) of every dictionary column (row0, nrows multiples of 4096 or the whole trace)

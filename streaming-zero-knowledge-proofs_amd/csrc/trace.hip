@@ -21,9 +21,9 @@ constexpr int TR_THREADS = 256;
 // ------------------------------------------------------------ expansion
 // One workgroup per block: row -> block id, first/last flags, and the
 // post-move head prefix sums per tape (head starts at 0 in every block).
-__global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T) {
+__global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) {
   __shared__ int64_t wsum[TR_THREADS / 64];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = b0 + blockIdx.x;
   const uint64_t s = T.blk_start[b], e = T.blk_start[b + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (uint64_t r = s + tid; r < e; r += TR_THREADS) {
@@ -186,9 +186,10 @@ __device__ __forceinline__ void hash4_labeled(const ColTemplate& ct, const uint6
 // per run value computes U_0..U_10 with U_0 = leaf(v), U_{l+1} = H(U_l || U_l),
 // the root of a 2^l-row subtree whose rows all hold v.
 __global__ void __launch_bounds__(TR_THREADS) k_col_tables(TraceDev T, const ColTemplate* __restrict__ tmpl,
-                                                           const uint32_t* __restrict__ cols, uint32_t* __restrict__ tabs) {
+                                                           const uint32_t* __restrict__ cols, uint32_t* __restrict__ tabs,
+                                                           uint32_t blk_lo, uint32_t blk_cnt) {
   const ColTemplate ct = tmpl[cols[blockIdx.y]];
-  const uint64_t i = (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
+  uint64_t i = (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
   uint32_t h[8];
   if (kind_has_leaf_table(ct.kind)) {
     if (i >= (1ULL << ct.tab_log)) return;
@@ -197,8 +198,10 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_tables(TraceDev T, const Col
     node_store(tabs + 8 * (ct.tab + i), h);
     return;
   }
-  const uint64_t units = (ct.kind == 1 || ct.kind == 2) ? 2 : T.nblk;
-  if (i >= units) return;
+  // per-block constants: only blocks [blk_lo, blk_lo + blk_cnt) (this rank's rows)
+  const bool flags = ct.kind == 1 || ct.kind == 2;
+  if (flags ? i >= 2 : i >= blk_cnt) return;
+  if (!flags) i += blk_lo;
   uint64_t v;
   if (ct.kind == 1 || ct.kind == 2) v = i;
   else {
@@ -858,16 +861,19 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
 }
 
 // ------------------------------------------------------------------ host
-hipError_t launch_expand(hipStream_t st, const TraceDev& T) {
-  if (T.nblk == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_expand, dim3(T.nblk), dim3(TR_THREADS), 0, st, T);
+hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt) {
+  if (blk_cnt == 0) return hipSuccess;
+  if ((uint64_t)blk_lo + blk_cnt > T.nblk) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_expand, dim3(blk_cnt), dim3(TR_THREADS), 0, st, T, blk_lo);
   return hipGetLastError();
 }
 hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_tab_cols,
-                             int n_tab_cols, uint64_t max_units, uint32_t* tabs) {
+                             int n_tab_cols, uint64_t max_units, uint32_t* tabs, uint32_t blk_lo, uint32_t blk_cnt) {
   if (n_tab_cols == 0) return hipSuccess;
+  if ((uint64_t)blk_lo + blk_cnt > T.nblk) return hipErrorInvalidValue;
   const unsigned gx = (unsigned)((max_units + TR_THREADS - 1) / TR_THREADS);
-  hipLaunchKernelGGL(k_col_tables, dim3(gx, n_tab_cols), dim3(TR_THREADS), 0, st, T, d_tmpl, d_tab_cols, tabs);
+  hipLaunchKernelGGL(k_col_tables, dim3(gx, n_tab_cols), dim3(TR_THREADS), 0, st, T, d_tmpl, d_tab_cols, tabs, blk_lo,
+                     blk_cnt);
   return hipGetLastError();
 }
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
