@@ -163,6 +163,8 @@ struct sezkp_ctx {
   int64_t* d_dpart = nullptr;
   DictPlan* d_dplans = nullptr;
   uint32_t* d_dtabs = nullptr;
+  uint32_t* d_dlev = nullptr;        // dictionary columns' chunk levels 6..9 (openings)
+  std::vector<uint32_t> dict_of;     // column -> dictionary index or NO_DICT
   uint32_t* d_outer = nullptr;
   uint32_t* d_err = nullptr;  // device-side guard word: non-zero = a kernel saw an out-of-range index
   uint64_t outer_stride = 0;
@@ -423,6 +425,9 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   d_dpart = dalloc<int64_t>(2 * dcols.size() * ((n + 4095) / 4096) + 2);
   d_dplans = dalloc<DictPlan>(dcols.size() + 1);
   d_dtabs = dalloc<uint32_t>(dcols.size() * DICT_LEVELS * DICT_CAP * 8 + 8);
+  d_dlev = dalloc<uint32_t>(dcols.size() * (n >> COL_CHUNK_LOG2) * DLEV_NODES * 8 + 8);
+  dict_of.assign(ncols, NO_DICT);
+  for (size_t i = 0; i < dcols.size(); i++) dict_of[dcols[i].col] = (uint32_t)i;
   n_pw_cols = (int)pw_cols.size();
   d_pw_cols = dalloc<uint32_t>(pw_cols.size() + 1);
   up(d_pw_cols, pw_cols.data(), pw_cols.size());
@@ -533,8 +538,8 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   }
   max_fri_req = (size_t)NUM_QUERIES * 2 * k;
   max_open_req = (size_t)NUM_QUERIES * (3 + 9 * tau);
-  d_req = dalloc<uint32_t>(max_fri_req * 3 + max_open_req * 4);
-  h_req = halloc<uint32_t>(max_fri_req * 3 + max_open_req * 4);
+  d_req = dalloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
+  h_req = halloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
   // ---- proof layout (proof.rs:80-98, bincode fixint LE)
   {
     BinWriter w;
@@ -600,7 +605,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   const uint64_t row_lo = n >= 1024 ? ch_lo << COL_CHUNK_LOG2 : 0;
   const uint64_t row_hi = n >= 1024 ? ch_hi << COL_CHUNK_LOG2 : n;
   ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
-                        row_hi - row_lo),
+                        row_hi - row_lo, d_dlev),
      "col_commit_dict");
   ok(launch_col_tables(st, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
   ok(launch_col_commit(st, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
@@ -786,10 +791,12 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   auto push_open = [&](int c, uint64_t row) {
     const uint64_t ch = n >= 1024 ? row >> COL_CHUNK_LOG2 : 0;
     if (ch >= ch_lo && ch < ch_hi) {
-      oreq[4 * no] = (uint32_t)c;
-      oreq[4 * no + 1] = (uint32_t)row;
-      oreq[4 * no + 2] = (uint32_t)(row >> 32);
-      oreq[4 * no + 3] = (uint32_t)ord;
+      uint32_t* rq = oreq + (size_t)OPEN_REQ_WORDS * no;
+      rq[0] = (uint32_t)c;
+      rq[1] = (uint32_t)row;
+      rq[2] = (uint32_t)(row >> 32);
+      rq[3] = (uint32_t)ord;
+      rq[4] = dict_of[c];
       no++;
     }
     ord++;
@@ -811,11 +818,12 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     push_open(2, row);  // is_last
     push_open(0, row);  // input_mv
   }
-  HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (3 * max_fri_req + 4 * no) * 4, hipMemcpyHostToDevice, st));
+  HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (3 * max_fri_req + OPEN_REQ_WORDS * no) * 4, hipMemcpyHostToDevice, st));
   if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
   ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL), "fri_paths");
   rec(ST_PATHS + 1);
-  ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 3 * max_fri_req, (int)no, PL),
+  ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 3 * max_fri_req, (int)no, PL, d_tabs,
+                     d_dlev),
      "col_open");
   if (sharded) comm->allreduce_sum_u8(PL.base, PL.total, st);
   rec(ST_OPEN + 1);

@@ -112,6 +112,13 @@ struct DictPlan {
   uint32_t pad;
 };
 __host__ __device__ inline bool kind_dict(uint32_t kind) { return kind == 0 || (kind >= 3 && kind <= 6); }
+// Chunk levels 6..9 of every dictionary column (16 + 8 + 4 + 2 nodes per
+// 1024-row chunk), written by the commitment, read by the openings.
+constexpr int DICT_LANE_LOG = 6;  // rows per lane of the dictionary commitment (level-6 nodes)
+constexpr int DLEV_NODES = 30;
+__host__ __device__ inline int dlev_base(int level) { return level == 6 ? 0 : level == 7 ? 16 : level == 8 ? 24 : 28; }
+constexpr uint32_t NO_DICT = 0xFFFFFFFFu;
+constexpr int OPEN_REQ_WORDS = 5;  // column, row lo, row hi, ordinal, dictionary index
 
 constexpr int LSTORE_FRI = 6;
 constexpr int COL_CHUNK_LOG2 = 10;
@@ -145,7 +152,7 @@ hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplat
 // rows [row0, row0 + nrows) of every dictionary column (row0, nrows multiples of 4096 or the whole trace)
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows);
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev);
 hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);
@@ -214,9 +221,9 @@ hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a);
 // requests: (layer, index, ordinal in the proof's FRI records) triples
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
                             const ProofLayout& P);
-// requests: (column, row lo, row hi, ordinal in the proof's openings) quadruples
+// requests: OPEN_REQ_WORDS words each
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
-                           const ProofLayout& P);
+                           const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev);
 
 }  // namespace sezkp

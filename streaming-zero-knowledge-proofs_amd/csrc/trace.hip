@@ -484,12 +484,14 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
 __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                          const uint32_t* __restrict__ outer, uint64_t outer_stride,
                                                          int logChunks, const uint32_t* __restrict__ req,
-                                                         ProofLayout P) {
+                                                         ProofLayout P, const uint32_t* __restrict__ tabs,
+                                                         const uint32_t* __restrict__ dlev) {
   __shared__ uint32_t lds[8][1024];
-  const uint32_t* rq = req + 4 * (uint64_t)blockIdx.x;
+  const uint32_t* rq = req + OPEN_REQ_WORDS * (uint64_t)blockIdx.x;
   const int c = rq[0];
   const uint64_t row = (uint64_t)rq[1] | ((uint64_t)rq[2] << 32);
-  const uint32_t q = rq[3];  // ordinal of this opening in the proof
+  const uint32_t q = rq[3];     // ordinal of this opening in the proof
+  const uint32_t dsel = rq[4];  // dictionary column index (chunk levels 6..9 stored), or NO_DICT
   const ColTemplate ct = tmpl[c];
   const int tid = threadIdx.x;
   const uint64_t n = T.n;
@@ -511,21 +513,36 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
     o[16] = (uint32_t)logcl; o[17] = 0;
     o[18 + 8 * logcl] = (uint32_t)logChunks; o[19 + 8 * logcl] = 0;
   }
-  for (uint64_t i = tid; i < cl; i += TR_THREADS) {
-    uint32_t h[8];
-    leaf_labeled_rt(ct, col_value(T, ct, start + i), h);
-#pragma unroll
-    for (int w = 0; w < 8; w++) lds[w][i] = h[w];
-  }
   if (tid == 0) {
     const uint64_t v = col_value(T, ct, row);
     o[0] = (uint32_t)v;
     o[1] = (uint32_t)(v >> 32);
   }
+  // Dictionary columns: rebuild only the 64-row group holding `row` (levels
+  // 0..5); levels 6..9 were stored by the commitment, the chunk root is the
+  // outer tree's leaf.
+  const bool dict = dsel != NO_DICT && logcl == COL_CHUNK_LOG2;
+  const int glog = dict ? DICT_LANE_LOG : logcl;
+  const uint64_t gstart = dict ? (row & ~((1ULL << DICT_LANE_LOG) - 1)) : start;
+  // piecewise columns read their leaves from the uniform-subtree tables (U_0)
+  const bool pw = kind_piecewise(ct.kind) && ct.tab != NO_TAB;
+  for (uint64_t i = tid; i < (1ULL << glog); i += TR_THREADS) {
+    uint32_t h[8];
+    const uint64_t r = gstart + i;
+    if (pw) {
+      const uint64_t u = (ct.kind == 1 || ct.kind == 2) ? ((T.row_flags[r] >> (ct.kind - 1)) & 1) : T.row_blk[r];
+      node_load(tabs + 8 * (ct.tab + u * U_LEVELS), h);
+    } else {
+      leaf_labeled_rt(ct, col_value(T, ct, r), h);
+    }
+#pragma unroll
+    for (int w = 0; w < 8; w++) lds[w][i] = h[w];
+  }
   __syncthreads();
-  int cnt = (int)cl;
-  for (int lvl = 0; lvl < logcl; lvl++) {
-    const int sib = (int)((in >> lvl) ^ 1);
+  const uint64_t gin = row - gstart;
+  int cnt = 1 << glog;
+  for (int lvl = 0; lvl < glog; lvl++) {
+    const int sib = (int)((gin >> lvl) ^ 1);
     if (tid < 8) o[18 + 8 * lvl + tid] = lds[tid][sib];
     const int half = cnt >> 1;
     uint32_t hh[2][8];
@@ -544,9 +561,18 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
     __syncthreads();
     cnt = half;
   }
-  if (tid < 8) o[8 + tid] = lds[tid][0];
-  // path_to_chunk from the stored outer tree (all levels kept)
   const uint32_t* ob = outer + (uint64_t)c * outer_stride * 8;
+  if (dict) {
+    const uint32_t* lev = dlev + 8 * ((uint64_t)dsel * (T.n >> COL_CHUNK_LOG2) + ch) * DLEV_NODES;
+    for (int lvl = DICT_LANE_LOG; lvl < COL_CHUNK_LOG2; lvl++) {
+      const uint64_t sib = (in >> lvl) ^ 1;
+      if (tid < 8) o[18 + 8 * lvl + tid] = lev[8 * (dlev_base(lvl) + sib) + tid];
+    }
+    if (tid < 8) o[8 + tid] = ob[8 * ch + tid];  // chunk root = outer leaf
+  } else {
+    if (tid < 8) o[8 + tid] = lds[tid][0];
+  }
+  // path_to_chunk from the stored outer tree (all levels kept)
   uint32_t* op = o + 20 + 8 * logcl;
   for (int lvl = 0; lvl < logChunks; lvl++) {
     const uint64_t sib = (ch >> lvl) ^ 1;
@@ -668,7 +694,6 @@ __device__ __forceinline__ void lane_tree(const Prov& P, uint32_t (&h)[8]) {
   }
 }
 
-constexpr int DICT_LANE_LOG = 6;                                     // rows per lane
 constexpr int DICT_WG_ROWS = 64 << DICT_LANE_LOG;                    // 4096 rows per 64-lane WG
 constexpr int DICT_RANGE_ROWS = TR_THREADS * 16;                     // rows per range WG
 
@@ -809,7 +834,8 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
                                                         const DictCol* __restrict__ dcols,
                                                         const DictPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ tabs, uint32_t* __restrict__ outer,
-                                                        uint64_t outer_stride, uint64_t row0) {
+                                                        uint64_t outer_stride, uint64_t row0,
+                                                        uint32_t* __restrict__ dlev) {
   __shared__ uint32_t lds[8][64];
   const DictCol dc = dcols[blockIdx.y];
   const ColTemplate* ctp = tmpl + dc.col;
@@ -830,9 +856,15 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
     }
 #pragma unroll
     for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
+    // chunk levels 6..9 are kept for the openings (DLEV_NODES per chunk)
+    node_store(dlev + 8 * (((uint64_t)blockIdx.y * (T.n >> COL_CHUNK_LOG2) + (lrow >> COL_CHUNK_LOG2)) * DLEV_NODES +
+                           ((lrow >> DICT_LANE_LOG) & 15)),
+               h);
   }
   __syncthreads();
-  for (int cnt = 64; cnt > 4; cnt >>= 1) {  // levels 7..10
+  const uint64_t nch_all = T.n >> COL_CHUNK_LOG2;
+  int lv = 7;
+  for (int cnt = 64; cnt > 4; cnt >>= 1, lv++) {  // levels 7..10
     const int half = cnt >> 1;
     uint32_t h[8];
     const bool a2 = lane < half;
@@ -850,6 +882,10 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
     if (a2) {
 #pragma unroll
       for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
+      const int per = half >> 2;  // nodes of this level per chunk
+      const uint64_t chq = (wg_row >> COL_CHUNK_LOG2) + lane / per;
+      if (lv <= 9 && chq < nch_all)
+        node_store(dlev + 8 * (((uint64_t)blockIdx.y * nch_all + chq) * DLEV_NODES + dlev_base(lv) + lane % per), h);
     }
     __syncthreads();
   }
@@ -878,7 +914,7 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
 }
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows) {
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev) {
   if (ndict == 0) return hipSuccess;
   if (T.n < (1ULL << COL_CHUNK_LOG2)) return hipErrorInvalidValue;
   if (row0 + nrows > T.n || (nrows != T.n && (row0 % DICT_WG_ROWS || nrows % DICT_WG_ROWS))) return hipErrorInvalidValue;
@@ -897,7 +933,7 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
   }
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
   hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
-                     outer_nodes, outer_stride_nodes, row0);
+                     outer_nodes, outer_stride_nodes, row0, d_dlev);
   return hipGetLastError();
 }
 
@@ -929,11 +965,11 @@ hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, co
 }
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
-                           const ProofLayout& P) {
+                           const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev) {
   if (nreq == 0) return hipSuccess;
   if ((uint64_t)nreq > (uint64_t)P.nq * P.open_per_q) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_col_open, dim3(nreq), dim3(TR_THREADS), 0, st, T, d_tmpl, outer_nodes, outer_stride_nodes,
-                     logChunks, d_req, P);
+                     logChunks, d_req, P, tabs, d_dlev);
   return hipGetLastError();
 }
 
