@@ -136,7 +136,7 @@ struct sezkp_ctx {
   int device = 0;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // side stream: small FRI layers overlap the forest
-  hipEvent_t ev_fold = nullptr, ev_tail = nullptr;
+  hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr;
   NttTables tw{};
   std::vector<void*> dev_allocs;
   std::vector<void*> host_allocs;
@@ -241,6 +241,8 @@ struct sezkp_ctx {
     if (st2) (void)hipStreamSynchronize(st2);
     if (ev_fold) (void)hipEventDestroy(ev_fold);
     if (ev_tail) (void)hipEventDestroy(ev_tail);
+    if (ev_expand) (void)hipEventDestroy(ev_expand);
+    if (ev_cols) (void)hipEventDestroy(ev_cols);
     if (st) (void)hipStreamDestroy(st);
     if (st2) (void)hipStreamDestroy(st2);
   }
@@ -604,13 +606,19 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   rec(1);
   const uint64_t row_lo = n >= 1024 ? ch_lo << COL_CHUNK_LOG2 : 0;
   const uint64_t row_hi = n >= 1024 ? ch_hi << COL_CHUNK_LOG2 : n;
+  // piecewise / table / dense columns on the side stream, concurrent with the
+  // (VALU-bound) dictionary columns; disjoint outer-tree leaves
+  HIP_OR_THROW(hipEventRecord(ev_expand, st));
+  HIP_OR_THROW(hipStreamWaitEvent(st2, ev_expand, 0));
+  ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
+  ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
+  ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
+                          outer_stride, d_err), "col_commit_pw");
+  HIP_OR_THROW(hipEventRecord(ev_cols, st2));
   ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
                         row_hi - row_lo, d_dlev),
      "col_commit_dict");
-  ok(launch_col_tables(st, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
-  ok(launch_col_commit(st, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
-  ok(launch_col_commit_pw(st, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
-                          outer_stride, d_err), "col_commit_pw");
+  HIP_OR_THROW(hipStreamWaitEvent(st, ev_cols, 0));
   if (sharded) {
     const size_t bytes = (size_t)(ch_hi - ch_lo) * 32;
     comm->group_start();
@@ -723,8 +731,16 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     ok(launch_fri_tail(st2, ta), "fri_tail");
     HIP_OR_THROW(hipEventRecord(ev_tail, st2));
   };
-  for (int r = 0; r < rR; r++)
-    ok(launch_fold(st, lvals[r], lvals[r + 1], ltrees[r + 1].logLen, beta_of(r)), "fri_fold");
+  for (int r = 0; r < rR;) {  // fold chain, two layers per pass where possible
+    if (r + 1 < rR) {
+      ok(launch_fold2(st, lvals[r], lvals[r + 1], lvals[r + 2], ltrees[r + 2].logLen, beta_of(r), beta_of(r + 1)),
+         "fri_fold2");
+      r += 2;
+    } else {
+      ok(launch_fold(st, lvals[r], lvals[r + 1], ltrees[r + 1].logLen, beta_of(r)), "fri_fold");
+      r += 1;
+    }
+  }
   const uint64_t* rep_src = rR >= 0 ? lvals[rR] : d_lde;  // full values of the layer above the replicated ones
   if (!sharded) launch_tail(rep_src);
   ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
@@ -823,7 +839,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL), "fri_paths");
   rec(ST_PATHS + 1);
   ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 3 * max_fri_req, (int)no, PL, d_tabs,
-                     d_dlev),
+                     d_dlev, d_dplans),
      "col_open");
   if (sharded) comm->allreduce_sum_u8(PL.base, PL.total, st);
   rec(ST_OPEN + 1);
@@ -910,6 +926,8 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
+    HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));
+    HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_cols, hipEventDisableTiming));
     c->tw = tables_for_device(device);
     // SEZKP_FORCE_SHARDED=1 runs the sharded algorithm (and its RCCL calls)
     // with a one-rank communicator: tests it on a single GPU

@@ -118,6 +118,9 @@ constexpr int DICT_LANE_LOG = 6;  // rows per lane of the dictionary commitment 
 constexpr int DLEV_NODES = 30;
 __host__ __device__ inline int dlev_base(int level) { return level == 6 ? 0 : level == 7 ? 16 : level == 8 ? 24 : 28; }
 constexpr uint32_t NO_DICT = 0xFFFFFFFFu;
+// extra lane rows (log2) of the dictionary commitment for table level K:
+// high K leaves few table nodes per 64 rows, so lanes take 2^(6+a) rows
+__host__ __device__ inline int dict_extra(int K) { return K >= 3 ? 2 : (K == 2 ? 1 : 0); }
 constexpr int OPEN_REQ_WORDS = 5;  // column, row lo, row hi, ordinal, dictionary index
 
 constexpr int LSTORE_FRI = 6;
@@ -200,6 +203,9 @@ hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals
                           TreeDev tree);
 // Fold chain kernel (values only) and the one-launch forest of layer trees.
 hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta);
+// two consecutive folds in one pass; logLen2 = log2 of the second output
+hipError_t launch_fold2(hipStream_t st, const uint64_t* in, uint64_t* out1, uint64_t* out2, int logLen2, uint64_t b1,
+                        uint64_t b2);
 struct ForestLayer {
   const uint64_t* vals;
   TreeDev tree;
@@ -224,6 +230,7 @@ hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const u
 // requests: OPEN_REQ_WORDS words each
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
-                           const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev);
+                           const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev,
+                           const DictPlan* d_plans);
 
 }  // namespace sezkp

@@ -485,7 +485,8 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
                                                          const uint32_t* __restrict__ outer, uint64_t outer_stride,
                                                          int logChunks, const uint32_t* __restrict__ req,
                                                          ProofLayout P, const uint32_t* __restrict__ tabs,
-                                                         const uint32_t* __restrict__ dlev) {
+                                                         const uint32_t* __restrict__ dlev,
+                                                         const DictPlan* __restrict__ plans) {
   __shared__ uint32_t lds[8][1024];
   const uint32_t* rq = req + OPEN_REQ_WORDS * (uint64_t)blockIdx.x;
   const int c = rq[0];
@@ -522,8 +523,8 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
   // 0..5); levels 6..9 were stored by the commitment, the chunk root is the
   // outer tree's leaf.
   const bool dict = dsel != NO_DICT && logcl == COL_CHUNK_LOG2;
-  const int glog = dict ? DICT_LANE_LOG : logcl;
-  const uint64_t gstart = dict ? (row & ~((1ULL << DICT_LANE_LOG) - 1)) : start;
+  const int glog = dict ? DICT_LANE_LOG + dict_extra(plans[dsel].K) : logcl;
+  const uint64_t gstart = dict ? (row & ~((1ULL << glog) - 1)) : start;
   // piecewise columns read their leaves from the uniform-subtree tables (U_0)
   const bool pw = kind_piecewise(ct.kind) && ct.tab != NO_TAB;
   for (uint64_t i = tid; i < (1ULL << glog); i += TR_THREADS) {
@@ -564,7 +565,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
   const uint32_t* ob = outer + (uint64_t)c * outer_stride * 8;
   if (dict) {
     const uint32_t* lev = dlev + 8 * ((uint64_t)dsel * (T.n >> COL_CHUNK_LOG2) + ch) * DLEV_NODES;
-    for (int lvl = DICT_LANE_LOG; lvl < COL_CHUNK_LOG2; lvl++) {
+    for (int lvl = glog; lvl < COL_CHUNK_LOG2; lvl++) {
       const uint64_t sib = (in >> lvl) ^ 1;
       if (tid < 8) o[18 + 8 * lvl + tid] = lev[8 * (dlev_base(lvl) + sib) + tid];
     }
@@ -817,12 +818,13 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __
 template <typename Key>
 __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const uint32_t* tab,
                                           const ColTemplate* ct, uint32_t (&h)[8]) {
+  // a lane covers 2^(6 + dict_extra(K)) rows: 2^(6+a-K) table nodes
   switch (P.K) {
     case 0: lane_tree<6>(DictNodes<Key, 0>{p, tab, P.min, P.R}, h); break;
     case 1: lane_tree<5>(DictNodes<Key, 1>{p, tab + 8 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 2: lane_tree<4>(DictNodes<Key, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 3: lane_tree<3>(DictNodes<Key, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 4: lane_tree<2>(DictNodes<Key, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 2: lane_tree<5>(DictNodes<Key, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 3: lane_tree<5>(DictNodes<Key, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 4: lane_tree<4>(DictNodes<Key, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
     default: lane_tree<6>(RawLeaves<Key>{p, ct}, h); break;
   }
 }
@@ -834,7 +836,7 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
                                                         const DictCol* __restrict__ dcols,
                                                         const DictPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ tabs, uint32_t* __restrict__ outer,
-                                                        uint64_t outer_stride, uint64_t row0,
+                                                        uint64_t outer_stride, uint64_t row0, uint64_t row_end,
                                                         uint32_t* __restrict__ dlev) {
   __shared__ uint32_t lds[8][64];
   const DictCol dc = dcols[blockIdx.y];
@@ -843,10 +845,15 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
   const DictPlan P = plans[blockIdx.y];
   const uint32_t* tab = tabs + 8 * dc.tab;
   const int lane = threadIdx.x;
-  const uint64_t wg_row = row0 + (uint64_t)blockIdx.x * DICT_WG_ROWS;
-  const uint64_t lrow = wg_row + ((uint64_t)lane << DICT_LANE_LOG);
-  const bool act = lrow < T.n;
-  if (act) {
+  // high-K columns give each lane more rows (fewer LDS levels per row)
+  const int a = dict_extra(P.K);
+  const int llog = DICT_LANE_LOG + a;  // rows per lane (log2)
+  const uint64_t wg_row = row0 + ((uint64_t)blockIdx.x << (llog + 6));
+  if (wg_row >= row_end) return;  // grid is sized for a = 0
+  const uint64_t lrow = wg_row + ((uint64_t)lane << llog);
+  const uint64_t nch_all = T.n >> COL_CHUNK_LOG2;
+  uint32_t* dl = dlev + 8 * (uint64_t)blockIdx.y * nch_all * DLEV_NODES;
+  if (lrow < row_end) {
     uint32_t h[8];
     switch (ct.kind) {
       case 0: case 3: dict_lane<int8_t>(dict_keys<int8_t>(T, ct) + lrow, P, tab, ctp, h); break;
@@ -856,15 +863,14 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
     }
 #pragma unroll
     for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
-    // chunk levels 6..9 are kept for the openings (DLEV_NODES per chunk)
-    node_store(dlev + 8 * (((uint64_t)blockIdx.y * (T.n >> COL_CHUNK_LOG2) + (lrow >> COL_CHUNK_LOG2)) * DLEV_NODES +
-                           ((lrow >> DICT_LANE_LOG) & 15)),
+    // chunk levels llog..9 are kept for the openings (DLEV_NODES per chunk)
+    node_store(dl + 8 * ((lrow >> COL_CHUNK_LOG2) * DLEV_NODES + dlev_base(llog) +
+                         ((lrow >> llog) & ((1u << (COL_CHUNK_LOG2 - llog)) - 1))),
                h);
   }
   __syncthreads();
-  const uint64_t nch_all = T.n >> COL_CHUNK_LOG2;
-  int lv = 7;
-  for (int cnt = 64; cnt > 4; cnt >>= 1, lv++) {  // levels 7..10
+  int cnt = 64;
+  for (int lv = llog + 1; lv <= COL_CHUNK_LOG2; lv++) {
     const int half = cnt >> 1;
     uint32_t h[8];
     const bool a2 = lane < half;
@@ -882,18 +888,19 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
     if (a2) {
 #pragma unroll
       for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
-      const int per = half >> 2;  // nodes of this level per chunk
+      const int per = 1 << (COL_CHUNK_LOG2 - lv);  // nodes of this level per chunk
       const uint64_t chq = (wg_row >> COL_CHUNK_LOG2) + lane / per;
-      if (lv <= 9 && chq < nch_all)
-        node_store(dlev + 8 * (((uint64_t)blockIdx.y * nch_all + chq) * DLEV_NODES + dlev_base(lv) + lane % per), h);
+      if (lv < COL_CHUNK_LOG2 && chq < nch_all) node_store(dl + 8 * (chq * DLEV_NODES + dlev_base(lv) + lane % per), h);
     }
     __syncthreads();
+    cnt = half;
   }
-  // chunk i of this WG: rows [blockIdx.x*4096 + 1024 i, +1024)
-  const uint64_t nch = T.n >> COL_CHUNK_LOG2;
-  const int q = lane >> 3, w = lane & 7;
-  const uint64_t ch = (wg_row >> COL_CHUNK_LOG2) + q;
-  if (q < 4 && ch < nch) outer[(uint64_t)dc.col * outer_stride * 8 + ch * 8 + w] = lds[w][q];
+  // cnt chunk roots of this WG -> leaves of the column's outer tree
+  for (int i = lane; i < cnt * 8; i += 64) {
+    const uint64_t ch = (wg_row >> COL_CHUNK_LOG2) + (i >> 3);
+    if (ch < nch_all && (ch << COL_CHUNK_LOG2) < row_end)
+      outer[(uint64_t)dc.col * outer_stride * 8 + ch * 8 + (i & 7)] = lds[i & 7][i >> 3];
+  }
 }
 
 // ------------------------------------------------------------------ host
@@ -933,7 +940,7 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
   }
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
   hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
-                     outer_nodes, outer_stride_nodes, row0, d_dlev);
+                     outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev);
   return hipGetLastError();
 }
 
@@ -965,11 +972,12 @@ hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, co
 }
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
-                           const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev) {
+                           const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev,
+                           const DictPlan* d_plans) {
   if (nreq == 0) return hipSuccess;
   if ((uint64_t)nreq > (uint64_t)P.nq * P.open_per_q) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_col_open, dim3(nreq), dim3(TR_THREADS), 0, st, T, d_tmpl, outer_nodes, outer_stride_nodes,
-                     logChunks, d_req, P, tabs, d_dlev);
+                     logChunks, d_req, P, tabs, d_dlev, d_plans);
   return hipGetLastError();
 }
 
