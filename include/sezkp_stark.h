@@ -98,8 +98,8 @@ int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], 
                                const uint8_t** data, size_t* len, char* err, size_t err_len);
 /* Per-stage device times (ms) of the last prove, measured with HIP events on
  * the context's stream. Order: expand, col_commit, col_outer, compose, intt,
- * lde_ntt, deep, layer0_tree, layer0_upper, fri_fold_trees, fri_paths,
- * col_openings, total, then host wall / sync-wait / final-wait / serialize.
+ * lde_ntt, deep, layer0_tree, layer0_upper, fri_fold_trees, col_openings,
+ * fri_paths, total, then host wall / sync-wait / final-wait / serialize.
  * Returns the number of values written. */
 int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max);
 /* Device hipStream_t of the context (as void*), for external timing. */

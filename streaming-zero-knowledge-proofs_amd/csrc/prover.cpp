@@ -35,7 +35,7 @@ constexpr int BLOWUP_LOG2 = 3;   // params.rs:28
 // ST_L0TREE brackets exactly one launch (k_layer16 over the LDE) so bench.py
 // can quote that kernel's live duration; ST_L0UP holds its upper levels.
 enum Stage { ST_EXPAND, ST_COMMIT, ST_OUTER, ST_COMPOSE, ST_INTT, ST_LDE, ST_DEEP, ST_L0TREE, ST_L0UP, ST_FRI,
-             ST_PATHS, ST_OPEN, ST_NSTAGE };
+             ST_OPEN, ST_PATHS, ST_NSTAGE };
 
 struct Err {
   int32_t code;
@@ -836,15 +836,26 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   }
   HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (3 * max_fri_req + OPEN_REQ_WORDS * no) * 4, hipMemcpyHostToDevice, st));
   if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
-  ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL), "fri_paths");
-  rec(ST_PATHS + 1);
+  // openings first: their section of the proof (~70% of it) goes back over
+  // PCIe on the side stream while the FRI path kernel runs
   ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 3 * max_fri_req, (int)no, PL, d_tabs,
                      d_dlev, d_dplans),
      "col_open");
-  if (sharded) comm->allreduce_sum_u8(PL.base, PL.total, st);
   rec(ST_OPEN + 1);
-  HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.total, hipMemcpyDeviceToHost, st));
+  if (!sharded) {
+    HIP_OR_THROW(hipEventRecord(ev_fold, st));
+    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+    HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.fr_off, hipMemcpyDeviceToHost, st2));
+    HIP_OR_THROW(hipEventRecord(ev_tail, st2));
+  }
+  ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL), "fri_paths");
+  if (sharded) comm->allreduce_sum_u8(PL.base, PL.total, st);
+  rec(ST_PATHS + 1);
+  const uint64_t d2h_from = sharded ? 0 : PL.fr_off;
+  HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes + d2h_from, (const uint8_t*)PL.base + d2h_from,
+                              PL.total - d2h_from, hipMemcpyDeviceToHost, st));
   HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), lvals[k], 8, hipMemcpyDeviceToHost, st));
+  if (!sharded) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
   sync();
   for (int s = 0; s < ST_NSTAGE; s++) {
     float ms = 0;

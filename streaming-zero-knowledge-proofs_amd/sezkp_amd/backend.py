@@ -15,7 +15,7 @@ from ._lib import SEZKP_FLAG_STREAMING, Buf, SezkpError, check, lib, take_buf
 from .blocks import BlockSoA
 
 STAGES = ["expand", "col_commit", "col_outer", "compose", "intt", "lde_ntt", "deep", "layer0_tree",
-          "layer0_upper", "fri_fold_trees", "fri_paths", "col_openings", "total",
+          "layer0_upper", "fri_fold_trees", "col_openings", "fri_paths", "total",
           # host-side split of the same prove() call (wall clock)
           "host_wall", "host_sync_wait", "host_final_wait", "host_serialize"]
 
