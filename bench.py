@@ -68,9 +68,9 @@ def cpu_baseline(T_sample: int, tau: int, T_mt: int):
     and the single-thread build, each on a bounded sample of the workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as O
-    from sezkp_amd import synthetic_blocks
+    from sezkp_amd import reference_blocks
     O.build()
-    blocks = synthetic_blocks(T_sample, 512, tau, 42)
+    blocks = reference_blocks(T_sample, 512, tau)
     root = blocks.manifest_root()
     t0 = time.perf_counter()
     O.prove_v1(blocks, root)
@@ -84,7 +84,7 @@ def cpu_baseline(T_sample: int, tau: int, T_mt: int):
                         f"tau={tau}; {dt:.2f} s"}
     threads = min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1))
     used = O.use_mt(threads)
-    bl = synthetic_blocks(T_mt, 512, tau, 42)
+    bl = reference_blocks(T_mt, 512, tau)
     r = bl.manifest_root()
     t1 = time.perf_counter()
     O.prove_v1(bl, r)
@@ -115,6 +115,9 @@ def main():
     ap.add_argument("--sharded-steps", type=int, default=3)
     ap.add_argument("--sharded-timeout", type=float, default=240.0,
                     help="watchdog: print the main line and exit if the sharded measurement stalls")
+    ap.add_argument("--dntt-log-n", type=int, default=26,
+                    help="distributed four-step NTT sub-measurement size (BASELINE config 4: 2^26); 0 = skip")
+    ap.add_argument("--dntt-steps", type=int, default=5)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,9 +132,9 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    from sezkp_amd import ProverContext, synthetic_blocks
+    from sezkp_amd import ProverContext, reference_blocks
     T = 1 << args.log_t
-    blocks = synthetic_blocks(T, args.b, args.tau, 42)
+    blocks = reference_blocks(T, args.b, args.tau)
     mroot = blocks.manifest_root()
     ctx = ProverContext(local if world > 1 else 0)
     ctx.upload(blocks)  # trace image resident in HBM before timing
@@ -197,7 +200,9 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "field-elements/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": f"synthetic: the blocks `sezkp-cli simulate --t {T} --b {args.b} --tau {args.tau}` writes "
+                    f"(reference generator + partition, bit-exact restatement)",
             "config": {"workload": f"stark-v1 prove, T=2^{args.log_t} rows (N=2^{args.log_t + 3} LDE domain), "
                                    f"b={args.b}, tau={args.tau}, trace resident in HBM",
                        "T": T, "N": N, "tau": args.tau, "b": args.b, "proof_bytes": proof_len,
@@ -210,37 +215,93 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(1 << args.cpu_sample_log_t, args.tau, 1 << args.cpu_mt_log_t)
     ctx.close()
-    if world > 1 and not args.no_sharded:
-        # ONE proof over all ranks (weak: 2^log_t rows per GPU),
-        # RCCL all-to-all + allgathers inside the library. Reported beside the
-        # replica line; a watchdog keeps a stalled collective from costing it.
+    del blocks
+
+    def guarded(key, fn):
+        # extra measurements are reported beside the main line; a watchdog
+        # keeps a stalled collective from costing it
         import threading
 
         def _bail():
             if rank == 0:
-                out["sharded"] = {"error": f"watchdog: no result within {args.sharded_timeout:.0f} s"}
+                out[key] = {"error": f"watchdog: no result within {args.sharded_timeout:.0f} s"}
                 print(json.dumps(out), flush=True)
             os._exit(0)
         wd = threading.Timer(args.sharded_timeout, _bail)
         wd.daemon = True
         wd.start()
         try:
-            sh = measure_sharded(args, world, rank, local, dist, torch)
+            res = fn()
         except Exception as e:  # reported, never fatal to the main line
-            sh = {"error": f"{type(e).__name__}: {e}"}
+            res = {"error": f"{type(e).__name__}: {e}"}
         wd.cancel()
         if rank == 0:
-            out["sharded"] = sh
+            out[key] = res
+
+    if args.dntt_log_n:
+        # BASELINE config 4 (at N = 8): 2^26-point four-step NTT over all ranks
+        guarded("dist_ntt", lambda: measure_dist_ntt(args, world, rank, local, dist, torch))
+    if world > 1 and not args.no_sharded:
+        # ONE proof over all ranks (weak: 2^log_t rows per GPU)
+        guarded("sharded", lambda: measure_sharded(args, world, rank, local, dist, torch))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
+def measure_dist_ntt(args, world, rank, local, dist, torch):
+    """sezkp_ctx_dist_ntt: n = 2^dntt_log_n points split over the ranks
+    (strong scaling: fixed n), forward + inverse per step on the context
+    stream; one RCCL all-to-all per transform. Round trip checked."""
+    from sezkp_amd import ProverContext, ShardedProverContext
+    ctx = ShardedProverContext(rank, world, device=local, comm="rccl") if world > 1 else ProverContext(0)
+    log_n = args.dntt_log_n
+    M = (1 << log_n) // world
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + rank)
+    x = torch.randint(0, 0xFFFFFFFF00000001 >> 1, (M,), dtype=torch.int64, device="cuda", generator=g)
+    d = x.clone()
+    scratch = torch.empty_like(d)
+    for _ in range(2):
+        ctx.dist_ntt(d, scratch)
+        ctx.dist_ntt(d, scratch, inverse=True)
+    ok = bool(torch.equal(d, x))
+    st = torch.cuda.ExternalStream(ctx.stream)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.dntt_steps):
+        ctx.dist_ntt(d, scratch, sync=False)
+        ctx.dist_ntt(d, scratch, inverse=True, sync=False)
+    st.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        oks = [None] * world
+        dist.all_gather_object(oks, ok)
+        ok = all(oks)
+    ctx.close()
+    n = 1 << log_n
+    per = dt / (2 * args.dntt_steps)
+    alg = 16 * M / per / 1e9  # read + write each local element once, per GPU
+    return {"workload": f"2^{log_n}-point Goldilocks NTT over {world} GPU(s), forward + inverse (four-step: "
+                        f"local 2^{log_n - (world.bit_length() - 1)} NTT, twiddle, "
+                        f"{'1 RCCL all-to-all' if world > 1 else 'no exchange'}, {world}-point DFTs)",
+            "value": n / per, "unit": "field-elements/s", "ms_per_transform": per * 1e3, "steps": args.dntt_steps,
+            "scaling": "strong", "roundtrip_ok": ok, "alg_GBs_per_gpu": alg, "frac_hbm_alg": alg / HBM_PEAK_GBS}
+
+
 def measure_sharded(args, world, rank, local, dist, torch):
-    from sezkp_amd import ShardedProverContext, synthetic_blocks
+    from sezkp_amd import ShardedProverContext, reference_blocks
     T = (1 << args.log_t) * world
-    blocks = synthetic_blocks(T, args.b, args.tau, 42)
+    blocks = reference_blocks(T, args.b, args.tau)
     mroot = blocks.manifest_root()
     ctx = ShardedProverContext(rank, world, device=local, comm="rccl")
     ctx.upload(blocks)

@@ -130,6 +130,20 @@ typedef struct sezkp_host_comm {
 sezkp_ctx* sezkp_ctx_create_sharded_host(int32_t device, int32_t rank, int32_t world, const sezkp_host_comm* comm,
                                          char* err, size_t err_len);
 
+/* Distributed four-step NTT of n = 2^log_n points over the context's P ranks
+ * (BASELINE config 4: 2^26 points across 8 GPUs, the transpose as one RCCL
+ * all-to-all). Rank g's `local` holds M = n/P elements. Forward (dir=+1):
+ * in  local[j] = x[g + P j] (cyclic),
+ * out local[k1 Q + q] = X[g Q + q + M k1]  (Q = M/P; rank g owns the k with
+ *     (k mod M) / Q == g).
+ * Inverse (dir=-1, incl. n^-1) maps the output layout back to the input one.
+ * X_k = sum_t x_t w_n^(tk) as in ntt.rs:79-155. `scratch` holds M elements.
+ * Asynchronous on sezkp_ctx_stream(ctx); needs 2^(8 + log P) <= n <= 2^32.
+ * Any context works (P = 1 for sezkp_ctx_create). Extends the reference:
+ * its NTT is single-threaded CPU code with no sharded form. */
+int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, uint32_t log_n, int32_t dir,
+                           char* err, size_t err_len);
+
 /* ------------------------------------------------ kernel-level entry points
  * Device pointers (u64 canonical Goldilocks, natural order), 32-byte digests,
  * stream = hipStream_t (NULL = default stream). Asynchronous on `stream`. */
@@ -163,6 +177,19 @@ int32_t sezkp_blocks_decode_jsonl(const uint8_t* data, size_t len, sezkp_blocks*
 int32_t sezkp_blocks_encode_jsonl(const sezkp_block_view* blocks, sezkp_buf* out);
 const sezkp_block_view* sezkp_blocks_view(const sezkp_blocks* b);
 void sezkp_blocks_free(sezkp_blocks* b);
+/* Vec<BlockSummary> as CBOR, byte-identical to the reference's writer
+ * (io.rs, ciborium; pins: the reference's blocks.cbor fixtures). */
+int32_t sezkp_blocks_encode_cbor(const sezkp_block_view* blocks, sezkp_buf* out);
+/* The reference's input producer, bit-exact (`sezkp-cli simulate`, main.rs:317-350):
+ * generate_trace (sezkp-trace generator.rs:38-73, rand 0.9.2 StdRng seeded by
+ * seed_from_u64(seed); the reference always uses 42) into step-major arrays
+ * input_mv[t], mv/has_write/wsym[t][tau] ... */
+int32_t sezkp_simulate_trace(uint64_t t, uint32_t tau, uint64_t seed, int8_t* input_mv, int8_t* mv,
+                             uint8_t* has_write, uint16_t* wsym);
+/* ... and partition_trace (partition.rs:43-150) into blocks of b steps;
+ * free with sezkp_blocks_free. */
+int32_t sezkp_simulate_blocks(uint64_t t, uint32_t b, uint32_t tau, uint64_t seed, sezkp_blocks** out, char* err,
+                              size_t err_len);
 /* Decode a manifest file (sezkp-merkle commit output: {root: [32], n_leaves}),
  * CBOR or JSON (is_json != 0). */
 int32_t sezkp_manifest_decode(const uint8_t* data, size_t len, int32_t is_json, uint8_t root[32],

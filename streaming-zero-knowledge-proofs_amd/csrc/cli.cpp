@@ -93,6 +93,7 @@ std::string pretty_artifact(const Artifact& a) {
 struct Args {
   std::string cmd, backend = "stark", blocks, manifest, out, proof;
   bool stream = false, assume = false;
+  std::string t = "32", b = "4", tau = "2";  // simulate defaults (main.rs:87-100)
 };
 
 int precheck(const Args& a, const BlockStore& bs) {  // verify_block_file_against_manifest
@@ -207,11 +208,53 @@ int cmd_commit(const Args& a) {
   return 0;
 }
 
+// `simulate` (main.rs:317-350): generate_trace + partition_trace, written as
+// CBOR (.cbor) or NDJSON (.jsonl/.ndjson) by extension
+int cmd_simulate(const Args& a) {
+  char* end = nullptr;
+  const unsigned long long t = strtoull(a.t.c_str(), &end, 10);
+  const unsigned long long b = strtoull(a.b.c_str(), nullptr, 10);
+  const unsigned long long tau = strtoull(a.tau.c_str(), nullptr, 10);
+  if (t == 0 || t > 0xFFFFFFFFull || b == 0 || tau == 0 || tau > 255) {
+    fprintf(stderr, "Error: need --t in 1..=2^32-1, --b >= 1, --tau in 1..=255\n");
+    return 2;
+  }
+  if (b > t) {
+    fprintf(stderr, "Error: number of blocks b (%llu) cannot exceed trace length T (%llu)\n", b, t);
+    return 1;
+  }
+  const std::string e = ext_lower(a.out);
+  if (e != "cbor" && e != "jsonl" && e != "ndjson") {
+    fprintf(stderr, "Error: --out-blocks must end in .cbor, .jsonl or .ndjson\n");
+    return 2;
+  }
+  sezkp_blocks* h = nullptr;
+  char err[512] = {0};
+  if (sezkp_simulate_blocks(t, (uint32_t)b, (uint32_t)tau, 42, &h, err, sizeof err) != SEZKP_OK) {
+    fprintf(stderr, "Error: %s\n", err);
+    return 1;
+  }
+  const sezkp_block_view* v = sezkp_blocks_view(h);
+  const uint32_t nb = v->n_blocks;
+  sezkp_buf buf{};
+  const int32_t rc = e == "cbor" ? sezkp_blocks_encode_cbor(v, &buf) : sezkp_blocks_encode_jsonl(v, &buf);
+  sezkp_blocks_free(h);
+  if (rc != SEZKP_OK) { fprintf(stderr, "Error: encoding blocks failed (%d)\n", rc); return 1; }
+  std::vector<uint8_t> out(buf.data, buf.data + buf.len);
+  sezkp_buf_free(&buf);
+  std::string werr;
+  if (!write_file(a.out, out, werr)) { fprintf(stderr, "Error: %s\n", werr.c_str()); return 1; }
+  printf("Simulated trace: T=%llu, b=%llu, \xcf\x84=%llu \xe2\x86\x92 %u blocks \xe2\x86\x92 %s\n", t, b, tau, nb,
+         a.out.c_str());
+  return 0;
+}
+
 void usage() {
   fprintf(stderr,
           "usage: sezkp-cli prove  --backend stark --blocks B --manifest M --out P [--stream] [--assume-committed]\n"
           "       sezkp-cli verify --backend stark --blocks B --manifest M --proof P [--assume-committed]\n"
-          "       sezkp-cli commit --blocks B --out M\n");
+          "       sezkp-cli commit --blocks B --out M\n"
+          "       sezkp-cli simulate --t T --b STEPS_PER_BLOCK --tau TAU --out-blocks B(.cbor|.jsonl)\n");
 }
 
 }  // namespace
@@ -231,12 +274,17 @@ int main(int argc, char** argv) {
     else if (s == "--manifest") val(a.manifest);
     else if (s == "--out" || s == "-o") val(a.out);
     else if (s == "--proof") val(a.proof);
+    else if (s == "--out-blocks") val(a.out);
+    else if (s == "--t") val(a.t);
+    else if (s == "--b") val(a.b);
+    else if (s == "--tau") val(a.tau);
     else if (s == "--stream") a.stream = true;
     else if (s == "--assume-committed") a.assume = true;
     else { fprintf(stderr, "unknown argument %s\n", s.c_str()); usage(); return 2; }
   }
   for (auto& c : a.backend) c = (char)tolower((unsigned char)c);
   if (a.cmd == "commit") return cmd_commit(a);
+  if (a.cmd == "simulate") return cmd_simulate(a);
   if (a.backend != "stark") {
     fprintf(stderr, "Error: only --backend stark is implemented by the MI355X build\n");
     return 2;

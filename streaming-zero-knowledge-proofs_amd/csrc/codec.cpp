@@ -493,6 +493,59 @@ std::string encode_blocks_jsonl(const sezkp_block_view& v) {
   return o;
 }
 
+// Vec<BlockSummary> as ciborium writes it (sezkp-core types.rs:116-151, io.rs
+// write path): maps with serde field order, minimal-length ints, Option ->
+// null, [u8;16] tags -> arrays of uints (zero).
+std::vector<uint8_t> encode_blocks_cbor(const sezkp_block_view& v) {
+  std::vector<uint8_t> o;
+  const uint32_t tau = v.tau;
+  o.reserve((size_t)v.step_start[v.n_blocks] * (24 + 12 * tau) + (size_t)v.n_blocks * (200 + 60 * tau));
+  auto sint = [&](int64_t x) { if (x >= 0) cb_head(o, 0, (uint64_t)x); else cb_head(o, 1, (uint64_t)(-1 - x)); };
+  auto key = [&](const char* k) { cb_text(o, k); };
+  static const uint8_t zero_tag[16] = {0};
+  cb_head(o, 4, v.n_blocks);
+  for (uint32_t k = 0; k < v.n_blocks; k++) {
+    cb_head(o, 5, 14);
+    key("version"); cb_head(o, 0, v.version[k]);
+    key("block_id"); cb_head(o, 0, v.block_id[k]);
+    key("step_lo"); cb_head(o, 0, v.step_lo[k]);
+    key("step_hi"); cb_head(o, 0, v.step_hi[k]);
+    key("ctrl_in"); cb_head(o, 0, v.ctrl_in[k]);
+    key("ctrl_out"); cb_head(o, 0, v.ctrl_out[k]);
+    key("in_head_in"); sint(v.in_head_in[k]);
+    key("in_head_out"); sint(v.in_head_out[k]);
+    key("windows"); cb_head(o, 4, tau);
+    for (uint32_t r = 0; r < tau; r++) {
+      cb_head(o, 5, 2);
+      key("left"); sint(v.win_left[(size_t)k * tau + r]);
+      key("right"); sint(v.win_right[(size_t)k * tau + r]);
+    }
+    key("head_in_offsets"); cb_head(o, 4, tau);
+    for (uint32_t r = 0; r < tau; r++) cb_head(o, 0, v.off_in[(size_t)k * tau + r]);
+    key("head_out_offsets"); cb_head(o, 4, tau);
+    for (uint32_t r = 0; r < tau; r++) cb_head(o, 0, v.off_out[(size_t)k * tau + r]);
+    key("movement_log"); cb_head(o, 5, 1);
+    key("steps"); cb_head(o, 4, v.step_start[k + 1] - v.step_start[k]);
+    for (uint64_t st = v.step_start[k]; st < v.step_start[k + 1]; st++) {
+      cb_head(o, 5, 2);
+      key("input_mv"); sint(v.input_mv[st]);
+      key("tapes"); cb_head(o, 4, tau);
+      for (uint32_t r = 0; r < tau; r++) {
+        const size_t i = (size_t)st * tau + r;
+        cb_head(o, 5, 2);
+        key("write");
+        if (v.has_write[i]) cb_head(o, 0, v.wsym[i]); else o.push_back(0xf6);
+        key("mv"); sint(v.mv[i]);
+      }
+    }
+    key("pre_tags"); cb_head(o, 4, tau);
+    for (uint32_t r = 0; r < tau; r++) cb_byte_array(o, zero_tag, 16);
+    key("post_tags"); cb_head(o, 4, tau);
+    for (uint32_t r = 0; r < tau; r++) cb_byte_array(o, zero_tag, 16);
+  }
+  return o;
+}
+
 bool decode_manifest_cbor(const uint8_t* data, size_t len, uint8_t root[32], uint32_t* n_leaves, std::string& err) {
   try {
     Cbor d(data, len);

@@ -29,6 +29,10 @@ bool decode_blocks_cbor(const uint8_t* data, size_t len, BlockStore& out, std::s
 bool decode_blocks_json(const char* data, size_t len, BlockStore& out, std::string& err);
 bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::string& err);
 std::string encode_blocks_jsonl(const sezkp_block_view& v);
+std::vector<uint8_t> encode_blocks_cbor(const sezkp_block_view& v);
+// partition_trace (partition.rs:43-150) of a step-major movement log into blocks of b steps
+void partition_trace(BlockStore& s, uint64_t t, uint32_t tau, uint32_t b, const int8_t* input_mv, const int8_t* mv,
+                     const uint8_t* has_write, const uint16_t* wsym);
 bool decode_manifest_cbor(const uint8_t* data, size_t len, uint8_t root[32], uint32_t* n_leaves, std::string& err);
 bool decode_manifest_json(const char* data, size_t len, uint8_t root[32], uint32_t* n_leaves, std::string& err);
 

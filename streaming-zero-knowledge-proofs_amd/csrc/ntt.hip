@@ -407,6 +407,59 @@ __global__ void k_bitrev_permute_small(const uint64_t* __restrict__ in, uint64_t
   }
 }
 
+// ------------------------------------------------ distributed four-step NTT
+// N = P * M points over P ranks (BASELINE config 4). Rank g holds
+// x[g + P j] (j < M) and, after a local M-point NTT Y_g (bit-reversed), this
+// kernel writes s[k2] = Y_g[k2] * w_N^(+-g k2) (* scale) in natural k2 order:
+// s is already the all-to-all send image (peer d gets k2 in [d M/P, (d+1) M/P)).
+// Same 16x16 LDS tile as k_bitrev_permute. The inverse transform runs the
+// pipeline backwards and twiddles by the SOURCE index (tw_src = 1).
+__global__ void __launch_bounds__(256) k_dntt_permute_twiddle(const uint64_t* __restrict__ in,
+                                                               uint64_t* __restrict__ out, int logM, NttTables T,
+                                                               uint64_t e_step, int inverse, int tw_src,
+                                                               uint64_t scale) {
+  __shared__ uint64_t sh[16 * 17];
+  const int a = 4, b = logM - 2 * a;
+  const uint32_t y = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int x = tid >> 4, z = tid & 15;
+  const uint32_t ry = b ? (__brev(y) >> (32 - b)) : 0;
+  sh[x * 17 + z] = in[((uint64_t)x << (a + b)) | ((uint64_t)y << a) | z];
+  __syncthreads();
+  const int rz = tid >> 4, rx = tid & 15;
+  const int zz = __brev((uint32_t)rz) >> 28, xx = __brev((uint32_t)rx) >> 28;
+  const uint64_t k2 = ((uint64_t)rz << (a + b)) | ((uint64_t)ry << a) | rx;
+  const uint64_t src = ((uint64_t)xx << (a + b)) | ((uint64_t)y << a) | zz;
+  uint64_t v = sh[xx * 17 + zz];
+  if (e_step) v = gl_mul(v, tw_pow(T, (tw_src ? src : k2) * e_step, inverse != 0));
+  if (scale != 1) v = gl_mul(v, scale);
+  out[k2] = v;
+}
+
+// After the all-to-all r[g * Q + q] = rank g's s[d Q + q] (Q = M/P). In place:
+// r[k1 * Q + q] = sum_g w_P^(+-g k1) r[g * Q + q] = X[d Q + q + M k1]. The
+// P-point DFT uses only powers of two (w_8 = 2^120), i.e. shifts.
+template <int P, bool INV>
+__global__ void __launch_bounds__(256) k_dntt_dft(uint64_t* __restrict__ r, uint64_t Q) {
+  const uint64_t q = blockIdx.x * 256ull + threadIdx.x;
+  if (q >= Q) return;
+  uint64_t v[P], o[P];
+#pragma unroll
+  for (int g = 0; g < P; g++) v[g] = r[g * Q + q];
+#pragma unroll
+  for (int k1 = 0; k1 < P; k1++) {
+    uint64_t acc = v[0];
+#pragma unroll
+    for (int g = 1; g < P; g++) {
+      const int j = (g * k1) % P;
+      acc = gl_add(acc, j ? tw_small<INV>(v[g], j, P / 2) : v[g]);  // w_P^j
+    }
+    o[k1] = acc;
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < P; k1++) r[k1 * Q + q] = o[k1];
+}
+
 // ------------------------------------------------------------------ host side
 // SEZKP_NTT_RADIX2=1 forces the radix-2 LDS passes (A/B comparison)
 static bool ntt4_disabled() {
@@ -479,4 +532,23 @@ hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int
   return hipGetLastError();
 }
 
+hipError_t dntt_permute_twiddle(hipStream_t st, const uint64_t* in, uint64_t* out, int logM, const NttTables& T,
+                                uint64_t e_step, bool inverse, bool tw_src, uint64_t scale) {
+  if (logM < 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dntt_permute_twiddle, dim3(1u << (logM - 8)), dim3(256), 0, st, in, out, logM, T, e_step,
+                     inverse ? 1 : 0, tw_src ? 1 : 0, scale);
+  return hipGetLastError();
+}
+hipError_t dntt_dft(hipStream_t st, uint64_t* r, int P, uint64_t Q, bool inverse) {
+  const dim3 g((unsigned)((Q + 255) / 256));
+#define SEZKP_DFT(PP)                                                                              \
+  if (P == PP) {                                                                                   \
+    if (inverse) hipLaunchKernelGGL((k_dntt_dft<PP, true>), g, dim3(256), 0, st, r, Q);           \
+    else hipLaunchKernelGGL((k_dntt_dft<PP, false>), g, dim3(256), 0, st, r, Q);                  \
+    return hipGetLastError();                                                                      \
+  }
+  SEZKP_DFT(2) SEZKP_DFT(4) SEZKP_DFT(8)
+#undef SEZKP_DFT
+  return P == 1 ? hipSuccess : hipErrorInvalidValue;
+}
 }  // namespace sezkp

@@ -1049,6 +1049,51 @@ int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max)
 }
 void* sezkp_ctx_stream(const sezkp_ctx* ctx) { return ctx ? (void*)ctx->st : nullptr; }
 
+// Distributed four-step NTT over the context's ranks (BASELINE
+// config 4). Forward: local M-point NTT (DIF) -> bit-reverse + w_N^(g k2)
+// twiddle into the send image -> one all-to-all -> in-place P-point DFTs.
+// Inverse: the same pipeline backwards, so the two round-trip in place.
+int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, uint32_t log_n, int32_t dir,
+                           char* err, size_t err_len) {
+  try {
+    if (!ctx || !local || !scratch) throw Err{SEZKP_E_INVALID, "null argument"};
+    if (dir != 1 && dir != -1) throw Err{SEZKP_E_INVALID, "dir must be +1 or -1"};
+    const int P = ctx->world, logP = ctx->logP;
+    if (log_n > 32 || (int)log_n < 8 + logP)
+      throw Err{SEZKP_E_INVALID, "dist_ntt needs 2^(8 + log P) <= n <= 2^32"};
+    HIP_OR_THROW(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->st;
+    const int logM = (int)log_n - logP;
+    const uint64_t M = 1ULL << logM, Q = M >> logP;
+    const uint64_t e_step = (uint64_t)ctx->rank << (32 - log_n);  // w_N^(g k) = w_{2^32}^(g k 2^(32 - log n))
+    const bool inv = dir < 0;
+    auto ok = [](hipError_t e, const char* what) {
+      if (e != hipSuccess) throw Err{SEZKP_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
+    };
+    if (!inv) {
+      ok(ntt_dif(st, local, logM, false, ctx->tw), "dist_ntt local");
+      ok(dntt_permute_twiddle(st, local, scratch, logM, ctx->tw, e_step, false, false, 1), "dist_ntt twiddle");
+      if (P > 1) ctx->comm->alltoall(scratch, local, Q * 8, st);
+      else HIP_OR_THROW(hipMemcpyAsync(local, scratch, M * 8, hipMemcpyDeviceToDevice, st));
+      ok(dntt_dft(st, local, P, Q, false), "dist_ntt dft");
+    } else {
+      const uint64_t inv_n = hgl_inv((1ULL << log_n) % GL_P_HOST);
+      ok(dntt_dft(st, local, P, Q, true), "dist_ntt dft");
+      if (P > 1) ctx->comm->alltoall(local, scratch, Q * 8, st);
+      else HIP_OR_THROW(hipMemcpyAsync(scratch, local, M * 8, hipMemcpyDeviceToDevice, st));
+      ok(dntt_permute_twiddle(st, scratch, local, logM, ctx->tw, e_step, true, true, inv_n), "dist_ntt twiddle");
+      ok(ntt_dit(st, local, logM, true, ctx->tw, nullptr, 0, 1), "dist_ntt local");
+    }
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+    return SEZKP_E_DEVICE;
+  }
+}
+
 static std::vector<MetaEntry> meta_for(uint64_t domain_n, uint32_t tau, uint32_t flags) {
   std::vector<MetaEntry> m = {{"proto", true, "stark-v1", 0}, {"domain_n", false, "", domain_n}, {"tau", false, "", tau}};
   if (flags & SEZKP_FLAG_STREAMING) m.push_back({"mode", true, "streaming", 0});
@@ -1192,6 +1237,39 @@ int32_t sezkp_blocks_decode_jsonl(const uint8_t* data, size_t len, sezkp_blocks*
   }
   *out = b.release();
   return SEZKP_OK;
+}
+// `sezkp-cli simulate --t T --b b --tau tau` (main.rs:317-350): generate_trace
+// (tracegen.cpp, rand 0.9 StdRng bit-exact; the reference fixes seed 42) +
+// partition_trace into blocks of b steps.
+int32_t sezkp_simulate_blocks(uint64_t t, uint32_t b, uint32_t tau, uint64_t seed, sezkp_blocks** out, char* err,
+                              size_t err_len) {
+  try {
+    if (!out || b == 0 || tau > 255 || t == 0 || t > (1ULL << 32)) {
+      set_err(err, err_len, "simulate: need 0 < t <= 2^32, b > 0, tau <= 255");
+      return SEZKP_E_INVALID;
+    }
+    std::vector<int8_t> imv(t), mv(t * tau);
+    std::vector<uint8_t> hw(t * tau);
+    std::vector<uint16_t> ws(t * tau);
+    int32_t rc = sezkp_simulate_trace(t, tau, seed, imv.data(), mv.data(), hw.data(), ws.data());
+    if (rc != SEZKP_OK) return rc;
+    std::unique_ptr<sezkp_blocks> bl(new sezkp_blocks());
+    partition_trace(bl->s, t, tau, b, imv.data(), mv.data(), hw.data(), ws.data());
+    *out = bl.release();
+    return SEZKP_OK;
+  } catch (const std::bad_alloc&) {
+    set_err(err, err_len, "simulate: out of host memory");
+    return SEZKP_E_NOMEM;
+  }
+}
+int32_t sezkp_blocks_encode_cbor(const sezkp_block_view* blocks, sezkp_buf* out) {
+  try {
+    if (!blocks || !out) return SEZKP_E_INVALID;
+    to_buf(encode_blocks_cbor(*blocks), out);
+    return SEZKP_OK;
+  } catch (const std::exception&) {
+    return SEZKP_E_NOMEM;
+  }
 }
 int32_t sezkp_blocks_encode_jsonl(const sezkp_block_view* blocks, sezkp_buf* out) {
   try {

@@ -33,6 +33,10 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
                    const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e = 0);
 hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale,
                           bool do_scale);
+// distributed four-step NTT pieces (ntt.hip)
+hipError_t dntt_permute_twiddle(hipStream_t st, const uint64_t* in, uint64_t* out, int logM, const NttTables& T,
+                                uint64_t e_step, bool inverse, bool tw_src, uint64_t scale);
+hipError_t dntt_dft(hipStream_t st, uint64_t* r, int P, uint64_t Q, bool inverse);
 
 // A binary Merkle tree over 2^logLen leaves whose levels >= lstore are kept
 // in HBM: level l (lstore <= l <= logLen) starts at node

@@ -6,7 +6,7 @@ C ABI in include/sezkp_stark.h. All compute runs in lib/libsezkp_stark.so
 """
 from ._lib import LIB_PATH, SezkpError, lib  # noqa: F401  (raises ImportError if the .so is missing)
 from .backend import STAGES, ProofArtifact, ProverContext, ShardedProverContext, StarkV1  # noqa: F401
-from .blocks import BlockSoA, partition, simulate, synthetic_blocks  # noqa: F401
+from .blocks import BlockSoA, partition, reference_blocks, reference_trace, simulate, synthetic_blocks  # noqa: F401
 
 __all__ = ["StarkV1", "ProverContext", "ShardedProverContext", "ProofArtifact", "BlockSoA", "SezkpError", "simulate", "partition",
-           "synthetic_blocks", "STAGES", "LIB_PATH", "lib"]
+           "synthetic_blocks", "reference_blocks", "reference_trace", "STAGES", "LIB_PATH", "lib"]

@@ -27,7 +27,8 @@ EXPORTS = [
     "sezkp_gl_coset_lde_deep", "sezkp_fri_fold_commit", "sezkp_merkle_root_u64", "sezkp_manifest_root",
     "sezkp_blocks_decode_cbor", "sezkp_blocks_view", "sezkp_blocks_free", "sezkp_blake3",
     "sezkp_comm_unique_id", "sezkp_ctx_create_sharded", "sezkp_ctx_create_sharded_host", "sezkp_ctx_prove_borrow",
-    "sezkp_blocks_decode_jsonl", "sezkp_blocks_encode_jsonl", "sezkp_manifest_decode",
+    "sezkp_blocks_decode_jsonl", "sezkp_blocks_encode_jsonl", "sezkp_manifest_decode", "sezkp_ctx_dist_ntt",
+    "sezkp_blocks_encode_cbor", "sezkp_simulate_trace", "sezkp_simulate_blocks",
 ]
 
 
@@ -104,6 +105,10 @@ def _load():
     L.sezkp_ctx_create_sharded.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_char_p] + E
     L.sezkp_ctx_create_sharded_host.restype = C.c_void_p
     L.sezkp_ctx_create_sharded_host.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.POINTER(HostComm)] + E
+    L.sezkp_blocks_encode_cbor.argtypes = [C.POINTER(BlockView), C.POINTER(Buf)]
+    L.sezkp_simulate_trace.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64] + [C.c_void_p] * 4
+    L.sezkp_simulate_blocks.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)] + E
+    L.sezkp_ctx_dist_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32] + E
     return L
 
 

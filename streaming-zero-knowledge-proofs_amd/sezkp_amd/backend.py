@@ -138,6 +138,28 @@ class ProverContext:
         n = lib.sezkp_ctx_stage_times(self._h, buf, 32)
         return {STAGES[i]: buf[i] for i in range(min(n, len(STAGES)))}
 
+    def dist_ntt(self, local, scratch=None, inverse: bool = False, sync: bool = True):
+        """Distributed four-step NTT of n = world * local.numel() points, in
+        place on `local` (a device u64/i64 tensor; layouts in sezkp_stark.h,
+        sezkp_ctx_dist_ntt). Every rank calls it together."""
+        import torch
+        if local.dtype not in (torch.int64, torch.uint64) or not local.is_cuda or not local.is_contiguous():
+            raise SezkpError(-1, "local must be a contiguous 64-bit device tensor")
+        m = local.numel()
+        if m & (m - 1):
+            raise SezkpError(-1, "local length must be a power of two")
+        if scratch is None:
+            scratch = torch.empty_like(local)
+        log_n = (m * self.world).bit_length() - 1
+        if sync:
+            torch.cuda.current_stream(local.device).synchronize()
+        err = C.create_string_buffer(1024)
+        check(lib.sezkp_ctx_dist_ntt(self._h, local.data_ptr(), scratch.data_ptr(), log_n, -1 if inverse else 1,
+                                     err, 1024), err)
+        if sync:
+            torch.cuda.ExternalStream(self.stream, device=local.device).synchronize()
+        return local
+
     @property
     def stream(self) -> int:
         return lib.sezkp_ctx_stream(self._h) or 0

@@ -5,8 +5,10 @@
 (`sezkp-cli simulate`: crates/sezkp-trace/src/generator.rs:38-73 and
 partition.rs:43-150) with numpy: same distributions (input/tape moves uniform
 in {-1,0,1}, writes with p=0.4 of a symbol in 0..=15) and the same partition
-semantics, but a numpy PCG64 stream instead of rand 0.9's ChaCha12 StdRng, so
-the traces are a deterministic stand-in, not the reference's exact bytes.
+semantics, but a numpy PCG64 stream (any seed, fast) instead of rand 0.9's
+ChaCha12 StdRng. `reference_trace()` / `reference_blocks()` are the bit-exact
+restatement of the reference's own generator (tracegen.cpp), pinned by the
+reference's trace.cbor / blocks.cbor fixtures.
 """
 from __future__ import annotations
 
@@ -82,6 +84,14 @@ class BlockSoA:
             raise SezkpError(rc, "encode jsonl")
         return take_buf(b)
 
+    def to_cbor(self) -> bytes:
+        """Vec<BlockSummary> as the reference writes blocks.cbor (ciborium), via the C ABI."""
+        b = Buf()
+        rc = lib.sezkp_blocks_encode_cbor(C.byref(self.view()), C.byref(b))
+        if rc != 0:
+            raise SezkpError(rc, "encode cbor")
+        return take_buf(b)
+
     @classmethod
     def _decode(cls, fn, data: bytes) -> "BlockSoA":
         h = C.c_void_p()
@@ -89,6 +99,11 @@ class BlockSoA:
         rc = fn(data, len(data), C.byref(h), err, 512)
         if rc != 0:
             raise SezkpError(rc, err.value.decode())
+        return cls._take(h)
+
+    @classmethod
+    def _take(cls, h) -> "BlockSoA":
+        """Copy a library-owned sezkp_blocks into numpy arrays and free it."""
         try:
             v = lib.sezkp_blocks_view(h).contents
             nb, tau = v.n_blocks, v.tau
@@ -153,6 +168,31 @@ def partition(input_mv, mv, has_write, wsym, b: int) -> BlockSoA:
         step_start=np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64),
         input_mv=input_mv, mv=mv.reshape(-1), has_write=has_write.reshape(-1), wsym=wsym.reshape(-1),
     )
+
+
+def reference_trace(t: int, tau: int, seed: int = 42):
+    """The reference's own `generate_trace(t, tau)` (generator.rs:38-73, rand
+    0.9.2 StdRng, bit-exact; the reference fixes seed 42), in the same
+    (input_mv[t], mv[t,tau], has_write[t,tau], wsym[t,tau]) form as simulate()."""
+    im = np.zeros(t, np.int8)
+    mv = np.zeros((t, tau), np.int8)
+    hw = np.zeros((t, tau), np.uint8)
+    ws = np.zeros((t, tau), np.uint16)
+    rc = lib.sezkp_simulate_trace(t, tau, seed, im.ctypes.data, mv.ctypes.data, hw.ctypes.data, ws.ctypes.data)
+    if rc != 0:
+        raise SezkpError(rc, "simulate_trace: tau must be <= 255")
+    return im, mv, hw, ws
+
+
+def reference_blocks(t: int, b: int = 512, tau: int = 8, seed: int = 42) -> BlockSoA:
+    """Exactly what `sezkp-cli simulate --t T --b b --tau tau` writes
+    (main.rs:317-350: generate_trace + partition_trace), built natively."""
+    h = C.c_void_p()
+    err = C.create_string_buffer(512)
+    rc = lib.sezkp_simulate_blocks(t, b, tau, seed, C.byref(h), err, 512)
+    if rc != 0:
+        raise SezkpError(rc, err.value.decode())
+    return BlockSoA._take(h)
 
 
 def synthetic_blocks(t: int, b: int = 512, tau: int = 8, seed: int = 42) -> BlockSoA:

@@ -1,0 +1,102 @@
+"""GPU parity of the distributed four-step NTT (sezkp_ctx_dist_ntt; SURVEY
+8(e), BASELINE config 4) against the oracle's single-domain NTT (ntt.rs:79-155).
+
+P ranks share the box's one GPU and exchange through HostCollectives (gloo);
+the kernels and layouts are the production ones, only the all-to-all
+transport differs from RCCL. Layouts (sezkp_stark.h): rank g's input is
+x[g + P j]; its output is X[g Q + q + M k1] at k1 Q + q (M = n/P, Q = M/P).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ORACLE, PKG
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def expected_local(X: np.ndarray, rank: int, world: int) -> np.ndarray:
+    M = X.size // world
+    Q = M // world
+    return X.reshape(world, M)[:, rank * Q:(rank + 1) * Q].reshape(-1)
+
+
+def _worker(rank, world, port, log_n, seed, q):
+    sys.path[:0] = [PKG, ORACLE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle_ctypes as orc
+        import sezkp_amd
+        x = orc.det_vec(1 << log_n, seed)
+        X = orc.ntt_forward(x)
+        ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
+        loc = torch.from_numpy(np.ascontiguousarray(x[rank::world]).view(np.int64)).cuda()
+        ctx.dist_ntt(loc)
+        fwd_ok = np.array_equal(loc.cpu().numpy().view(np.uint64), expected_local(X, rank, world))
+        ctx.dist_ntt(loc, inverse=True)
+        inv_ok = np.array_equal(loc.cpu().numpy().view(np.uint64), x[rank::world])
+        calls = dict(ctx._coll.calls)
+        ctx.close()
+        q.put((rank, fwd_ok, inv_ok, calls))
+    except Exception as e:
+        q.put((rank, f"ERR {type(e).__name__}: {e}", False, {}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_n,seed", [(2, 9, 1), (2, 16, 2), (4, 10, 3), (4, 20, 4), (8, 14, 5)])
+def test_dist_ntt_matches_oracle(gpu_ok, world, log_n, seed):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, log_n, seed, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for rank, fwd_ok, inv_ok, calls in res:
+        assert fwd_ok is True, f"rank {rank}: {fwd_ok}"
+        assert inv_ok, f"rank {rank}: inverse did not round-trip"
+        assert calls["alltoall"] == 2  # one transpose per direction
+
+
+@pytest.mark.parametrize("log_n", [8, 12, 20, 22])
+def test_dist_ntt_one_rank_is_plain_ntt(gpu_ok, product, oracle, log_n):
+    torch = gpu_ok
+    x = oracle.det_vec(1 << log_n, 40 + log_n)
+    ctx = product.ProverContext(0)
+    d = torch.from_numpy(x.view(np.int64).copy()).cuda()
+    ctx.dist_ntt(d)
+    np.testing.assert_array_equal(d.cpu().numpy().view(np.uint64), oracle.ntt_forward(x))
+    ctx.dist_ntt(d, inverse=True)
+    np.testing.assert_array_equal(d.cpu().numpy().view(np.uint64), x)
+    ctx.close()
+
+
+def test_dist_ntt_rejects_bad_sizes(gpu_ok, product):
+    import ctypes as C
+    import sezkp_amd._lib as L
+    torch = gpu_ok
+    ctx = product.ProverContext(0)
+    d = torch.zeros(128, dtype=torch.int64, device="cuda")
+    err = C.create_string_buffer(256)
+    assert L.lib.sezkp_ctx_dist_ntt(ctx._h, d.data_ptr(), d.data_ptr(), 7, 1, err, 256) == L.SEZKP_E_INVALID
+    assert b"2^(8 + log P)" in err.value
+    assert L.lib.sezkp_ctx_dist_ntt(ctx._h, d.data_ptr(), d.data_ptr(), 8, 0, err, 256) == L.SEZKP_E_INVALID
+    ctx.close()

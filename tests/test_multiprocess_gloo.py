@@ -186,3 +186,55 @@ def test_sharded_layout_model_gloo(oracle, world, log_n):
     for rank, ok_layout, ok_fold, root in res:
         assert ok_layout and ok_fold
         assert root == want
+
+
+GL = 0xFFFFFFFF00000001
+
+
+def _dntt_worker(rank, world, port, log_n, q):
+    """The four-step distributed NTT of sezkp_ctx_dist_ntt restated on the
+    CPU: local M-point NTT (oracle), twiddle w_N^(g k2), one gloo all-to-all,
+    P-point DFTs. Checks the algorithm and the documented layouts."""
+    sys.path[:0] = [PKG, ORACLE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle_ctypes as O
+        n = 1 << log_n
+        M, Q = n // world, n // world // world
+        x = O.det_vec(n, 5)
+        Y = O.ntt_forward(np.ascontiguousarray(x[rank::world]))
+        wN = pow(7, (GL - 1) >> log_n, GL)
+        s = np.array([int(Y[k]) * pow(wN, rank * k, GL) % GL for k in range(M)], dtype=np.uint64)
+        recv = torch.empty(M, dtype=torch.int64)
+        dist.all_to_all_single(recv, torch.from_numpy(s.view(np.int64)))
+        r = recv.numpy().view(np.uint64)
+        wP = pow(7, (GL - 1) // world, GL)
+        out = np.zeros(M, dtype=np.uint64)
+        for qq in range(Q):
+            v = [int(r[g * Q + qq]) for g in range(world)]
+            for k1 in range(world):
+                out[k1 * Q + qq] = sum(v[g] * pow(wP, g * k1, GL) for g in range(world)) % GL
+        X = O.ntt_forward(x)
+        want = X.reshape(world, M)[:, rank * Q:(rank + 1) * Q].reshape(-1)
+        q.put((rank, bool(np.array_equal(out, want))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_n", [(2, 10), (4, 10)])
+def test_four_step_dist_ntt_model_gloo(oracle, world, log_n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dntt_worker, args=(r, world, port, log_n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)
