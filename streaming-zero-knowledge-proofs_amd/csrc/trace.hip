@@ -409,19 +409,14 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
                                                         uint64_t m3, NttTables tw, int logn, uint64_t* __restrict__ out,
                                                         uint64_t row0, uint64_t row_end) {
   const uint64_t n = T.n;
-  // lane rows i0 + 256 j (j < 4): every load/store instruction covers 64
-  // consecutive rows (coalesced), row i+1 shares the neighbour's cache line
-  const uint64_t i0 = row0 + (uint64_t)blockIdx.x * TR_THREADS * 4 + threadIdx.x;
-  if (i0 >= row_end) return;
-  // x = w_n^i0, then x *= w_n^256
-  const uint64_t e0 = i0 << (tw.K - logn), e1 = (uint64_t)TR_THREADS << (tw.K - logn);
-  const uint64_t smask = (1ULL << tw.S) - 1;
-  uint64_t x = gl_mul(tw.hi[e0 >> tw.S], tw.lo[e0 & smask]);
-  const uint64_t e1m = e1 & ((tw.K >= 64) ? ~0ULL : ((1ULL << tw.K) - 1));
-  const uint64_t wn = gl_mul(tw.hi[e1m >> tw.S], tw.lo[e1m & smask]);
-  for (int j = 0; j < 4; j++) {
-    const uint64_t i = i0 + (uint64_t)j * TR_THREADS;
-    if (i >= row_end) break;
+  // one row per lane: each load instruction covers 64 consecutive rows
+  // (coalesced), row i+1 shares the neighbour's cache line; many rows in
+  // flight per CU hide the dependent loads of the tape loop
+  const uint64_t i = row0 + (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
+  if (i >= row_end) return;
+  const uint64_t e0 = i << (tw.K - logn);
+  const uint64_t x = gl_mul(tw.hi[e0 >> tw.S], tw.lo[e0 & ((1ULL << tw.S) - 1)]);  // w_n^i
+  {
     const uint64_t ip1 = (i + 1) & (n - 1);
     const uint8_t fl = T.row_flags[i];
     const bool is_first = fl & 1, is_last = (fl >> 1) & 1;
@@ -431,6 +426,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
     // small) and multiplied once: sum_r a*t_r = a * sum_r t_r in the field.
     int64_t s_c2 = 0, s_c3 = 0, s_sy = 0;
     uint64_t s_hr = 0, s_sl = 0, s_bf = 0, s_bl = 0;
+#pragma unroll 4
     for (int r = 0; r < T.tau; r++) {
       const uint64_t o = (uint64_t)r * n;
       const int64_t mv = T.mv[o + i];
@@ -471,7 +467,6 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
     // mask R(x) = m0 + m1 x + m2 x^2 + m3 x^3 (Horner)
     uint64_t R = gl_add(gl_mul(gl_add(gl_mul(gl_add(gl_mul(m3, x), m2), x), m1), x), m0);
     out[i] = gl_add(acc, R);
-    x = gl_mul(x, wn);
   }
 }
 
@@ -963,8 +958,7 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
                           const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows) {
   if (row0 + nrows > T.n) return hipErrorInvalidValue;
-  const uint64_t thr = (nrows + 3) / 4;
-  const unsigned grid = (unsigned)((thr + TR_THREADS - 1) / TR_THREADS);
+  const unsigned grid = (unsigned)((nrows + TR_THREADS - 1) / TR_THREADS);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(k_compose, dim3(grid), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3], tw,
                      logn, out, row0, row0 + nrows);

@@ -169,6 +169,21 @@ def test_prove_wide_values_bit_exact(gpu_ok, product, oracle):
     assert art.proof_bytes == oracle.prove_v1(blocks, mroot)
 
 
+@pytest.mark.parametrize("bad", [0, 5, 65537])
+def test_prove_invalid_moves_bit_exact(gpu_ok, product, oracle, bad):
+    """`bad` rows move by +-2 (AIR C2: mv^3 - mv != 0 on exactly those rows,
+    the rest of the trace valid): the proof still equals the reference's."""
+    T, tau = 1 << 17, 1
+    imv = np.zeros(T, np.int8)
+    mv = np.zeros((T, tau), np.int8)
+    mv[:bad, 0] = np.where(np.arange(bad) % 2 == 0, 2, -2)
+    hw = np.zeros((T, tau), np.uint8)
+    ws = np.zeros((T, tau), np.uint16)
+    blocks = product.partition(imv, mv, hw, ws, 4096)
+    mroot = blocks.manifest_root()
+    assert product.StarkV1.prove(blocks, mroot).proof_bytes == oracle.prove_v1(blocks, mroot)
+
+
 def test_prove_dictionary_branches_bit_exact(gpu_ok, product, oracle, monkeypatch):
     """Dense columns are committed through range dictionaries whose table level K
     is chosen per column on the device; force every branch at T = 2^17 in one
