@@ -353,7 +353,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     t.tab = NO_TAB;
     t.tab_log = 0;
     if (use_dict && kind_dict(t.kind)) {
-      dcols.push_back(DictCol{(uint32_t)c, 0, (uint64_t)dcols.size() * DICT_LEVELS * DICT_CAP});
+      dcols.push_back(DictCol{(uint32_t)c, NO_DICT, (uint64_t)dcols.size() * DICT_LEVELS * DICT_CAP});
     } else if (kind_has_leaf_table(t.kind)) {
       t.tab_log = t.kind == 5 ? 16 : 8;
       t.tab = tab_nodes;
@@ -421,6 +421,10 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   n_tab_cols = (int)tab_cols.size();
   d_tab_cols = dalloc<uint32_t>(tab_cols.size() + 1);
   up(d_tab_cols, tab_cols.data(), tab_cols.size());
+  for (DictCol& h : dcols)  // head columns: the same tape's mv column (delta plan)
+    if (tm[h.col].kind == 6)
+      for (size_t i = 0; i < dcols.size(); i++)
+        if (tm[dcols[i].col].kind == 3 && tm[dcols[i].col].tape == tm[h.col].tape) h.mv = (uint32_t)i;
   n_dict = (int)dcols.size();
   d_dcols = dalloc<DictCol>(dcols.size() + 1);
   up(d_dcols, dcols.data(), dcols.size());

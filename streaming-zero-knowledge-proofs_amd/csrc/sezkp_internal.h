@@ -105,7 +105,7 @@ constexpr int DICT_LEVELS = 5;          // tables T_0..T_4
 constexpr uint32_t DICT_CAP = 65536;    // entries per table level
 struct DictCol {
   uint32_t col;
-  uint32_t pad;
+  uint32_t mv;   // head columns: dictionary index of the same tape's mv column (delta plan), else NO_DICT
   uint64_t tab;  // node offset of this column's DICT_LEVELS x DICT_CAP tables
 };
 struct DictPlan {
@@ -113,8 +113,16 @@ struct DictPlan {
   uint32_t R;    // range size (codes = raw - min < R)
   int32_t K;     // table level used by the commit kernel; -1 = leaves computed
   uint32_t pw[DICT_LEVELS];  // entries of T_k = R^(2^k) (0 above K)
+  uint32_t delta;  // head delta plan: K = 2 and slot 2 holds TD (below)
+  int64_t dmin;    // delta plan: range of the tape's moves
+  uint32_t dR;
   uint32_t pad;
 };
+// Head delta plan: inside a block head[r] = head[r-1] + mv[r], so an aligned
+// 4-row head group is a function of (head[g], mv[g+1], mv[g+2], mv[g+3]):
+// TD[c0 + R (d1 + dR d2 + dR^2 d3)] = H(T_1[c0 + R c1], T_1[c2 + R c3]) with
+// c_j = c_{j-1} + mv_j (codes). Groups with a block start at g+1..g+3 use
+// the two T_1 nodes directly. Needs R^2 <= DICT_CAP and R dR^3 <= DICT_CAP.
 __host__ __device__ inline bool kind_dict(uint32_t kind) { return kind == 0 || (kind >= 3 && kind <= 6); }
 // Chunk levels 6..9 of every dictionary column (16 + 8 + 4 + 2 nodes per
 // 1024-row chunk), written by the commitment, read by the openings.

@@ -652,6 +652,32 @@ struct DictNodes {
     node_load(tab + 8 * (uint64_t)idx, h);
   }
 };
+// head delta plan: node j = the 4-row group at row 4j of the lane
+struct DeltaNodes {
+  const int64_t* hp;      // head, first row of the lane
+  const int8_t* mp;       // mv of the same tape
+  const uint8_t* fp;      // row_flags (bit 0 = block start)
+  const uint32_t* t1;     // T_1
+  const uint32_t* td;     // TD
+  int64_t mn, dmin;
+  uint32_t R, dR;
+  __device__ __forceinline__ void get(int j, uint32_t (&h)[8]) const {
+    const uint64_t g = (uint64_t)j << 2;
+    const uint32_t f = *reinterpret_cast<const uint32_t*>(fp + g);
+    const int64_t c0 = hp[g] - mn;
+    if (!(f & 0x01010100u)) {
+      const uint32_t m = *reinterpret_cast<const uint32_t*>(mp + g);
+      const int64_t d1 = (int64_t)(int8_t)(m >> 8) - dmin, d2 = (int64_t)(int8_t)(m >> 16) - dmin,
+                    d3 = (int64_t)(int8_t)(m >> 24) - dmin;
+      node_load(td + 8 * (uint64_t)(c0 + (int64_t)R * (d1 + (int64_t)dR * (d2 + (int64_t)dR * d3))), h);
+    } else {  // a block starts inside the group: two T_1 nodes
+      uint32_t a[8], b[8];
+      node_load(t1 + 8 * (uint64_t)(c0 + (int64_t)R * (hp[g + 1] - mn)), a);
+      node_load(t1 + 8 * (uint64_t)((hp[g + 2] - mn) + (int64_t)R * (hp[g + 3] - mn)), b);
+      b3_parent(a, b, h);
+    }
+  }
+};
 template <typename Key>
 struct RawLeaves {
   const Key* p;
@@ -737,12 +763,12 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const Col
 }
 
 // one WG per dictionary column: reduce the partial ranges and choose K
-__global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restrict__ part, uint32_t nparts,
-                                                          uint64_t n, DictPlan* __restrict__ plans) {
-  __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
+// WG-wide min / max of one column's partial ranges (result valid on tid 0)
+__device__ __forceinline__ void reduce_parts(const int64_t* pp, uint32_t nparts, int64_t& lo, int64_t& hi,
+                                             int64_t* slo, int64_t* shi) {
   const int tid = threadIdx.x;
-  int64_t lo = INT64_MAX, hi = INT64_MIN;
-  const int64_t* pp = part + 2 * (uint64_t)blockIdx.x * nparts;
+  lo = INT64_MAX;
+  hi = INT64_MIN;
   for (uint32_t i = tid; i < nparts; i += TR_THREADS) {
     lo = pp[2 * i] < lo ? pp[2 * i] : lo;
     hi = pp[2 * i + 1] > hi ? pp[2 * i + 1] : hi;
@@ -755,11 +781,23 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restr
   }
   if ((tid & 63) == 0) { slo[tid >> 6] = lo; shi[tid >> 6] = hi; }
   __syncthreads();
-  if (tid != 0) return;
-  for (int w = 1; w < TR_THREADS / 64; w++) {
+  for (int w = 0; w < TR_THREADS / 64; w++) {
     lo = slo[w] < lo ? slo[w] : lo;
     hi = shi[w] > hi ? shi[w] : hi;
   }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restrict__ part, uint32_t nparts,
+                                                          uint64_t n, const DictCol* __restrict__ dcols,
+                                                          DictPlan* __restrict__ plans) {
+  __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
+  const int tid = threadIdx.x;
+  int64_t lo, hi, mlo = 0, mhi = -1;
+  reduce_parts(part + 2 * (uint64_t)blockIdx.x * nparts, nparts, lo, hi, slo, shi);
+  const uint32_t mvc = dcols[blockIdx.x].mv;
+  if (mvc != NO_DICT) reduce_parts(part + 2 * (uint64_t)mvc * nparts, nparts, mlo, mhi, slo, shi);
+  if (tid != 0) return;
   DictPlan P{};
   P.min = lo;
   P.K = -1;
@@ -775,6 +813,19 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restr
       sz = sz * sz;
     }
     for (int k = P.K + 1; k < DICT_LEVELS; k++) P.pw[k] = 0;
+    // head delta plan (see DictPlan): 4-row groups from (head, 3 moves)
+    const uint64_t dR = mhi >= mlo ? (uint64_t)mhi - (uint64_t)mlo + 1 : 0;
+    if (mvc != NO_DICT && P.K <= 1 && n >= 4 && dR && R * R <= DICT_CAP && dR <= 256 &&
+        R * dR * dR * dR <= DICT_CAP) {
+      P.K = 2;
+      P.delta = 1;
+      P.dmin = mlo;
+      P.dR = (uint32_t)dR;
+      P.pw[0] = (uint32_t)R;
+      P.pw[1] = (uint32_t)(R * R);
+      P.pw[2] = (uint32_t)(R * dR * dR * dR);
+      for (int k = 3; k < DICT_LEVELS; k++) P.pw[k] = 0;
+    }
   }
   plans[blockIdx.x] = P;
 }
@@ -795,6 +846,29 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __
   const DictCol dc = dcols[blockIdx.y];
   uint32_t* tl = tabs + 8 * (dc.tab + (uint64_t)lvl * DICT_CAP);
   const ColTemplate ct = tmpl[dc.col];
+  if (lvl == 2 && P.delta) {  // TD: (head code, 3 move codes) -> H(T_1, T_1)
+    const uint32_t* t1 = tl - 8 * (uint64_t)DICT_CAP;
+    const int64_t R = P.R, dR = P.dR;
+    for (uint32_t e = blockIdx.x * TR_THREADS + threadIdx.x; e < size; e += gridDim.x * TR_THREADS) {
+      int64_t c[4];
+      c[0] = e % R;
+      int64_t rest = e / R;
+      bool ok = true;
+#pragma unroll
+      for (int j = 1; j < 4; j++) {
+        c[j] = c[j - 1] + P.dmin + rest % dR;
+        rest /= dR;
+        ok = ok && c[j] >= 0 && c[j] < R;
+      }
+      if (!ok) continue;  // not a reachable group: never read
+      uint32_t a[8], b[8], h[8];
+      node_load(t1 + 8 * (uint64_t)(c[0] + R * c[1]), a);
+      node_load(t1 + 8 * (uint64_t)(c[2] + R * c[3]), b);
+      b3_parent(a, b, h);
+      node_store(tl + 8 * (uint64_t)e, h);
+    }
+    return;
+  }
   for (uint32_t e = blockIdx.x * TR_THREADS + threadIdx.x; e < size; e += gridDim.x * TR_THREADS) {
     uint32_t h[8];
     if (lvl == 0) {
@@ -854,7 +928,16 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
       case 0: case 3: dict_lane<int8_t>(dict_keys<int8_t>(T, ct) + lrow, P, tab, ctp, h); break;
       case 4: dict_lane<uint8_t>(dict_keys<uint8_t>(T, ct) + lrow, P, tab, ctp, h); break;
       case 5: dict_lane<uint16_t>(dict_keys<uint16_t>(T, ct) + lrow, P, tab, ctp, h); break;
-      default: dict_lane<int64_t>(dict_keys<int64_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      default:
+        if (P.delta) {
+          const uint64_t o = (uint64_t)ct.tape * T.n + lrow;
+          lane_tree<5>(DeltaNodes{T.head + o, T.mv + o, T.row_flags + lrow, tab + 8 * (uint64_t)DICT_CAP,
+                                  tab + 16 * (uint64_t)DICT_CAP, P.min, P.dmin, P.R, P.dR},
+                       h);
+        } else {
+          dict_lane<int64_t>(dict_keys<int64_t>(T, ct) + lrow, P, tab, ctp, h);
+        }
+        break;
     }
 #pragma unroll
     for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
@@ -925,7 +1008,7 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
                      row0, row0 + nrows);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_plans);
+  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_dcols, d_plans);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   for (int l = 0; l < DICT_LEVELS; l++) {
     // grid-stride: most (column, level) pairs are empty or tiny; 64 WGs per

@@ -140,6 +140,7 @@ CASES = [  # (T, b, tau, seed)
     (1, 1, 1, 6),           # n = 1 -> N = 8
     (512, 512, 0, 7),       # tau = 0: only the 3 scalar columns
     (1 << 13, 8192, 4, 8),  # one block spanning many column chunks
+    (1 << 14, 333, 4, 9),   # block starts inside 4-row head groups (delta-plan fallback)
 ]
 
 
