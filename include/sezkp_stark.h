@@ -102,6 +102,15 @@ int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], 
  * fri_paths, total, then host wall / sync-wait / final-wait / serialize.
  * Returns the number of values written. */
 int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max);
+/* Asynchronous proving: the context's worker thread runs the proof; wait
+ * returns the borrowed proof bytes (as sezkp_ctx_prove_borrow). One proof in
+ * flight per context; keep several contexts (one per trace, same device) in
+ * flight to overlap one proof's VALU-bound trees with another's memory- and
+ * latency-bound stages. Other calls on a context with a proof in flight fail
+ * with SEZKP_E_INVALID; destroy waits for it. */
+int32_t sezkp_ctx_prove_async(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, char* err,
+                              size_t err_len);
+int32_t sezkp_ctx_wait(sezkp_ctx* ctx, const uint8_t** data, size_t* len, char* err, size_t err_len);
 /* Device hipStream_t of the context (as void*), for external timing. */
 void* sezkp_ctx_stream(const sezkp_ctx* ctx);
 

@@ -14,10 +14,12 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sezkp_stark.h"
@@ -132,8 +134,26 @@ int ilog2(uint64_t x) {
 }  // namespace
 
 // ======================================================================== ctx
+// Per-context executor (sezkp_ctx_prove_async / sezkp_ctx_wait): one worker
+// thread runs the context's proofs, so a caller keeps several contexts in
+// flight on one GPU and the VALU-bound trees of one proof overlap the
+// memory- and latency-bound stages and host round trips of another.
+struct AsyncSlot {
+  enum State { IDLE, RUNNING, DONE };
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  State state = IDLE;
+  bool stop = false;
+  uint8_t root[32];
+  int32_t rc = 0;
+  std::string msg;
+  size_t len = 0;
+};
+
 struct sezkp_ctx {
   int device = 0;
+  std::unique_ptr<AsyncSlot> async;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // side stream: small FRI layers overlap the forest
   hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr;
@@ -233,7 +253,50 @@ struct sezkp_ctx {
     host_allocs.clear();
     loaded = false;
   }
+  bool busy() {
+    if (!async) return false;
+    std::lock_guard<std::mutex> lk(async->mu);
+    return async->state != AsyncSlot::IDLE;
+  }
+  void worker() {
+    AsyncSlot& a = *async;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(a.mu);
+      a.cv.wait(lk, [&] { return a.state == AsyncSlot::RUNNING || a.stop; });
+      if (a.state != AsyncSlot::RUNNING) return;  // stop requested while idle
+      uint8_t r[32];
+      memcpy(r, a.root, 32);
+      lk.unlock();
+      int32_t rc = SEZKP_OK;
+      std::string m;
+      size_t len = 0;
+      try {
+        len = prove(r);
+      } catch (const Err& e) {
+        rc = e.code;
+        m = e.msg;
+      } catch (const std::exception& e) {
+        rc = SEZKP_E_NOMEM;
+        m = e.what();
+      }
+      lk.lock();
+      a.rc = rc;
+      a.msg = std::move(m);
+      a.len = len;
+      a.state = AsyncSlot::DONE;
+      a.cv.notify_all();
+    }
+  }
   ~sezkp_ctx() {
+    if (async) {  // let a proof in flight finish, then stop the worker
+      {
+        std::unique_lock<std::mutex> lk(async->mu);
+        async->cv.wait(lk, [&] { return async->state != AsyncSlot::RUNNING; });
+        async->stop = true;
+      }
+      async->cv.notify_all();
+      if (async->th.joinable()) async->th.join();
+    }
     if (st) (void)hipStreamSynchronize(st);
     free_all();
     for (auto& e : ev)
@@ -996,6 +1059,7 @@ void sezkp_ctx_destroy(sezkp_ctx* ctx) { delete ctx; }
 int32_t sezkp_ctx_upload(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len) {
   try {
     if (!ctx || !blocks) throw Err{SEZKP_E_INVALID, "null argument"};
+    if (ctx->busy()) throw Err{SEZKP_E_INVALID, "a proof is in flight on this context (call sezkp_ctx_wait)"};
     ctx->upload(*blocks);
     return SEZKP_OK;
   } catch (const Err& e) {
@@ -1012,6 +1076,7 @@ int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_
   (void)flags;
   try {
     if (!ctx || !manifest_root || !proof_bytes) throw Err{SEZKP_E_INVALID, "null argument"};
+    if (ctx->busy()) throw Err{SEZKP_E_INVALID, "a proof is in flight on this context (call sezkp_ctx_wait)"};
     const size_t len = ctx->prove(manifest_root);
     proof_bytes->data = (uint8_t*)malloc(len ? len : 1);
     if (!proof_bytes->data) throw Err{SEZKP_E_NOMEM, "out of host memory"};
@@ -1032,6 +1097,7 @@ int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], 
   (void)flags;
   try {
     if (!ctx || !manifest_root || !data || !len) throw Err{SEZKP_E_INVALID, "null argument"};
+    if (ctx->busy()) throw Err{SEZKP_E_INVALID, "a proof is in flight on this context (call sezkp_ctx_wait)"};
     *len = ctx->prove(manifest_root);
     *data = ctx->h_proof;
     return SEZKP_OK;
@@ -1042,6 +1108,61 @@ int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], 
     set_err(err, err_len, e.what());
     return SEZKP_E_NOMEM;
   }
+}
+
+int32_t sezkp_ctx_prove_async(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, char* err,
+                              size_t err_len) {
+  (void)flags;
+  try {
+    if (!ctx || !manifest_root) throw Err{SEZKP_E_INVALID, "null argument"};
+    if (!ctx->loaded) throw Err{SEZKP_E_INVALID, "context has no trace: call sezkp_ctx_upload first"};
+    if (!ctx->async) {
+      ctx->async.reset(new AsyncSlot());
+      ctx->async->th = std::thread([ctx] { ctx->worker(); });
+    }
+    AsyncSlot& a = *ctx->async;
+    {
+      std::lock_guard<std::mutex> lk(a.mu);
+      if (a.state != AsyncSlot::IDLE)
+        throw Err{SEZKP_E_INVALID, "a proof is already in flight on this context (call sezkp_ctx_wait)"};
+      memcpy(a.root, manifest_root, 32);
+      a.state = AsyncSlot::RUNNING;
+    }
+    a.cv.notify_all();
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+    return SEZKP_E_NOMEM;
+  }
+}
+
+int32_t sezkp_ctx_wait(sezkp_ctx* ctx, const uint8_t** data, size_t* len, char* err, size_t err_len) {
+  if (!ctx || !data || !len) {
+    set_err(err, err_len, "null argument");
+    return SEZKP_E_INVALID;
+  }
+  if (!ctx->async) {
+    set_err(err, err_len, "no proof in flight on this context");
+    return SEZKP_E_INVALID;
+  }
+  AsyncSlot& a = *ctx->async;
+  std::unique_lock<std::mutex> lk(a.mu);
+  if (a.state == AsyncSlot::IDLE) {
+    set_err(err, err_len, "no proof in flight on this context");
+    return SEZKP_E_INVALID;
+  }
+  a.cv.wait(lk, [&] { return a.state == AsyncSlot::DONE; });
+  a.state = AsyncSlot::IDLE;
+  if (a.rc != SEZKP_OK) {
+    set_err(err, err_len, a.msg);
+    return a.rc;
+  }
+  *data = ctx->h_proof;
+  *len = a.len;
+  return SEZKP_OK;
 }
 
 int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max) {
@@ -1061,6 +1182,8 @@ int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, u
                            char* err, size_t err_len) {
   try {
     if (!ctx || !local || !scratch) throw Err{SEZKP_E_INVALID, "null argument"};
+    if (ctx->busy()) throw Err{SEZKP_E_INVALID, "a proof is in flight on this context (call sezkp_ctx_wait)"};
+
     if (dir != 1 && dir != -1) throw Err{SEZKP_E_INVALID, "dir must be +1 or -1"};
     const int P = ctx->world, logP = ctx->logP;
     if (log_n > 32 || (int)log_n < 8 + logP)

@@ -133,6 +133,19 @@ class ProverContext:
         check(lib.sezkp_ctx_prove_borrow(self._h, bytes(manifest_root), 0, C.byref(ptr), C.byref(n), err, 1024), err)
         return memoryview((C.c_uint8 * n.value).from_address(C.addressof(ptr.contents))).cast("B").toreadonly()
 
+    def prove_async(self, manifest_root: bytes) -> None:
+        """Start a proof on the context's worker thread (sezkp_ctx_prove_async)."""
+        err = C.create_string_buffer(1024)
+        check(lib.sezkp_ctx_prove_async(self._h, bytes(manifest_root), 0, err, 1024), err)
+
+    def wait_view(self) -> memoryview:
+        """Wait for the proof started by prove_async; a borrowed view as prove_view."""
+        ptr = C.POINTER(C.c_uint8)()
+        n = C.c_size_t()
+        err = C.create_string_buffer(1024)
+        check(lib.sezkp_ctx_wait(self._h, C.byref(ptr), C.byref(n), err, 1024), err)
+        return memoryview((C.c_uint8 * n.value).from_address(C.addressof(ptr.contents))).cast("B").toreadonly()
+
     def stage_times_ms(self) -> dict:
         buf = (C.c_double * 32)()
         n = lib.sezkp_ctx_stage_times(self._h, buf, 32)

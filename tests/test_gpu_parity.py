@@ -276,3 +276,37 @@ def test_cli_prove_verify_matches_oracle_artifact(gpu_ok, product, oracle, tmp_p
     r = subprocess.run([cli, "prove", "--backend", "stark", "--blocks", str(tmp_path / "b.jsonl"), "--manifest",
                         str(mpath), "--out", str(out)], capture_output=True, text=True)
     assert r.returncode != 0
+
+
+def test_async_proofs_in_flight_bit_exact(gpu_ok, product, oracle):
+    """sezkp_ctx_prove_async / sezkp_ctx_wait: three contexts (distinct
+    traces) in flight on one GPU, resubmitted round-robin; every proof equals
+    the oracle's, and misuse is refused without disturbing the context."""
+    traces = [product.synthetic_blocks(1 << 12, 512, 4, s) for s in (1, 2, 3)]
+    roots = [b.manifest_root() for b in traces]
+    want = [oracle.prove_v1(b, r) for b, r in zip(traces, roots)]
+    ctxs = []
+    for b in traces:
+        c = product.ProverContext(0)
+        c.upload(b)
+        ctxs.append(c)
+    for c, r in zip(ctxs, roots):
+        c.prove_async(r)
+    for rnd in range(3):
+        for i, c in enumerate(ctxs):
+            assert bytes(c.wait_view()) == want[i]
+            if rnd < 2:
+                c.prove_async(roots[i])
+    c = ctxs[0]
+    with pytest.raises(product.SezkpError, match="no proof in flight"):
+        c.wait_view()
+    c.prove_async(roots[0])
+    with pytest.raises(product.SezkpError, match="in flight"):
+        c.prove_async(roots[0])
+    with pytest.raises(product.SezkpError, match="in flight"):
+        c.prove(roots[0])
+    assert bytes(c.wait_view()) == want[0]
+    assert c.prove(roots[0]).proof_bytes == want[0]
+    ctxs[1].prove_async(roots[1])  # destroy with a proof in flight waits for it
+    for c in ctxs:
+        c.close()
