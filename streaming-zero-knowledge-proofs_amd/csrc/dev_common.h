@@ -19,30 +19,71 @@ constexpr uint64_t GL_P = 0xffffffff00000001ULL;
 constexpr uint64_t GL_EPS = 0xffffffffULL;  // 2^64 mod p
 
 // ------------------------------------------------------------------ Goldilocks
+// Carry-chain forms: 64-bit adds/subs as v_add_co/v_addc (v_sub_co/v_subb)
+// pairs whose carry feeds a select, instead of 64-bit compares + cndmask
+// (which also cost s_nop hazards on gfx950). tools/gl_variants.hip measures
+// them bit-identical to the compare forms and 1.2-1.6x faster.
+__device__ __forceinline__ uint64_t add64c(uint64_t a, uint64_t b, uint32_t& carry) {
+  uint32_t c0;
+  const uint32_t lo = __builtin_addc((uint32_t)a, (uint32_t)b, 0u, &c0);
+  const uint32_t hi = __builtin_addc((uint32_t)(a >> 32), (uint32_t)(b >> 32), c0, &carry);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t sub64b(uint64_t a, uint64_t b, uint32_t& borrow) {
+  uint32_t b0;
+  const uint32_t lo = __builtin_subc((uint32_t)a, (uint32_t)b, 0u, &b0);
+  const uint32_t hi = __builtin_subc((uint32_t)(a >> 32), (uint32_t)(b >> 32), b0, &borrow);
+  return ((uint64_t)hi << 32) | lo;
+}
+// canonical a, b: s = a + b; t = s + eps = s - p (mod 2^64); the true sum is
+// >= p exactly when either addition carried.
 __device__ __forceinline__ uint64_t gl_add(uint64_t a, uint64_t b) {
-  uint64_t s = a + b;
-  // carry out of 2^64 -> add eps; then one conditional subtract of p.
-  uint64_t c = (s < a) ? GL_EPS : 0;
-  s += c;
-  return (s >= GL_P) ? s - GL_P : s;
+  uint32_t c1, c2;
+  const uint64_t s = add64c(a, b, c1);
+  const uint64_t t = add64c(s, GL_EPS, c2);
+  return (c1 | c2) ? t : s;
 }
+// canonical a, b: a - b, and on borrow + p (= - eps mod 2^64)
 __device__ __forceinline__ uint64_t gl_sub(uint64_t a, uint64_t b) {
-  uint64_t d = a - b;
-  return (a < b) ? d + GL_P : d;
+  uint32_t br;
+  const uint64_t d = sub64b(a, b, br);
+  return br ? d - GL_EPS : d;
 }
-// x = hi*2^64 + lo  ->  x mod p   (2^64 = eps, 2^96 = -1)
+// any r < 2^64 -> r mod p (r - p iff r + eps carries)
+__device__ __forceinline__ uint64_t gl_canon(uint64_t r) {
+  uint32_t c;
+  const uint64_t t = add64c(r, GL_EPS, c);
+  return c ? t : r;
+}
+// x = hi*2^64 + lo -> r < 2^64 with r = x mod p (2^64 = eps, 2^96 = -1), not
+// necessarily canonical. Neither fix-up can wrap again: after a borrow t0 >=
+// 2^64 - 2^32 > eps, after a carry r < 2^64 - 2^33.
+__device__ __forceinline__ uint64_t gl_reduce128_weak(uint64_t lo, uint64_t hi) {
+  const uint32_t h0 = (uint32_t)hi, h1 = (uint32_t)(hi >> 32);
+  uint32_t br, c;
+  uint64_t t0 = sub64b(lo, h1, br);
+  if (br) t0 -= GL_EPS;
+  const uint64_t t1 = ((uint64_t)h0 << 32) - h0;
+  const uint64_t r = add64c(t0, t1, c);
+  return c ? r + GL_EPS : r;
+}
 __device__ __forceinline__ uint64_t gl_reduce128(uint64_t lo, uint64_t hi) {
-  uint64_t hi_hi = hi >> 32;
-  uint64_t hi_lo = hi & GL_EPS;
-  uint64_t t0 = lo - hi_hi;
-  if (lo < hi_hi) t0 -= GL_EPS;           // borrow: + p mod 2^64
-  uint64_t t1 = hi_lo * GL_EPS;           // < 2^64
-  uint64_t r = t0 + t1;
-  if (r < t1) r += GL_EPS;                // carry
-  return (r >= GL_P) ? r - GL_P : r;
+  return gl_canon(gl_reduce128_weak(lo, hi));
 }
+// 64x64 -> 128 with four v_mad_u64_u32 (the partial sums cannot overflow 64 bits)
+__device__ __forceinline__ void gl_mul128(uint64_t a, uint64_t b, uint64_t& lo, uint64_t& hi) {
+  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+  const uint64_t p00 = (uint64_t)a0 * b0;
+  const uint64_t t = (uint64_t)a0 * b1 + (p00 >> 32);
+  const uint64_t u = (uint64_t)a1 * b0 + (uint32_t)t;
+  hi = (uint64_t)a1 * b1 + ((t >> 32) + (u >> 32));
+  lo = ((uint64_t)(uint32_t)u << 32) | (uint32_t)p00;
+}
+// any a, b < 2^64 -> canonical a*b mod p
 __device__ __forceinline__ uint64_t gl_mul(uint64_t a, uint64_t b) {
-  return gl_reduce128(a * b, __umul64hi(a, b));
+  uint64_t lo, hi;
+  gl_mul128(a, b, lo, hi);
+  return gl_reduce128(lo, hi);
 }
 __device__ __forceinline__ uint64_t gl_sqr(uint64_t a) { return gl_mul(a, a); }
 __device__ __forceinline__ uint64_t gl_from_i64(int64_t x) {
