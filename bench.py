@@ -102,11 +102,13 @@ def cpu_baseline(T_sample: int, tau: int, T_mt: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-t", type=int, default=21, help="trace rows T = 2^log_t (N = 8T)")
     ap.add_argument("--tau", type=int, default=8)
     ap.add_argument("--b", type=int, default=512)
+    ap.add_argument("--stagger-ms", type=float, default=-1.0,
+                    help="start offset between the in-flight pipelines (-1 = one proof time / inflight)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="independent proofs in flight per GPU (one resident context each, sezkp_ctx_prove_async)")
     ap.add_argument("--cpu-sample-log-t", type=int, default=18)
@@ -163,22 +165,36 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    # timed: steps x K proofs, K in flight (each context's worker thread runs
-    # its proof; the host waits round-robin and resubmits)
+    # stagger: context i starts i/K of a proof later, so the K pipelines run
+    # different stages (VALU-bound trees beside memory/latency-bound NTT,
+    # openings, compose) instead of the same stage at the same time
+    t_s = time.perf_counter()
+    ctx.prove_async(mroot)
+    ctx.wait_view()
+    stagger = (args.stagger_ms * 1e-3 if args.stagger_ms >= 0 else (time.perf_counter() - t_s) / K)
+
+    # timed: steps x K proofs, K in flight: one host thread per context keeps
+    # its context busy (prove_async / wait, each proof on the context's own
+    # worker thread); the ctypes calls release the GIL
     total = args.steps * K
+    l0_conc = []
+
+    def pipeline(i):
+        if i and stagger > 0:
+            time.sleep(i * stagger)
+        for _ in range(args.steps):
+            ctxs[i].prove_async(roots[i])
+            ctxs[i].wait_view()
+            l0_conc.append(ctxs[i].stage_times_ms().get("layer0_tree", float("nan")))
+
+    import threading
     barrier()
     t0 = time.perf_counter()
-    for c, r in zip(ctxs, roots):
-        c.prove_async(r)
-    submitted, done, l0_conc = K, 0, []
-    while done < total:
-        i = done % K
-        ctxs[i].wait_view()
-        l0_conc.append(ctxs[i].stage_times_ms().get("layer0_tree", float("nan")))
-        done += 1
-        if submitted < total:
-            ctxs[i].prove_async(roots[i])
-            submitted += 1
+    workers = [threading.Thread(target=pipeline, args=(i,)) for i in range(K)]
+    for w in workers:
+        w.start()
+    for w in workers:
+        w.join()
     barrier()
     dt = time.perf_counter() - t0
     if dist:

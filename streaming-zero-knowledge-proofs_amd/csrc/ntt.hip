@@ -147,26 +147,44 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(NttPassArgs P) {
 //     step 2 (thread per q): F1-point DIF over r -> X[k_lo + F2*k_hi] lands at
 //     position q*F1 + q' (k_hi = rev_M1(q')).
 __device__ __forceinline__ uint64_t gl_neg(uint64_t x) { return x ? GL_P - x : 0; }
-__device__ __forceinline__ uint64_t gl_shl(uint64_t x, int e) {  // x * 2^e mod p, 0 < e < 64
-  return gl_reduce128(x << e, x >> (64 - e));
+// x * 2^e mod p for 0 <= e < 96 with e a compile-time constant after
+// unrolling, by 32-bit limb placement (2^64 = 2^32 - 1, 2^96 = -1) instead of
+// a 128-bit reduction. gl_add(A, B) is exact for any A < 2^64 when B < p.
+//   e < 32:  x 2^e = A + y2 2^64 = A + y2 eps,   A = x << e, y2 = x >> (64-e)
+//   e < 64:  x 2^e = A 2^32 + y2 2^96 = (A_lo << 32) + A_hi eps - y2, A = x << (e-32)
+//   e < 96:  x 2^e = (x 2^(e-64)) 2^64 = y 2^32 - y
+__device__ __forceinline__ uint64_t mul_eps32(uint32_t h) { return ((uint64_t)h << 32) - h; }  // h * eps < p
+__device__ __forceinline__ uint64_t gl_mul2e_lo(uint64_t x, int e) {  // 0 <= e < 32
+  if (e == 0) return x;
+  const uint64_t A = x << e;
+  const uint32_t y2 = (uint32_t)(x >> (64 - e));
+  return gl_add(A, mul_eps32(y2));
 }
-// x * 2^e mod p, 0 <= e < 192 (2^96 = -1); e is a compile-time constant after unrolling
-__device__ __forceinline__ uint64_t gl_mul_pow2(uint64_t x, int e) {
-  const bool neg = e >= 96;
-  if (neg) e -= 96;
-  uint64_t r = x;
-  if (e >= 64) {
-    r = gl_shl(r, e / 2);
-    e -= e / 2;
+__device__ __forceinline__ uint64_t gl_mul2e(uint64_t x, int e) {
+  if (e < 32) return gl_mul2e_lo(x, e);
+  if (e < 64) {
+    const int r = e - 32;
+    const uint64_t A = r ? x << r : x;
+    const uint32_t y2 = r ? (uint32_t)(x >> (64 - r)) : 0u;
+    const uint64_t t = gl_add(A << 32, mul_eps32((uint32_t)(A >> 32)));
+    return r ? gl_sub(t, y2) : t;
   }
-  if (e > 0) r = gl_shl(r, e);
-  return neg ? gl_neg(r) : r;
+  const uint64_t y = gl_mul2e_lo(x, e - 64);
+  return gl_sub(gl_add(y << 32, mul_eps32((uint32_t)(y >> 32))), y);
 }
+// x * 2^e mod p, 0 <= e < 192 (2^96 = -1)
+__device__ __forceinline__ uint64_t gl_mul_pow2(uint64_t x, int e) {
+  return e >= 96 ? gl_neg(gl_mul2e(x, e - 96)) : gl_mul2e(x, e);
+}
+// exponent of w_{2h}^j as a power of two: w_16 = 2^156 (w_16^-1 = 2^36)
+template <bool INV>
+__device__ __forceinline__ constexpr int tw_exp(int j, int h) { return ((INV ? 36 : 156) * j * (8 / h)) % 192; }
 // x * w_{2h}^j for 2h <= 16
 template <bool INV>
 __device__ __forceinline__ uint64_t tw_small(uint64_t x, int j, int h) {
-  return gl_mul_pow2(x, ((INV ? 36 : 156) * j * (8 / h)) % 192);
+  return gl_mul_pow2(x, tw_exp<INV>(j, h));
 }
+// Butterflies take the sign of w^j = -2^(e-96) into the add/sub instead of negating.
 template <int LOGF, bool INV, int SKIP>
 __device__ __forceinline__ void fft_dit_regs(uint64_t (&x)[1 << LOGF]) {
 #pragma unroll
@@ -176,10 +194,12 @@ __device__ __forceinline__ void fft_dit_regs(uint64_t (&x)[1 << LOGF]) {
     for (int t0 = 0; t0 < (1 << LOGF); t0++) {
       if (!(t0 & h)) {
         const int j = t0 & (h - 1);
-        const uint64_t y = j ? tw_small<INV>(x[t0 + h], j, h) : x[t0 + h];
+        const int e = j ? tw_exp<INV>(j, h) : 0;
+        const bool neg = e >= 96;
+        const uint64_t y = gl_mul2e(x[t0 + h], neg ? e - 96 : e);
         const uint64_t a = x[t0];
-        x[t0] = gl_add(a, y);
-        x[t0 + h] = gl_sub(a, y);
+        x[t0] = neg ? gl_sub(a, y) : gl_add(a, y);
+        x[t0 + h] = neg ? gl_add(a, y) : gl_sub(a, y);
       }
     }
   }
@@ -193,10 +213,11 @@ __device__ __forceinline__ void fft_dif_regs(uint64_t (&x)[1 << LOGF]) {
     for (int t0 = 0; t0 < (1 << LOGF); t0++) {
       if (!(t0 & h)) {
         const int j = t0 & (h - 1);
+        const int e = j ? tw_exp<INV>(j, h) : 0;
+        const bool neg = e >= 96;
         const uint64_t a = x[t0], b = x[t0 + h];
         x[t0] = gl_add(a, b);
-        const uint64_t d = gl_sub(a, b);
-        x[t0 + h] = j ? tw_small<INV>(d, j, h) : d;
+        x[t0 + h] = gl_mul2e(neg ? gl_sub(b, a) : gl_sub(a, b), neg ? e - 96 : e);
       }
     }
   }
@@ -224,7 +245,59 @@ __device__ __forceinline__ uint64_t tile_pos(const Tile& G, int t, int c, uint64
   return G.tile * ((uint64_t)NTT_CMAX << G.m) + (cb << (G.sL + G.m)) + ((uint64_t)t << G.sL) + low;
 }
 
-template <bool DIF, bool INV, int M1, int M2, int SKIP>
+// Fused DEEP (last forward DIT pass of the LDE only): out_i = y_i / (x_i - z),
+// x_i = 3 w_N^(g + P i) (merkle.hip k_deep, lde.rs:76-93). A thread's F2
+// outputs sit F1 << sL apart, so consecutive x differ by w_F2 (a power of
+// two: a shift); one Montgomery batch inversion per workgroup (4096 points).
+template <int F>
+__device__ __forceinline__ void deep_tile(uint64_t (&y)[F], uint64_t x, uint64_t z) {
+  __shared__ uint64_t wtot[NTT_THREADS / 64];
+  __shared__ uint64_t s_inv;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint64_t d[F], a[F];
+  uint64_t Pp = 1;
+#pragma unroll
+  for (int j = 0; j < F; j++) {
+    d[j] = gl_sub(x, z);
+    Pp = j ? gl_mul(Pp, d[j]) : d[j];
+    a[j] = Pp;
+    x = tw_small<false>(x, 1, F / 2);  // * w_F
+  }
+  uint64_t S = Pp, Tq = Pp;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t u = __shfl_up(S, o, 64);
+    if (lane >= o) S = gl_mul(S, u);
+    const uint64_t v = __shfl_down(Tq, o, 64);
+    if (lane + o < 64) Tq = gl_mul(Tq, v);
+  }
+  uint64_t Q = __shfl_down(Tq, 1, 64);
+  if (lane == 63) Q = 1;
+  uint64_t Sprev = __shfl_up(S, 1, 64);
+  if (lane == 0) Sprev = 1;
+  if (lane == 63) wtot[wave] = S;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t t = wtot[0];
+#pragma unroll
+    for (int w = 1; w < NTT_THREADS / 64; w++) t = gl_mul(t, wtot[w]);
+    s_inv = gl_inv(t);
+  }
+  __syncthreads();
+  uint64_t invW = s_inv;
+#pragma unroll
+  for (int w = 0; w < NTT_THREADS / 64; w++)
+    if (w != wave) invW = gl_mul(invW, wtot[w]);
+  uint64_t inv_run = gl_mul(gl_mul(invW, Q), Sprev);  // 1 / (this thread's product)
+#pragma unroll
+  for (int j = F - 1; j >= 0; j--) {
+    const uint64_t inv_dj = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
+    if (j) inv_run = gl_mul(inv_run, d[j]);
+    y[j] = gl_mul(y[j], inv_dj);
+  }
+}
+
+template <bool DIF, bool INV, int M1, int M2, int SKIP, bool DEEP = false>
 __global__ void __launch_bounds__(NTT_THREADS) k_ntt4(NttPassArgs P) {
   constexpr int F1 = 1 << M1, F2 = 1 << M2, m = M1 + M2, R = 1 << m;
   __shared__ uint64_t sh[R * NTT_PADC];
@@ -296,6 +369,13 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt4(NttPassArgs P) {
       for (int u = 0; u < F2; u++) y[u] = sh[(u * F1 + k2) * NTT_PADC + c];
       fft_dit_regs<M2, INV, 0>(y);
       uint64_t low;
+      if constexpr (DEEP) {
+        static_assert(F1 * NTT_CMAX == NTT_THREADS && !INV && !DIF, "fused DEEP needs every thread in step 2");
+        const uint64_t pos0 = tile_pos(G, k2, c, low);
+        const uint64_t e = ((uint64_t)P.deep_g + (pos0 << P.deep_logP)) << (T.K - P.deep_logN);
+        const uint64_t x0 = gl_mul(gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]), 3);
+        deep_tile<F2>(y, x0, P.deep_z);
+      }
 #pragma unroll
       for (int k1 = 0; k1 < F2; k1++) P.a[tile_pos(G, k2 + F1 * k1, c, low)] = y[k1];
     }
@@ -497,8 +577,14 @@ hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
 // DIT from bit-reversed input. If src != nullptr, the first pass loads the
 // replicated, scaled coefficients (LDE) and skips the 3 stages replication
 // makes trivial (blowup 8).
+static bool deep_fused_disabled() {  // SEZKP_NO_DEEP_FUSE=1: separate k_deep (A/B comparison)
+  static const bool off = getenv("SEZKP_NO_DEEP_FUSE") != nullptr;
+  return off;
+}
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
-                   const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e) {
+                   const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e, const DeepFuse* deep,
+                   bool* fused) {
+  if (fused) *fused = false;
   if (logN == 0) return hipSuccess;
   int ms[8], np;
   plan_passes(logN, src ? 3 : 1, ms, &np);
@@ -513,6 +599,18 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     P.skip = (i == 0 && src) ? (logN - log_src) : 0;
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
     uint64_t tiles = (1ULL << logN) >> (P.m + logC);
+    // last pass, forward, 16 wide columns, M1 = 4 (m = 7 or 8), not the replicated first pass
+    if (deep && fused && i == np - 1 && i > 0 && !inverse && !ntt4_disabled() && !deep_fused_disabled() &&
+        logC == 4 && P.sL >= 4 && (P.m == 8 || P.m == 7)) {
+      P.deep_z = deep->z; P.deep_logN = deep->logN; P.deep_logP = deep->logP; P.deep_g = deep->g;
+      if (P.m == 8)
+        hipLaunchKernelGGL((k_ntt4<false, false, 4, 4, 0, true>), dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
+      else
+        hipLaunchKernelGGL((k_ntt4<false, false, 4, 3, 0, true>), dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
+      *fused = true;
+      sL += ms[i];
+      continue;
+    }
     const bool fast = !ntt4_disabled() &&
                       (inverse ? launch_ntt4<false, true>(st, P, (unsigned)tiles)
                                : launch_ntt4<false, false>(st, P, (unsigned)tiles));

@@ -746,9 +746,11 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   const uint64_t inv_n = hgl_inv(n % GL_P_HOST);
   uint64_t* lde_out = sharded ? d_cyc : d_lde;
   const uint64_t coset_e = sharded ? ((uint64_t)rank << (tw.K - logN)) : 0;
-  ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e), "lde_ntt");
+  const DeepFuse dfuse{z, logN, logP, (uint32_t)rank};
+  bool deep_fused = false;
+  ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused), "lde_ntt");
   rec(6);
-  ok(launch_deep(st, lde_out, logN, z, tw, logP, (uint32_t)rank), "deep");
+  if (!deep_fused) ok(launch_deep(st, lde_out, logN, z, tw, logP, (uint32_t)rank), "deep");
   if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI
     ok(launch_cyc_pack(st, d_cyc, d_xbuf, M, logP), "cyc_pack");
     comm->alltoall(d_xbuf, d_cyc, (size_t)(M >> logP) * 8, st);
@@ -1294,8 +1296,11 @@ int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_bl
     const int logN = (int)(log_n + log_blowup);
     if (ntt_dif(st, evals, (int)log_n, true, T) != hipSuccess) return SEZKP_E_DEVICE;
     const uint64_t inv_n = hgl_inv((1ULL << log_n) % GL_P_HOST);
-    if (ntt_dit(st, out, logN, false, T, evals, (int)log_n, inv_n) != hipSuccess) return SEZKP_E_DEVICE;
-    if (launch_deep(st, out, logN, z, T) != hipSuccess) return SEZKP_E_DEVICE;
+    const DeepFuse dfuse{z, logN, 0, 0};
+    bool deep_fused = false;
+    if (ntt_dit(st, out, logN, false, T, evals, (int)log_n, inv_n, 0, &dfuse, &deep_fused) != hipSuccess)
+      return SEZKP_E_DEVICE;
+    if (!deep_fused && launch_deep(st, out, logN, z, T) != hipSuccess) return SEZKP_E_DEVICE;
     return SEZKP_OK;
   } catch (const Err& e) {
     return e.code;

@@ -26,11 +26,24 @@ struct NttPassArgs {
   uint64_t inv_n;
   uint64_t coset_e;  // LDE load: extra factor w_{2^K}^(coset_e * bitrev(k)) (sharded coset), 0 = none
   int m, sL, logC, inverse, skip, log_src;
+  // fused DEEP on the last forward pass (k_ntt4<..., DEEP = true>)
+  uint64_t deep_z;
+  int deep_logN, deep_logP;
+  uint32_t deep_g;
+};
+// DEEP division y_i / (3 w_N^(g + P i) - z) fused into the LDE's last pass
+struct DeepFuse {
+  uint64_t z;
+  int logN, logP;
+  uint32_t g;
 };
 
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
+// deep != nullptr: fuse the DEEP division into the last pass when its shape
+// allows; *fused says whether it did (else the caller runs launch_deep).
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
-                   const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e = 0);
+                   const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e = 0,
+                   const DeepFuse* deep = nullptr, bool* fused = nullptr);
 hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale,
                           bool do_scale);
 // distributed four-step NTT pieces (ntt.hip)

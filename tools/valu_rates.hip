@@ -84,6 +84,35 @@ DEF_KERNEL(k_pkadd16, OP_PKADD16)
 DEF_KERNEL(k_addco, OP_ADDCO)
 DEF_KERNEL(k_cnd, OP_CND)
 
+// instruction mixes (per chain, per unrolled step): BLAKE3's G is
+// 2 add3 + 2 add + 4 xor + 4 alignbit
+#define MIX_XA(x) CH8(OP_XOR) CH8(OP_ALIGN)
+#define MIX_XXA(x) CH8(OP_XOR) CH8(OP_XOR) CH8(OP_ALIGN)
+#define MIX_G(x) CH8(OP_ADD3) CH8(OP_XOR) CH8(OP_ALIGN) CH8(OP_ADD) CH8(OP_XOR) CH8(OP_ALIGN)
+#define MIX_G2(x) CH8(OP_ADD) CH8(OP_ADD) CH8(OP_XOR) CH8(OP_ALIGN) CH8(OP_ADD) CH8(OP_XOR) CH8(OP_ALIGN)
+#define MIX_XADD(x) CH8(OP_XOR) CH8(OP_ADD)
+#define MIX_AA(x) CH8(OP_ALIGN) CH8(OP_ADD3)
+#define ONCE(OP) OP(a0)
+#define DEF_MIX(NAME, BODY)                                                            \
+  __global__ void __launch_bounds__(256) NAME(uint32_t* out, uint64_t* cyc, int iters) { \
+    uint32_t a0 = threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 * 11,     \
+             a5 = a0 * 13, a6 = a0 * 17, a7 = a0 * 19;                                  \
+    uint32_t b = blockIdx.x | 1, c = blockIdx.x * 7 + 1;                                \
+    uint64_t t0 = __builtin_amdgcn_s_memtime();                                        \
+    for (int i = 0; i < iters; i++) {                                                   \
+      _Pragma("unroll") for (int k = 0; k < 8; k++) { BODY(0) }                        \
+    }                                                                                   \
+    uint64_t t1 = __builtin_amdgcn_s_memtime();                                        \
+    out[blockIdx.x * 256 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;        \
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;                                   \
+  }
+DEF_MIX(k_mix_xa, MIX_XA)
+DEF_MIX(k_mix_xxa, MIX_XXA)
+DEF_MIX(k_mix_g, MIX_G)
+DEF_MIX(k_mix_g2, MIX_G2)
+DEF_MIX(k_mix_xadd, MIX_XADD)
+DEF_MIX(k_mix_aa, MIX_AA)
+
 // 64-bit: mad_u64_u32 chains
 __global__ void __launch_bounds__(256) k_mad64(uint32_t* out, uint64_t* cyc, int iters) {
   uint64_t a[8];
@@ -150,6 +179,8 @@ int main() {
       {"v_alignbyte_b32", k_alignbyte}, {"v_cndmask_e64", k_cnde64}, {"v_addc_co_u32", k_addc},
       {"v_mad_u32_u24", k_madu24}, {"v_mul_u32_u24", k_mulu24}, {"v_bfi_b32", k_bfi}, {"v_sub_co_u32", k_subco},
       {"v_max_u32", k_max},
+      {"mix xor+align (/2)", k_mix_xa}, {"mix 2xor+align (/3)", k_mix_xxa}, {"mix G-half add3 (/6)", k_mix_g},
+      {"mix G-half 2add (/7)", k_mix_g2}, {"mix xor+add (/2)", k_mix_xadd}, {"mix align+add3 (/2)", k_mix_aa},
       {"v_lshl_add_u64", k_lshladd64}, {"v_lshrrev_b64", k_lshr64}, {"v_mov_b64", k_mov64},
       {"v_pk_mov_b32", k_pkmov}, {"v_pk_add_f32", k_pkaddf32},
   };
