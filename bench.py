@@ -178,16 +178,25 @@ def main():
     # worker thread); the ctypes calls release the GIL
     total = args.steps * K
     l0_conc = []
+    import threading
+    lock = threading.Lock()
+    left = [total]  # shared work queue: a context takes the next proof when it is free
+
+    def take():
+        with lock:
+            if left[0] == 0:
+                return False
+            left[0] -= 1
+            return True
 
     def pipeline(i):
         if i and stagger > 0:
             time.sleep(i * stagger)
-        for _ in range(args.steps):
+        while take():
             ctxs[i].prove_async(roots[i])
             ctxs[i].wait_view()
             l0_conc.append(ctxs[i].stage_times_ms().get("layer0_tree", float("nan")))
 
-    import threading
     barrier()
     t0 = time.perf_counter()
     workers = [threading.Thread(target=pipeline, args=(i,)) for i in range(K)]

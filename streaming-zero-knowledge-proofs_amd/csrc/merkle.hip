@@ -45,9 +45,10 @@ __device__ __forceinline__ void lds_pair(uint32_t (*lds)[W], int i, uint32_t (&l
 // Reduce `cnt` level-`lvl` nodes in LDS to one; WG-local node i at level l has
 // global index wg * (cnt_at_l) + i.
 template <int W>
-__device__ __forceinline__ void wg_reduce(uint32_t (*lds)[W], int cnt, int lvl, uint64_t wg, const TreeDev& T) {
+__device__ __forceinline__ void wg_reduce(uint32_t (*lds)[W], int cnt, int lvl, uint64_t wg, const TreeDev& T,
+                                          int stop = 64) {
   const int tid = threadIdx.x;
-  while (cnt > 1) {
+  while (cnt > 1 && lvl < stop) {
     const int half = cnt >> 1;
     uint32_t h[8];
     const bool act = tid < half;
@@ -290,7 +291,7 @@ __device__ __forceinline__ void subtree_regs(const uint64_t (&v)[16], uint64_t i
 // Levels above 12 are left to the upper-level jobs.
 __device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int logLen,
                                            int fold, uint64_t beta, const TreeDev& T, uint64_t wg,
-                                           uint32_t (*lds)[MK_THREADS]) {
+                                           uint32_t (*lds)[MK_THREADS], int stop) {
   const int tid = threadIdx.x;
   const uint64_t len = 1ULL << logLen;
   const uint64_t i0 = (wg << L16_LOG) + ((uint64_t)tid << 4);
@@ -319,13 +320,13 @@ __device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint
   subtree_regs<4, 0>(v, i0, T, h);
   lds_put(lds, tid, h);
   __syncthreads();
-  wg_reduce(lds, MK_THREADS, 4, wg, T);
+  wg_reduce(lds, MK_THREADS, 4, wg, T, stop);
 }
 
 __global__ void __launch_bounds__(MK_THREADS) k_layer16(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
-                                                        int logLen, int fold, uint64_t beta, TreeDev T) {
+                                                        int logLen, int fold, uint64_t beta, TreeDev T, int stop) {
   __shared__ uint32_t lds[8][MK_THREADS];
-  layer16_wg(in, out, logLen, fold, beta, T, blockIdx.x, lds);
+  layer16_wg(in, out, logLen, fold, beta, T, blockIdx.x, lds, stop);
 }
 
 // All fold layers of >= 4096 leaves hashed in one launch (their values were
@@ -336,7 +337,7 @@ __global__ void __launch_bounds__(MK_THREADS) k_forest16(const ForestLayer* __re
   int l = 0;
   while (l + 1 < nlayers && layers[l + 1].wg_start <= blockIdx.x) l++;
   const ForestLayer F = layers[l];
-  layer16_wg(F.vals, nullptr, F.tree.logLen, 0, 0, F.tree, blockIdx.x - F.wg_start, lds);
+  layer16_wg(F.vals, nullptr, F.tree.logLen, 0, 0, F.tree, blockIdx.x - F.wg_start, lds, (int)F.stop);
 }
 
 // FRI fold y'_i = y_i + beta * y_{i+len} (prover.rs:200-239), 4 per lane.
@@ -591,10 +592,10 @@ hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out
 }
 
 hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
-                          TreeDev tree) {
-  if (logLen < L16_LOG) return hipErrorInvalidValue;
+                          TreeDev tree, int stop) {
+  if (logLen < L16_LOG || stop < tree.lstore || stop > L16_LOG) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_layer16, dim3((unsigned)(1ULL << (logLen - L16_LOG))), dim3(MK_THREADS), 0, st, in, out_vals,
-                     logLen, fold, beta, tree);
+                     logLen, fold, beta, tree, stop);
   return hipGetLastError();
 }
 

@@ -249,8 +249,8 @@ __device__ __forceinline__ uint64_t tile_pos(const Tile& G, int t, int c, uint64
 // x_i = 3 w_N^(g + P i) (merkle.hip k_deep, lde.rs:76-93). A thread's F2
 // outputs sit F1 << sL apart, so consecutive x differ by w_F2 (a power of
 // two: a shift); one Montgomery batch inversion per workgroup (4096 points).
-template <int F>
-__device__ __forceinline__ void deep_tile(uint64_t (&y)[F], uint64_t x, uint64_t z) {
+template <int F, class Emit>
+__device__ __forceinline__ void deep_tile(uint64_t x, uint64_t z, Emit emit) {
   __shared__ uint64_t wtot[NTT_THREADS / 64];
   __shared__ uint64_t s_inv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -261,7 +261,7 @@ __device__ __forceinline__ void deep_tile(uint64_t (&y)[F], uint64_t x, uint64_t
     d[j] = gl_sub(x, z);
     Pp = j ? gl_mul(Pp, d[j]) : d[j];
     a[j] = Pp;
-    x = tw_small<false>(x, 1, F / 2);  // * w_F
+    if (j + 1 < F) x = tw_small<false>(x, 1, F / 2);  // * w_F
   }
   uint64_t S = Pp, Tq = Pp;
 #pragma unroll
@@ -291,14 +291,13 @@ __device__ __forceinline__ void deep_tile(uint64_t (&y)[F], uint64_t x, uint64_t
   uint64_t inv_run = gl_mul(gl_mul(invW, Q), Sprev);  // 1 / (this thread's product)
 #pragma unroll
   for (int j = F - 1; j >= 0; j--) {
-    const uint64_t inv_dj = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
+    emit(j, j ? gl_mul(inv_run, a[j - 1]) : inv_run);  // 1 / d_j
     if (j) inv_run = gl_mul(inv_run, d[j]);
-    y[j] = gl_mul(y[j], inv_dj);
   }
 }
 
 template <bool DIF, bool INV, int M1, int M2, int SKIP, bool DEEP = false>
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt4(NttPassArgs P) {
+__global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   constexpr int F1 = 1 << M1, F2 = 1 << M2, m = M1 + M2, R = 1 << m;
   __shared__ uint64_t sh[R * NTT_PADC];
   __shared__ uint64_t W[R];
@@ -371,13 +370,19 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt4(NttPassArgs P) {
       uint64_t low;
       if constexpr (DEEP) {
         static_assert(F1 * NTT_CMAX == NTT_THREADS && !INV && !DIF, "fused DEEP needs every thread in step 2");
+        // park y in this thread's own LDS slots (read above) to free registers
+#pragma unroll
+        for (int k1 = 0; k1 < F2; k1++) sh[(k1 * F1 + k2) * NTT_PADC + c] = y[k1];
         const uint64_t pos0 = tile_pos(G, k2, c, low);
         const uint64_t e = ((uint64_t)P.deep_g + (pos0 << P.deep_logP)) << (T.K - P.deep_logN);
         const uint64_t x0 = gl_mul(gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]), 3);
-        deep_tile<F2>(y, x0, P.deep_z);
-      }
+        deep_tile<F2>(x0, P.deep_z, [&](int k1, uint64_t inv) {
+          P.a[tile_pos(G, k2 + F1 * k1, c, low)] = gl_mul(sh[(k1 * F1 + k2) * NTT_PADC + c], inv);
+        });
+      } else {
 #pragma unroll
-      for (int k1 = 0; k1 < F2; k1++) P.a[tile_pos(G, k2 + F1 * k1, c, low)] = y[k1];
+        for (int k1 = 0; k1 < F2; k1++) P.a[tile_pos(G, k2 + F1 * k1, c, low)] = y[k1];
+      }
     }
   } else {
     if (g < F1) {  // step 1: thread (c, r), registers u (natural)

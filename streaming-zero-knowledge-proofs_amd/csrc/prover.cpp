@@ -198,6 +198,9 @@ struct sezkp_ctx {
   int rank = 0, world = 1, logP = 0;
   std::unique_ptr<Comm> comm;            // non-null: the sharded algorithm (also at P = 1, see ctx_create)
   bool sharded() const { return comm != nullptr; }
+  // level the run-layer WGs reduce to: the run root (12) when run roots are
+  // allgathered, else 6 so the upper jobs build levels 7.. with every lane busy
+  int tree_stop() const { return sharded() ? L16_LOG : LSTORE_FRI; }
   uint64_t M = 0;                       // local LDE length N / P
   int logM = 0;
   int rR = -1;                          // run layers 0..rR (len >= 4096 P), the rest replicated
@@ -582,7 +585,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     std::vector<ForestLayer> fl;
     uint32_t wgs = 0;
     for (int r = 1; r <= rR; r++) {
-      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, 0});
+      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)tree_stop()});
       wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
     }
     n_forest = (int)fl.size();
@@ -593,10 +596,15 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   // upper levels (> 12): layer 0's cap, then every other cap / replicated tree
   {
     std::vector<std::vector<UpperJob>> p0, pF;
-    if (rR >= 0 && caps[0].logLen > L16_LOG) plan_upper_jobs(caps[0], L16_LOG, p0);
-    for (int r = 1; r <= k; r++)
-      if ((r <= rR || std::find(rep16.begin(), rep16.end(), r) != rep16.end()) && caps[r].logLen > L16_LOG)
-        plan_upper_jobs(caps[r], L16_LOG, pF);
+    // run layers start from the level their layer16 WGs stopped at
+    const int from = tree_stop();
+    if (rR >= 0 && caps[0].logLen > from) plan_upper_jobs(caps[0], from, p0);
+    for (int r = 1; r <= k; r++) {
+      const bool runl = r <= rR;
+      if ((runl || std::find(rep16.begin(), rep16.end(), r) != rep16.end()) &&
+          caps[r].logLen > (runl ? from : L16_LOG))
+        plan_upper_jobs(caps[r], runl ? from : L16_LOG, pF);
+    }
     std::vector<UpperJob> all;
     jobs0.clear();
     jobsF.clear();
@@ -759,7 +767,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   rec(7);
   // ---- layer-0 tree: local runs, then the cap from allgathered run roots
   if (rR >= 0) {
-    ok(launch_layer16(st, d_lde, nullptr, ltrees[0].logLen, 0, 0, ltrees[0]), "layer0_tree");
+    ok(launch_layer16(st, d_lde, nullptr, ltrees[0].logLen, 0, 0, ltrees[0], tree_stop()), "layer0_tree");
     rec(ST_L0TREE + 1);
     if (sharded) {
       const uint64_t nrun = M >> L16_LOG;

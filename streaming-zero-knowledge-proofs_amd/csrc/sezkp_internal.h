@@ -224,8 +224,10 @@ void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJo
 hipError_t launch_upper_jobs(hipStream_t st, const UpperJob* d_jobs, int njobs);
 
 constexpr int L16_LOG = 12;  // leaves per WG of the 16-leaves-per-lane layer kernel
+// stop: highest level the WG reduces to (L16_LOG = its run root; LSTORE_FRI
+// leaves levels 7..12 to the upper jobs, whose lanes are all busy)
 hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
-                          TreeDev tree);
+                          TreeDev tree, int stop = L16_LOG);
 // Fold chain kernel (values only) and the one-launch forest of layer trees.
 hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta);
 // two consecutive folds in one pass; logLen2 = log2 of the second output
@@ -235,7 +237,7 @@ struct ForestLayer {
   const uint64_t* vals;
   TreeDev tree;
   uint32_t wg_start;  // first WG of this layer in the forest launch
-  uint32_t pad;
+  uint32_t stop;      // level the WG reduces to (see launch_layer16)
 };
 hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs);
 // Small FRI layers (logLen <= Ls <= 11) in one launch; layer Ls - j is
