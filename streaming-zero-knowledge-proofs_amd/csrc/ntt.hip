@@ -17,6 +17,8 @@
 // L2-resident), inverse uses e -> 2^K - e.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "dev_common.h"
 #include "sezkp_internal.h"
 
@@ -34,6 +36,19 @@ __device__ __forceinline__ uint64_t tw_pow(const NttTables& T, uint64_t e, bool 
 }
 __device__ __forceinline__ uint64_t pow3(const NttTables& T, uint64_t e) {
   return gl_mul(T.p3_hi[e >> T.S], T.p3_lo[e & ((1ULL << T.S) - 1)]);
+}
+
+// DEEP-quotient coefficient at bit-reversed position p of the N-point DIT
+// input: e = bitrev(p); the q part only where p's low b = log(N/n) bits are 0
+__device__ __forceinline__ uint64_t dp_load(const NttPassArgs& P, const NttTables& T, uint64_t p, int b) {
+  const uint64_t e = (uint64_t)(__brev((uint32_t)p) >> (32 - P.dp_logN));
+  uint64_t v = gl_mul(P.dp_rhi[e >> 12], P.dp_rlo[e & 4095]);
+  if ((p & ((1ULL << b) - 1)) == 0) {
+    const uint64_t k = p >> b;
+    const uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;  // = e
+    v = gl_add(v, gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk)));
+  }
+  return v;
 }
 
 template <bool DIF>
@@ -72,7 +87,9 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(NttPassArgs P) {
       pos = tile * (uint64_t)nel + q;
     }
     uint64_t v;
-    if (P.src) {  // LDE replicated load: B[2^skip k + s] = A[k] * n^-1 * (3 w^g)^bitrev(k)
+    if (P.dp_rlo) {
+      v = dp_load(P, T, pos, P.dp_logN - P.log_src);
+    } else if (P.src) {  // LDE replicated load: B[2^skip k + s] = A[k] * n^-1 * (3 w^g)^bitrev(k)
       uint64_t k = pos >> P.skip;
       uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;
       v = gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk));
@@ -324,7 +341,12 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
       const int u = g;
       uint64_t x[F1];
       uint64_t low = 0;
-      if (P.src) {  // LDE replicated load (first pass, sL = 0, low = 0)
+      if (P.dp_rlo) {  // DEEP-quotient LDE load (first pass, sL = 0, low = 0, SKIP = 0)
+        const uint64_t p0 = tile_pos(G, F1 * u, c, low);
+        const int b = P.dp_logN - P.log_src;
+#pragma unroll
+        for (int r = 0; r < F1; r++) x[r] = dp_load(P, T, p0 + r, b);
+      } else if (P.src) {  // LDE replicated load (first pass, sL = 0, low = 0)
         const uint64_t p0 = tile_pos(G, F1 * u, c, low);
 #pragma unroll
         for (int r = 0; r < F1; r += (1 << SKIP)) {
@@ -545,6 +567,137 @@ __global__ void __launch_bounds__(256) k_dntt_dft(uint64_t* __restrict__ r, uint
   for (int k1 = 0; k1 < P; k1++) r[k1 * Q + q] = o[k1];
 }
 
+// ------------------------------------------- DEEP quotient (base domain)
+// See DeepPoly (sezkp_internal.h). k_inv_base: inv_j = 1 / (w_n^j - z) for
+// the n base points (16 per lane, one Montgomery batch per 4096) and the
+// per-WG partial sums of C_j w_n^j inv_j.
+constexpr int DQ_PER = 4;
+__global__ void __launch_bounds__(NTT_THREADS) k_inv_base(const uint64_t* __restrict__ C, uint64_t* __restrict__ inv,
+                                                          uint64_t* __restrict__ partial, int logn, uint64_t z,
+                                                          NttTables T) {
+  __shared__ uint64_t wtot[NTT_THREADS / 64];
+  __shared__ uint64_t s_inv;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t n = 1ULL << logn;
+  const uint64_t i0 = ((uint64_t)blockIdx.x * NTT_THREADS + tid) * DQ_PER;
+  const bool act = i0 < n;  // n >= 16 > DQ_PER: a lane's points are all in or all out
+  uint64_t d[DQ_PER], a[DQ_PER];
+  uint64_t Pp = 1;
+  if (act) {
+    const uint64_t e = i0 << (T.K - logn);
+    uint64_t x = gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]);
+    const uint64_t e1 = 1ULL << (T.K - logn);
+    const uint64_t wn = gl_mul(T.hi[e1 >> T.S], T.lo[e1 & ((1ULL << T.S) - 1)]);
+#pragma unroll
+    for (int j = 0; j < DQ_PER; j++) {
+      d[j] = gl_sub(x, z);
+      Pp = j ? gl_mul(Pp, d[j]) : d[j];
+      a[j] = Pp;
+      x = gl_mul(x, wn);
+    }
+  }
+  uint64_t S = Pp, Tq = Pp;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t u = __shfl_up(S, o, 64);
+    if (lane >= o) S = gl_mul(S, u);
+    const uint64_t v = __shfl_down(Tq, o, 64);
+    if (lane + o < 64) Tq = gl_mul(Tq, v);
+  }
+  uint64_t Q = __shfl_down(Tq, 1, 64);
+  if (lane == 63) Q = 1;
+  uint64_t Sprev = __shfl_up(S, 1, 64);
+  if (lane == 0) Sprev = 1;
+  if (lane == 63) wtot[wave] = S;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t t = wtot[0];
+#pragma unroll
+    for (int w = 1; w < NTT_THREADS / 64; w++) t = gl_mul(t, wtot[w]);
+    s_inv = gl_inv(t);
+  }
+  __syncthreads();
+  uint64_t invW = s_inv;
+#pragma unroll
+  for (int w = 0; w < NTT_THREADS / 64; w++)
+    if (w != wave) invW = gl_mul(invW, wtot[w]);
+  uint64_t inv_run = gl_mul(gl_mul(invW, Q), Sprev);
+  uint64_t acc = 0;
+  if (act) {
+#pragma unroll
+    for (int j = DQ_PER - 1; j >= 0; j--) {
+      const uint64_t ij = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
+      if (j) inv_run = gl_mul(inv_run, d[j]);
+      inv[i0 + j] = ij;
+      const uint64_t xj = gl_add(d[j], z);  // w_n^(i0 + j)
+      acc = gl_add(acc, gl_mul(gl_mul(C[i0 + j], xj), ij));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc = gl_add(acc, __shfl_xor(acc, o, 64));
+  __syncthreads();
+  if (lane == 0) wtot[wave] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t t = wtot[0];
+#pragma unroll
+    for (int w = 1; w < NTT_THREADS / 64; w++) t = gl_add(t, wtot[w]);
+    partial[blockIdx.x] = t;
+  }
+}
+
+__device__ __forceinline__ uint64_t gl_pow_dev(uint64_t b, uint64_t e) {
+  uint64_t r = 1;
+  while (e) {
+    if (e & 1) r = gl_mul(r, b);
+    b = gl_sqr(b);
+    e >>= 1;
+  }
+  return r;
+}
+
+// Every WG reduces the partials (f(z) = K1 S, c' = f(z) K2), then grid-
+// strides: C_j <- (C_j - f(z)) inv_j (= q(w^j)), rlo[t] = r^t, rhi[t] = c' r^(4096 t).
+__global__ void __launch_bounds__(NTT_THREADS) k_q_tables(uint64_t* __restrict__ C, const uint64_t* __restrict__ inv,
+                                                          const uint64_t* __restrict__ partial, uint32_t nparts,
+                                                          uint64_t n, uint64_t K1, uint64_t K2, uint64_t r,
+                                                          uint64_t r4096, uint64_t* __restrict__ rlo,
+                                                          uint64_t* __restrict__ rhi, uint32_t nhi) {
+  __shared__ uint64_t wsum[NTT_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint64_t acc = 0;
+  for (uint32_t i = tid; i < nparts; i += NTT_THREADS) acc = gl_add(acc, partial[i]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc = gl_add(acc, __shfl_xor(acc, o, 64));
+  if (lane == 0) wsum[wave] = acc;
+  __syncthreads();
+  uint64_t S = wsum[0];
+#pragma unroll
+  for (int w = 1; w < NTT_THREADS / 64; w++) S = gl_add(S, wsum[w]);
+  const uint64_t fz = gl_mul(K1, S), cp = gl_mul(fz, K2);
+  const uint64_t g0 = (uint64_t)blockIdx.x * NTT_THREADS + tid, gs = (uint64_t)gridDim.x * NTT_THREADS;
+  for (uint64_t j = g0; j < n; j += gs) C[j] = gl_mul(gl_sub(C[j], fz), inv[j]);
+  for (uint64_t t = g0; t < 4096; t += gs) rlo[t] = gl_pow_dev(r, t);
+  for (uint64_t t = g0; t < nhi; t += gs) rhi[t] = gl_mul(cp, gl_pow_dev(r4096, t));
+}
+
+hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
+                                int logN, uint64_t z, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096,
+                                uint64_t* rlo, uint64_t* rhi, const NttTables& T) {
+  if (logn < 4 || logN < logn || logN > 32) return hipErrorInvalidValue;
+  const uint64_t n = 1ULL << logn;
+  const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
+  const uint32_t nparts = (uint32_t)((n + per - 1) / per);
+  hipLaunchKernelGGL(k_inv_base, dim3(nparts), dim3(NTT_THREADS), 0, st, C, inv_scratch, partial, logn, z, T);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t nhi = logN > 12 ? (1u << (logN - 12)) : 1u;
+  const unsigned grid = (unsigned)std::min<uint64_t>(1024, (n + NTT_THREADS - 1) / NTT_THREADS);
+  hipLaunchKernelGGL(k_q_tables, dim3(grid), dim3(NTT_THREADS), 0, st, C, inv_scratch, partial, nparts, n, K1, K2, r,
+                     r4096, rlo, rhi, nhi);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ host side
 // SEZKP_NTT_RADIX2=1 forces the radix-2 LDS passes (A/B comparison)
 static bool ntt4_disabled() {
@@ -588,9 +741,10 @@ static bool deep_fused_disabled() {  // SEZKP_NO_DEEP_FUSE=1: separate k_deep (A
 }
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
                    const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e, const DeepFuse* deep,
-                   bool* fused) {
+                   bool* fused, const DeepPoly* dpoly) {
   if (fused) *fused = false;
   if (logN == 0) return hipSuccess;
+  if (dpoly && (!src || coset_e || logN > 32 || log_src >= logN)) return hipErrorInvalidValue;
   int ms[8], np;
   plan_passes(logN, src ? 3 : 1, ms, &np);
   // DIT order: smallest strides first; ensure the first pass holds >= 3 stages for the LDE skip
@@ -601,7 +755,8 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     P.a = a; P.tw = T; P.m = ms[i]; P.sL = sL; P.inverse = inverse ? 1 : 0;
     P.src = (i == 0) ? src : nullptr;
     P.log_src = log_src; P.inv_n = inv_n; P.coset_e = (i == 0) ? coset_e : 0;
-    P.skip = (i == 0 && src) ? (logN - log_src) : 0;
+    P.skip = (i == 0 && src && !dpoly) ? (logN - log_src) : 0;
+    if (i == 0 && dpoly) { P.dp_rlo = dpoly->rlo; P.dp_rhi = dpoly->rhi; P.dp_logN = logN; }
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
     uint64_t tiles = (1ULL << logN) >> (P.m + logC);
     // last pass, forward, 16 wide columns, M1 = 4 (m = 7 or 8), not the replicated first pass

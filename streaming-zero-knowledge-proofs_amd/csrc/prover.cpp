@@ -190,6 +190,7 @@ struct sezkp_ctx {
   uint64_t outer_stride = 0;
   uint32_t* d_colroots = nullptr;
   uint64_t* d_base = nullptr;
+  uint64_t *d_dq_part = nullptr, *d_dq_rlo = nullptr, *d_dq_rhi = nullptr;  // DEEP quotient (DeepPoly)
   uint64_t* d_lde = nullptr;
   uint64_t* d_fri = nullptr;
   uint32_t* d_roots = nullptr;
@@ -520,6 +521,11 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   const int k = logN;
   const uint64_t S = 1ULL << L16_LOG;
   d_base = dalloc<uint64_t>(n);
+  if (!sharded()) {
+    d_dq_part = dalloc<uint64_t>(n / 1024 + 1);
+    d_dq_rlo = dalloc<uint64_t>(4096);
+    d_dq_rhi = dalloc<uint64_t>(N > 4096 ? N >> 12 : 1);
+  }
   M = N >> logP;
   logM = logN - logP;
   rR = sharded() ? k - L16_LOG - logP : (k >= L16_LOG ? k - L16_LOG : -1);
@@ -747,6 +753,21 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   ok(launch_compose(st, T, A, mask, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
   if (sharded) comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st);
   rec(4);
+  // single device: DEEP as the LDE of H = q + c S (DeepPoly); the base
+  // evaluations become q(w^j) before the INTT. Not when z^n = 1 (z on the
+  // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
+  const uint64_t zn = hgl_pow(z, n);
+  const bool dq = !sharded && logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY");
+  DeepPoly dpoly{d_dq_rlo, d_dq_rhi};
+  if (dq) {
+    const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
+    const uint64_t zN = hgl_pow(zn, N / n);
+    const uint64_t K2 = hgl_mul(hgl_pow(z, N - 1), hgl_inv(hgl_sub(hgl_pow(3, N), zN)));  // c' = f(z) K2
+    const uint64_t r = hgl_mul(3, hgl_inv(z));
+    ok(launch_deep_quotient(st, d_base, d_lde, d_dq_part, logn, logN, z, K1, K2, r, hgl_pow(r, 4096), d_dq_rlo,
+                            d_dq_rhi, tw),
+       "deep_quotient");
+  }
   ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
   rec(5);
   // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on
@@ -755,8 +776,11 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   uint64_t* lde_out = sharded ? d_cyc : d_lde;
   const uint64_t coset_e = sharded ? ((uint64_t)rank << (tw.K - logN)) : 0;
   const DeepFuse dfuse{z, logN, logP, (uint32_t)rank};
-  bool deep_fused = false;
-  ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused), "lde_ntt");
+  bool deep_fused = dq;
+  if (dq)
+    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, 0, nullptr, nullptr, &dpoly), "lde_ntt");
+  else
+    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused), "lde_ntt");
   rec(6);
   if (!deep_fused) ok(launch_deep(st, lde_out, logN, z, tw, logP, (uint32_t)rank), "deep");
   if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI

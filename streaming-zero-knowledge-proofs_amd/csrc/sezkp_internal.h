@@ -30,6 +30,11 @@ struct NttPassArgs {
   uint64_t deep_z;
   int deep_logN, deep_logP;
   uint32_t deep_g;
+  // DEEP quotient LDE (first DIT pass, SKIP = 0): position p loads
+  // h_e = [e < n] src[p >> 3] n^-1 3^e + rhi[e >> 12] rlo[e & 4095], e = bitrev(p)
+  const uint64_t* dp_rlo;
+  const uint64_t* dp_rhi;
+  int dp_logN;
 };
 // DEEP division y_i / (3 w_N^(g + P i) - z) fused into the LDE's last pass
 struct DeepFuse {
@@ -37,13 +42,27 @@ struct DeepFuse {
   int logN, logP;
   uint32_t g;
 };
+// DEEP as a polynomial (single-device path): y_i / (x_i - z) = H(x_i) with
+// H = q + c S, q = (f - f(z)) / (X - z), S = sum_k z^(N-1-k) X^k and
+// c = f(z) / (3^N - z^N) (x_i^N = 3^N on the coset), so the LDE of H's
+// coefficients h_k = q_k 3^k + c' r^k (r = 3/z, c' = c z^(N-1)) IS the DEEP
+// layer: no per-point inversion. q comes from the base domain, where
+// q(w^j) = (C_j - f(z)) / (w^j - z) needs one batch inversion over n points
+// and f(z) is the barycentric sum  (1 - z^n)/n * sum_j C_j w^j / (w^j - z).
+struct DeepPoly {
+  const uint64_t* rlo;  // 4096 entries: r^t
+  const uint64_t* rhi;  // N >> 12 entries: c' r^(4096 t)
+};
+hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
+                                int logN, uint64_t z, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096,
+                                uint64_t* rlo, uint64_t* rhi, const NttTables& T);
 
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
 // deep != nullptr: fuse the DEEP division into the last pass when its shape
 // allows; *fused says whether it did (else the caller runs launch_deep).
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
                    const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e = 0,
-                   const DeepFuse* deep = nullptr, bool* fused = nullptr);
+                   const DeepFuse* deep = nullptr, bool* fused = nullptr, const DeepPoly* dpoly = nullptr);
 hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale,
                           bool do_scale);
 // distributed four-step NTT pieces (ntt.hip)
