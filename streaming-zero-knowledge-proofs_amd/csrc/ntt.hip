@@ -571,7 +571,7 @@ __global__ void __launch_bounds__(256) k_dntt_dft(uint64_t* __restrict__ r, uint
 // See DeepPoly (sezkp_internal.h). k_inv_base: inv_j = 1 / (w_n^j - z) for
 // the n base points (16 per lane, one Montgomery batch per 4096) and the
 // per-WG partial sums of C_j w_n^j inv_j.
-constexpr int DQ_PER = 4;
+constexpr int DQ_PER = 16;
 __global__ void __launch_bounds__(NTT_THREADS) k_inv_base(const uint64_t* __restrict__ C, uint64_t* __restrict__ inv,
                                                           uint64_t* __restrict__ partial, int logn, uint64_t z,
                                                           NttTables T) {

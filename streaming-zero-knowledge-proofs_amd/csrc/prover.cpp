@@ -522,7 +522,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   const uint64_t S = 1ULL << L16_LOG;
   d_base = dalloc<uint64_t>(n);
   if (!sharded()) {
-    d_dq_part = dalloc<uint64_t>(n / 1024 + 1);
+    d_dq_part = dalloc<uint64_t>(n / 4096 + 1);
     d_dq_rlo = dalloc<uint64_t>(4096);
     d_dq_rhi = dalloc<uint64_t>(N > 4096 ? N >> 12 : 1);
   }

@@ -424,28 +424,36 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
     // Each constraint type shares one alpha across tapes (air.rs:49-136), so
     // its per-tape terms are summed first (exactly, as integers where they are
     // small) and multiplied once: sum_r a*t_r = a * sum_r t_r in the field.
-    int64_t s_c2 = 0, s_c3 = 0, s_sy = 0;
-    uint64_t s_hr = 0, s_sl = 0, s_bf = 0, s_bl = 0;
+    int32_t s_c2 = 0, s_sy = 0;
+    int64_t s_c3 = 0;
+    uint64_t s_bf = 0, s_bl = 0;
+    // x - (x & 0xFFFF) = x & ~0xFFFF for canonical x: the head / slack terms
+    // are summed as exact integers (< 2^67, lo + carry count), reduced once
+    uint64_t hr_lo = 0, sl_lo = 0;
+    uint32_t hr_hi = 0, sl_hi = 0;
 #pragma unroll 4
     for (int r = 0; r < T.tau; r++) {
       const uint64_t o = (uint64_t)r * n;
-      const int64_t mv = T.mv[o + i];
+      const int32_t mv = T.mv[o + i];
       const int64_t head = T.head[o + i];
       const uint64_t head_f = gl_from_i64(head);
-      // C2: mv(mv-1)(mv+1) = mv^3 - mv  (|mv| <= 128: exact in i64)
+      // C2: mv(mv-1)(mv+1) = mv^3 - mv  (|mv| <= 128: exact in i32, 8 tapes)
       s_c2 += mv * mv * mv - mv;
       // C3: (1 - is_last) * (head' - head - mv'), |head| <= 128 n
       if (!is_last) s_c3 += T.head[o + ip1] - head - (int64_t)T.mv[o + ip1];
       if (T.wflag[o + i]) {
+        uint32_t c;
         // head - sum(head_bits * 2^k)
-        s_hr = gl_add(s_hr, gl_sub(head_f, head_f & 0xFFFF));
+        hr_lo = add64c(hr_lo, head_f & ~0xFFFFULL, c);
+        hr_hi += c;
         // slack = (win_len - 1) - head, reconstructed from 16 bits
         const uint64_t winlen = T.blk_winlen[(uint64_t)r * T.nblk + blk];
         const uint64_t slack = gl_sub(gl_sub(winlen, 1), head_f);
-        s_sl = gl_add(s_sl, gl_sub(slack, slack & 0xFFFF));
+        sl_lo = add64c(sl_lo, slack & ~0xFFFFULL, c);
+        sl_hi += c;
         // symbol 4-bit decomposition
-        const int64_t sym = T.wsym[o + i];
-        s_sy += sym - (sym & 0xF);
+        const int32_t sym = T.wsym[o + i];
+        s_sy += sym & ~0xF;
       }
       if (is_first) {
         const uint64_t offin = T.blk_offin[(uint64_t)r * T.nblk + blk];
@@ -456,6 +464,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
         s_bl = gl_add(s_bl, gl_sub(head_f, offout));
       }
     }
+    const uint64_t s_hr = gl_reduce128(hr_lo, hr_hi), s_sl = gl_reduce128(sl_lo, sl_hi);
     uint64_t acc = 0;
     if (s_c2) acc = gl_mul(A.mv_domain, gl_from_i64(s_c2));
     if (s_c3) acc = gl_add(acc, gl_mul(A.head_update, gl_from_i64(s_c3)));
