@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--cpu-sample-log-t", type=int, default=18)
     ap.add_argument("--cpu-mt-log-t", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the BASELINE config 2 (2^20 NTT) and config 3 (T=2^18 prove) objects")
     ap.add_argument("--no-sharded", action="store_true",
                     help="N>1: skip the extra sharded (one proof over all GPUs) measurement")
     ap.add_argument("--sharded-steps", type=int, default=3)
@@ -306,6 +308,8 @@ def main():
         if rank == 0:
             out[key] = res
 
+    if rank == 0 and not args.no_configs:
+        guarded("configs", lambda: measure_configs(args, torch))
     if args.dntt_log_n:
         # BASELINE config 4 (at N = 8): 2^26-point four-step NTT over all ranks
         guarded("dist_ntt", lambda: measure_dist_ntt(args, world, rank, local, dist, torch))
@@ -316,6 +320,105 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def det_vec(n: int, seed: int):
+    """crates/sezkp-ffts/benches/ntt.rs:21-34: LCG (A=1664525, C=1013904223,
+    mod 2^32) started at A*seed + C, stepped before each use; value
+    (a_i ^ i*0x9E3779B97F4A7C15) mod p. Vectorised with the affine powers
+    f^(j+1)(x) = mul_j x + add_j (mod 2^32) per block of 4096."""
+    import numpy as np
+    P = 0xFFFFFFFF00000001
+    A, Cc, M32 = 1664525, 1013904223, 0xFFFFFFFF
+    blk = 1 << 12
+    mul = np.empty(blk, dtype=np.uint64)
+    add = np.empty(blk, dtype=np.uint64)
+    m, c = 1, 0
+    for j in range(blk):
+        m, c = (A * m) & M32, (A * c + Cc) & M32
+        mul[j], add[j] = m, c
+    a = np.empty(n, dtype=np.uint64)
+    x = (A * seed + Cc) & M32
+    for lo in range(0, n, blk):
+        hi = min(n, lo + blk)
+        a[lo:hi] = (mul[: hi - lo] * np.uint64(x) + add[: hi - lo]) & np.uint64(M32)
+        x = (int(mul[-1]) * x + int(add[-1])) & M32
+    v = a ^ (np.arange(n, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+    return np.where(v >= np.uint64(P), v - np.uint64(P), v)
+
+
+def measure_configs(args, torch):
+    """BASELINE configs 2 and 3 on this GPU: the 2^20-point forward + inverse
+    NTT of det_vec(2^20, 2024) through sezkp_gl_ntt (round trip checked), and
+    the full T = 2^18 prove (one proof at a time and 3 in flight)."""
+    from sezkp_amd import ProverContext, reference_blocks
+    from sezkp_amd._lib import lib
+    out = {}
+    n = 1 << 20
+    x = torch.from_numpy(det_vec(n, 2024).view("int64")).cuda()
+    d, s = x.clone(), torch.empty_like(x)
+    for _ in range(3):
+        assert lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, 1, None) == 0
+        assert lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, -1, None) == 0
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(d, x))
+    reps = 50
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, 1, None)
+        lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, -1, None)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    out["c2_ntt_2e20"] = {"workload": "2^20-point Goldilocks NTT, forward + inverse (natural order in and out), "
+                                      "det_vec(2^20, 2024) input, sezkp_gl_ntt",
+                          "ms_fwd_plus_inv": ms, "value": 2 * n / (ms * 1e-3), "unit": "field-elements/s",
+                          "roundtrip_ok": ok and bool(torch.equal(d, x))}
+    # config 3: T = 2^18 full prove
+    T = 1 << 18
+    ctxs, roots = [], []
+    for i in range(3):
+        bl = reference_blocks(T, args.b, args.tau, 42 + i)
+        c = ProverContext(0)
+        c.upload(bl)
+        ctxs.append(c)
+        roots.append(bl.manifest_root())
+    for c, r in zip(ctxs, roots):
+        c.prove_view(r)
+    torch.cuda.synchronize()
+    steps = 20
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctxs[0].prove_view(roots[0])
+    t1 = (time.perf_counter() - t0) / steps
+    import threading
+    lock = threading.Lock()
+    left = [3 * steps]
+
+    def pipe(i):
+        while True:
+            with lock:
+                if left[0] == 0:
+                    return
+                left[0] -= 1
+            ctxs[i].prove_async(roots[i])
+            ctxs[i].wait_view()
+    t0 = time.perf_counter()
+    ws = [threading.Thread(target=pipe, args=(i,)) for i in range(3)]
+    for w in ws:
+        w.start()
+    for w in ws:
+        w.join()
+    t3 = (time.perf_counter() - t0) / (3 * steps)
+    for c in ctxs:
+        c.close()
+    N = 8 * T
+    out["c3_prove_2e18"] = {"workload": f"stark-v1 prove T=2^18 (N=2^21), b={args.b}, tau={args.tau}",
+                            "single_proof_ms": t1 * 1e3, "value_single": N / t1,
+                            "inflight3_ms_per_proof": t3 * 1e3, "value_inflight3": N / t3,
+                            "unit": "field-elements/s"}
+    return out
 
 
 def measure_dist_ntt(args, world, rank, local, dist, torch):
