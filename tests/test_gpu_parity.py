@@ -211,6 +211,19 @@ def test_prove_dictionary_branches_bit_exact(gpu_ok, product, oracle, monkeypatc
     assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
 
 
+@pytest.mark.parametrize("T", [16, 1 << 12, 1 << 16])
+def test_prove_deep_paths_bit_exact(gpu_ok, product, oracle, monkeypatch, T):
+    """Single device: DEEP as the LDE of q + c*S (DeepPoly, the default) and the
+    per-point division fused into the last LDE pass (SEZKP_NO_DEEP_POLY=1)
+    give the reference's bytes; T = 16 is the smallest size on the polynomial path."""
+    blocks = product.synthetic_blocks(T, min(T, 512), 3, 7)
+    mroot = blocks.manifest_root()
+    want = oracle.prove_v1(blocks, mroot)
+    assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
+    monkeypatch.setenv("SEZKP_NO_DEEP_POLY", "1")
+    assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
+
+
 def test_prove_rejects_bad_shapes(gpu_ok, product):
     blocks = product.synthetic_blocks(96, 32, 2)  # n = 96, not a power of two
     with pytest.raises(product.SezkpError, match="power of two"):

@@ -156,6 +156,36 @@ def test_coset_invariants(oracle):  # coset_lde.rs:23-64
         np.testing.assert_array_equal(oracle.ntt_forward(scaled), oracle.coset_lde(np.array(c, np.uint64), k, shift))
 
 
+@pytest.mark.parametrize("logn", [2, 3, 4])
+def test_deep_as_polynomial_identity(logn):
+    """The product's single-device DEEP (DeepPoly, sezkp_internal.h): the
+    reference's y_i / (x_i - z), x_i = 3 w_N^i (lde.rs:76-93), equals the LDE
+    of h_k = q_k 3^k [k < n] + c' r^k with q = (f - f(z)) / (X - z) built on
+    the base domain, f(z) barycentric, r = 3/z, c' = f(z) z^(N-1) / (3^N - z^N).
+    Restated here with the pure-Python oracle's naive DFTs."""
+    import random
+    import sezkp_oracle_py as PY
+    rng = random.Random(logn)
+    n, N = 1 << logn, 8 << logn
+    wn, wN = PY.root_2exp(logn), PY.root_2exp(logn + 3)
+    C = [rng.randrange(P) for _ in range(n)]
+    z = rng.randrange(P)
+    assert pow(z * PY.inv(3) % P, N, P) != 1 and pow(z, n, P) != 1
+    # reference: coefficients, coset LDE, per-point division
+    f = PY.idft(C, wn) + [0] * (N - n)
+    y = PY.dft([fk * pow(3, k, P) % P for k, fk in enumerate(f)], wN)
+    want = [y[i] * PY.inv((3 * pow(wN, i, P) - z) % P) % P for i in range(N)]
+    # product formulation
+    invb = [PY.inv((pow(wn, j, P) - z) % P) for j in range(n)]
+    S = sum(C[j] * pow(wn, j, P) * invb[j] for j in range(n)) % P
+    fz = (1 - pow(z, n, P)) * PY.inv(n) * S % P
+    q = PY.idft([(C[j] - fz) * invb[j] % P for j in range(n)], wn)
+    cp = fz * pow(z, N - 1, P) * PY.inv((pow(3, N, P) - pow(z, N, P)) % P) % P
+    r = 3 * PY.inv(z) % P
+    h = [((q[k] * pow(3, k, P) if k < n else 0) + cp * pow(r, k, P)) % P for k in range(N)]
+    assert PY.dft(h, wN) == want
+
+
 def test_roots_of_unity(oracle):  # lib.rs:268-275
     for k in range(1, 33):
         w = oracle.lib().orc_gl_root_2exp(k)
