@@ -940,7 +940,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   // openings first: their section of the proof (~70% of it) goes back over
   // PCIe on the side stream while the FRI path kernel runs
   ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 3 * max_fri_req, (int)no, PL, d_tabs,
-                     d_dlev, d_dplans),
+                     d_dlev, d_dplans, d_dtabs, d_dcols),
      "col_open");
   rec(ST_OPEN + 1);
   if (!sharded) {

@@ -277,6 +277,6 @@ hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const u
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
                            const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev,
-                           const DictPlan* d_plans);
+                           const DictPlan* d_plans, const uint32_t* d_dtabs, const DictCol* d_dcols);
 
 }  // namespace sezkp

@@ -479,112 +479,6 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
   }
 }
 
-// -------------------------------------------------------- column openings
-// One 256-lane WG per request (column, row): rebuild the row's chunk tree in
-// LDS (<= 1024 leaves), emit value, chunk root, path in chunk, and the chunk
-// root's path in the stored outer tree.
-// Record words: [0,1] value, [2..9] chunk_root, [10..89] path_in (<=10),
-// [90..345] path_to_chunk (<=32).
-__global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTemplate* __restrict__ tmpl,
-                                                         const uint32_t* __restrict__ outer, uint64_t outer_stride,
-                                                         int logChunks, const uint32_t* __restrict__ req,
-                                                         ProofLayout P, const uint32_t* __restrict__ tabs,
-                                                         const uint32_t* __restrict__ dlev,
-                                                         const DictPlan* __restrict__ plans) {
-  __shared__ uint32_t lds[8][1024];
-  const uint32_t* rq = req + OPEN_REQ_WORDS * (uint64_t)blockIdx.x;
-  const int c = rq[0];
-  const uint64_t row = (uint64_t)rq[1] | ((uint64_t)rq[2] << 32);
-  const uint32_t q = rq[3];     // ordinal of this opening in the proof
-  const uint32_t dsel = rq[4];  // dictionary column index (chunk levels 6..9 stored), or NO_DICT
-  const ColTemplate ct = tmpl[c];
-  const int tid = threadIdx.x;
-  const uint64_t n = T.n;
-  const uint64_t ch = row >> COL_CHUNK_LOG2;
-  const uint64_t start = ch << COL_CHUNK_LOG2;
-  const uint64_t cl = n < 1024 ? n : 1024;
-  int logcl = 0;
-  while ((1ULL << logcl) < cl) logcl++;
-  // Opening record (proof.rs:44-66): value, index, chunk_index, index_in_chunk,
-  // chunk_root, path_in_chunk (u64 len + siblings), path_to_chunk (u64 len + siblings)
-  const uint32_t qi = q / P.open_per_q, s = q % P.open_per_q;
-  uint32_t* qb = P.base + (8 + (uint64_t)qi * P.q_bytes) / 4;
-  uint32_t* o = qb + (16 + (uint64_t)s * P.open_bytes) / 4;
-  const uint64_t in = row - start;
-  if (tid == 0) {
-    o[2] = (uint32_t)row; o[3] = (uint32_t)(row >> 32);
-    o[4] = (uint32_t)ch; o[5] = (uint32_t)(ch >> 32);
-    o[6] = (uint32_t)in; o[7] = 0;
-    o[16] = (uint32_t)logcl; o[17] = 0;
-    o[18 + 8 * logcl] = (uint32_t)logChunks; o[19 + 8 * logcl] = 0;
-  }
-  if (tid == 0) {
-    const uint64_t v = col_value(T, ct, row);
-    o[0] = (uint32_t)v;
-    o[1] = (uint32_t)(v >> 32);
-  }
-  // Dictionary columns: rebuild only the 64-row group holding `row` (levels
-  // 0..5); levels 6..9 were stored by the commitment, the chunk root is the
-  // outer tree's leaf.
-  const bool dict = dsel != NO_DICT && logcl == COL_CHUNK_LOG2;
-  const int glog = dict ? DICT_LANE_LOG + dict_extra(plans[dsel].K) : logcl;
-  const uint64_t gstart = dict ? (row & ~((1ULL << glog) - 1)) : start;
-  // piecewise columns read their leaves from the uniform-subtree tables (U_0)
-  const bool pw = kind_piecewise(ct.kind) && ct.tab != NO_TAB;
-  for (uint64_t i = tid; i < (1ULL << glog); i += TR_THREADS) {
-    uint32_t h[8];
-    const uint64_t r = gstart + i;
-    if (pw) {
-      const uint64_t u = (ct.kind == 1 || ct.kind == 2) ? ((T.row_flags[r] >> (ct.kind - 1)) & 1) : T.row_blk[r];
-      node_load(tabs + 8 * (ct.tab + u * U_LEVELS), h);
-    } else {
-      leaf_labeled_rt(ct, col_value(T, ct, r), h);
-    }
-#pragma unroll
-    for (int w = 0; w < 8; w++) lds[w][i] = h[w];
-  }
-  __syncthreads();
-  const uint64_t gin = row - gstart;
-  int cnt = 1 << glog;
-  for (int lvl = 0; lvl < glog; lvl++) {
-    const int sib = (int)((gin >> lvl) ^ 1);
-    if (tid < 8) o[18 + 8 * lvl + tid] = lds[tid][sib];
-    const int half = cnt >> 1;
-    uint32_t hh[2][8];
-    int k = 0;
-    for (int p = tid; p < half; p += TR_THREADS, k++) {
-      uint32_t a[8], b[8];
-#pragma unroll
-      for (int w = 0; w < 8; w++) { a[w] = lds[w][2 * p]; b[w] = lds[w][2 * p + 1]; }
-      b3_parent(a, b, hh[k]);
-    }
-    __syncthreads();
-    k = 0;
-    for (int p = tid; p < half; p += TR_THREADS, k++)
-#pragma unroll
-      for (int w = 0; w < 8; w++) lds[w][p] = hh[k][w];
-    __syncthreads();
-    cnt = half;
-  }
-  const uint32_t* ob = outer + (uint64_t)c * outer_stride * 8;
-  if (dict) {
-    const uint32_t* lev = dlev + 8 * ((uint64_t)dsel * (T.n >> COL_CHUNK_LOG2) + ch) * DLEV_NODES;
-    for (int lvl = glog; lvl < COL_CHUNK_LOG2; lvl++) {
-      const uint64_t sib = (in >> lvl) ^ 1;
-      if (tid < 8) o[18 + 8 * lvl + tid] = lev[8 * (dlev_base(lvl) + sib) + tid];
-    }
-    if (tid < 8) o[8 + tid] = ob[8 * ch + tid];  // chunk root = outer leaf
-  } else {
-    if (tid < 8) o[8 + tid] = lds[tid][0];
-  }
-  // path_to_chunk from the stored outer tree (all levels kept)
-  uint32_t* op = o + 20 + 8 * logcl;
-  for (int lvl = 0; lvl < logChunks; lvl++) {
-    const uint64_t sib = (ch >> lvl) ^ 1;
-    if (tid < 8) op[8 * lvl + tid] = ob[8 * (tree_level_off(logChunks, 0, lvl) + sib) + tid];
-  }
-}
-
 // ------------------------------------------------ dictionary commitments
 // Exact memoization for the dense columns (input_mv, mv, write_flag,
 // write_sym, head). Their raw integers lie in a small range [min, min+R) on
@@ -722,6 +616,252 @@ __device__ __forceinline__ void lane_tree(const Prov& P, uint32_t (&h)[8]) {
 #pragma unroll
       for (int w = 0; w < 8; w++) h[w] = x[w];
     }
+  }
+}
+
+// -------------------------------------------------------- column openings
+// Hash of the aligned range [r0, r0 + 2^lw) of a piecewise-constant column:
+// the run pieces of k_col_commit_pw (maximal aligned dyadic intervals, U_l
+// lookups) merged on this lane's LDS stack. False if the stack overflows or
+// the block table is inconsistent (the commitment flags those chunks).
+__device__ __forceinline__ bool pw_range_hash(const TraceDev& T, uint32_t kind, const uint32_t* __restrict__ U,
+                                              uint64_t r0, int lw, uint32_t (*stk)[8][64], int slot,
+                                              uint32_t (&out)[8]) {
+  const uint64_t c1 = r0 + (1ULL << lw);
+  uint64_t lvpack = 0;
+  int sp = 0;
+  uint32_t k = T.row_blk[r0];
+  uint64_t row = r0;
+  while (row < c1) {
+    if (k >= T.nblk) return false;
+    const uint64_t bs = T.blk_start[k], be = T.blk_start[k + 1];
+    if (be <= row) { k++; continue; }
+    const uint64_t pe = be < c1 ? be : c1;
+    uint64_t cut = pe;
+    uint32_t u = k;
+    if (kind == 1) { u = row == bs ? 1u : 0u; cut = row == bs ? row + 1 : pe; }
+    else if (kind == 2) { u = row + 1 == be ? 1u : 0u; cut = (row + 1 < be && pe == be) ? be - 1 : pe; }
+    while (row < cut) {
+      const uint64_t off = row - r0, len = cut - row;
+      int l = off ? __builtin_ctzll(off) : lw;
+      if (l > lw) l = lw;
+      while ((1ULL << l) > len) l--;
+      const uint64_t step = 1ULL << l;
+      uint32_t h[8];
+      node_load(U + 8 * ((uint64_t)u * U_LEVELS + l), h);
+      while (sp > 0 && (int)((lvpack >> (4 * (sp - 1))) & 15) == l) {
+        uint32_t left[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) left[w] = stk[sp - 1][w][slot];
+        b3_parent(left, h, h);
+        sp--;
+        l++;
+      }
+      if (sp >= PW_STACK) return false;
+#pragma unroll
+      for (int w = 0; w < 8; w++) stk[sp][w][slot] = h[w];
+      lvpack = (lvpack & ~(15ULL << (4 * sp))) | ((uint64_t)l << (4 * sp));
+      sp++;
+      row += step;
+    }
+  }
+  if (sp != 1) return false;
+#pragma unroll
+  for (int w = 0; w < 8; w++) out[w] = stk[0][w][slot];
+  return true;
+}
+
+// level-K node of a dictionary column covering rows [row, row + 2^K) (the
+// commitment's DictNodes / DeltaNodes for one node)
+__device__ __forceinline__ void dict_node_at(const TraceDev& T, const ColTemplate& ct, const DictPlan& P,
+                                             const uint32_t* __restrict__ tab, uint64_t row, uint32_t (&h)[8]) {
+  if (P.delta) {
+    const uint64_t o = (uint64_t)ct.tape * T.n + row;
+    DeltaNodes{T.head + o, T.mv + o, T.row_flags + row, tab + 8 * (uint64_t)DICT_CAP, tab + 16 * (uint64_t)DICT_CAP,
+               P.min, P.dmin, P.R, P.dR}
+        .get(0, h);
+    return;
+  }
+#define SEZKP_DN(KEY)                                                                                           \
+  {                                                                                                             \
+    const KEY* p = dict_keys<KEY>(T, ct) + row;                                                                 \
+    switch (P.K) {                                                                                              \
+      case 0: DictNodes<KEY, 0>{p, tab, P.min, P.R}.get(0, h); break;                                           \
+      case 1: DictNodes<KEY, 1>{p, tab + 8 * (uint64_t)DICT_CAP, P.min, P.R}.get(0, h); break;                  \
+      case 2: DictNodes<KEY, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}.get(0, h); break;                 \
+      case 3: DictNodes<KEY, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}.get(0, h); break;                 \
+      default: DictNodes<KEY, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}.get(0, h); break;                \
+    }                                                                                                           \
+  }
+  switch (ct.kind) {
+    case 0: case 3: SEZKP_DN(int8_t) break;
+    case 4: SEZKP_DN(uint8_t) break;
+    case 5: SEZKP_DN(uint16_t) break;
+    default: SEZKP_DN(int64_t) break;
+  }
+#undef SEZKP_DN
+}
+
+// One 256-lane WG per request (column, row). Record words: [0,1] value,
+// [2..9] chunk_root, [10..89] path_in (<= 10), [90..345] path_to_chunk (<= 32).
+//  - piecewise columns: sibling at level l = hash of an aligned 2^l-row range
+//    (one lane per level, U_l lookups + merges at run boundaries only);
+//  - dictionary columns (K >= 0): siblings below K are table entries T_l,
+//    levels K..(6+a)-1 reduce the group's 2^(6+a-K) level-K table nodes in
+//    LDS, levels (6+a)..9 were stored by the commitment;
+//  - other columns: the chunk (or 64-row group) rebuilt from leaves in LDS.
+// Chunk roots come from the stored outer tree (its leaves) for every column
+// kind but the rebuilt one, and path_to_chunk from the outer tree.
+__global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                         const uint32_t* __restrict__ outer, uint64_t outer_stride,
+                                                         int logChunks, const uint32_t* __restrict__ req,
+                                                         ProofLayout P, const uint32_t* __restrict__ tabs,
+                                                         const uint32_t* __restrict__ dlev,
+                                                         const DictPlan* __restrict__ plans,
+                                                         const uint32_t* __restrict__ dtabs,
+                                                         const DictCol* __restrict__ dcols) {
+  __shared__ uint32_t lds[8][1024];
+  const uint32_t* rq = req + OPEN_REQ_WORDS * (uint64_t)blockIdx.x;
+  const int c = rq[0];
+  const uint64_t row = (uint64_t)rq[1] | ((uint64_t)rq[2] << 32);
+  const uint32_t q = rq[3];     // ordinal of this opening in the proof
+  const uint32_t dsel = rq[4];  // dictionary column index (chunk levels stored), or NO_DICT
+  const ColTemplate ct = tmpl[c];
+  const int tid = threadIdx.x;
+  const uint64_t n = T.n;
+  const uint64_t ch = row >> COL_CHUNK_LOG2;
+  const uint64_t start = ch << COL_CHUNK_LOG2;
+  const uint64_t cl = n < 1024 ? n : 1024;
+  int logcl = 0;
+  while ((1ULL << logcl) < cl) logcl++;
+  // Opening record (proof.rs:44-66): value, index, chunk_index, index_in_chunk,
+  // chunk_root, path_in_chunk (u64 len + siblings), path_to_chunk (u64 len + siblings)
+  const uint32_t qi = q / P.open_per_q, s = q % P.open_per_q;
+  uint32_t* qb = P.base + (8 + (uint64_t)qi * P.q_bytes) / 4;
+  uint32_t* o = qb + (16 + (uint64_t)s * P.open_bytes) / 4;
+  const uint64_t in = row - start;
+  if (tid == 0) {
+    o[2] = (uint32_t)row; o[3] = (uint32_t)(row >> 32);
+    o[4] = (uint32_t)ch; o[5] = (uint32_t)(ch >> 32);
+    o[6] = (uint32_t)in; o[7] = 0;
+    o[16] = (uint32_t)logcl; o[17] = 0;
+    o[18 + 8 * logcl] = (uint32_t)logChunks; o[19 + 8 * logcl] = 0;
+    const uint64_t v = col_value(T, ct, row);
+    o[0] = (uint32_t)v;
+    o[1] = (uint32_t)(v >> 32);
+  }
+  const uint32_t* ob = outer + (uint64_t)c * outer_stride * 8;
+  const bool pw = kind_piecewise(ct.kind) && ct.tab != NO_TAB;
+  const bool dict = dsel != NO_DICT && logcl == COL_CHUNK_LOG2;
+  const int K = dict ? plans[dsel].K : -1;
+  if (pw) {
+    if (tid < logcl) {
+      uint32_t h[8];
+      const uint64_t rs = start + (((in >> tid) ^ 1) << tid);
+      if (pw_range_hash(T, ct.kind, tabs + 8 * (uint64_t)ct.tab, rs, tid,
+                        reinterpret_cast<uint32_t(*)[8][64]>(&lds[0][0]), tid, h)) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) o[18 + 8 * tid + w] = h[w];
+      }
+    }
+    if (tid < 8) o[8 + tid] = ob[8 * ch + tid];  // chunk root = outer leaf
+  } else if (dict && K >= 0) {
+    const DictPlan Pl = plans[dsel];
+    const uint32_t* tab = dtabs + 8 * dcols[dsel].tab;
+    const int glog = DICT_LANE_LOG + dict_extra(K);
+    const int D = glog - K;
+    const uint64_t gstart = row & ~((1ULL << glog) - 1);
+    for (int j = tid; j < (1 << D); j += TR_THREADS) {
+      uint32_t h[8];
+      dict_node_at(T, ct, Pl, tab, gstart + ((uint64_t)j << K), h);
+#pragma unroll
+      for (int w = 0; w < 8; w++) lds[w][j] = h[w];
+    }
+    if (tid < K) {  // siblings below the table level: T_l[code of the 2^l sibling rows]
+      const int l = tid;
+      const uint64_t rs = ((row >> l) ^ 1) << l;
+      uint64_t idx = 0;
+      for (int i = (1 << l) - 1; i >= 0; i--) idx = idx * Pl.R + (uint64_t)(dict_key_at(T, ct, rs + i) - Pl.min);
+      const uint32_t* e = tab + 8 * ((uint64_t)l * DICT_CAP + idx);
+#pragma unroll
+      for (int w = 0; w < 8; w++) o[18 + 8 * l + w] = e[w];
+    }
+    __syncthreads();
+    const uint64_t gin = (row - gstart) >> K;
+    int cnt = 1 << D;
+    for (int lvl = K; lvl < glog; lvl++) {
+      const int sib = (int)((gin >> (lvl - K)) ^ 1);
+      if (tid < 8) o[18 + 8 * lvl + tid] = lds[tid][sib];
+      const int half = cnt >> 1;
+      uint32_t hh[8];
+      if (tid < half) {
+        uint32_t a[8], b[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) { a[w] = lds[w][2 * tid]; b[w] = lds[w][2 * tid + 1]; }
+        b3_parent(a, b, hh);
+      }
+      __syncthreads();
+      if (tid < half)
+#pragma unroll
+        for (int w = 0; w < 8; w++) lds[w][tid] = hh[w];
+      __syncthreads();
+      cnt = half;
+    }
+    const uint32_t* lev = dlev + 8 * ((uint64_t)dsel * (T.n >> COL_CHUNK_LOG2) + ch) * DLEV_NODES;
+    for (int lvl = glog; lvl < COL_CHUNK_LOG2; lvl++) {
+      const uint64_t sib = (in >> lvl) ^ 1;
+      if (tid < 8) o[18 + 8 * lvl + tid] = lev[8 * (dlev_base(lvl) + sib) + tid];
+    }
+    if (tid < 8) o[8 + tid] = ob[8 * ch + tid];
+  } else {
+    // rebuild the chunk (or, for a K = -1 dictionary column, its 64-row group)
+    const int glog = dict ? DICT_LANE_LOG + dict_extra(K) : logcl;
+    const uint64_t gstart = dict ? (row & ~((1ULL << glog) - 1)) : start;
+    for (uint64_t i = tid; i < (1ULL << glog); i += TR_THREADS) {
+      uint32_t h[8];
+      leaf_labeled_rt(ct, col_value(T, ct, gstart + i), h);
+#pragma unroll
+      for (int w = 0; w < 8; w++) lds[w][i] = h[w];
+    }
+    __syncthreads();
+    const uint64_t gin = row - gstart;
+    int cnt = 1 << glog;
+    for (int lvl = 0; lvl < glog; lvl++) {
+      const int sib = (int)((gin >> lvl) ^ 1);
+      if (tid < 8) o[18 + 8 * lvl + tid] = lds[tid][sib];
+      const int half = cnt >> 1;
+      uint32_t hh[2][8];
+      int k = 0;
+      for (int p = tid; p < half; p += TR_THREADS, k++) {
+        uint32_t a[8], b[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) { a[w] = lds[w][2 * p]; b[w] = lds[w][2 * p + 1]; }
+        b3_parent(a, b, hh[k]);
+      }
+      __syncthreads();
+      k = 0;
+      for (int p = tid; p < half; p += TR_THREADS, k++)
+#pragma unroll
+        for (int w = 0; w < 8; w++) lds[w][p] = hh[k][w];
+      __syncthreads();
+      cnt = half;
+    }
+    if (dict) {
+      const uint32_t* lev = dlev + 8 * ((uint64_t)dsel * (T.n >> COL_CHUNK_LOG2) + ch) * DLEV_NODES;
+      for (int lvl = glog; lvl < COL_CHUNK_LOG2; lvl++) {
+        const uint64_t sib = (in >> lvl) ^ 1;
+        if (tid < 8) o[18 + 8 * lvl + tid] = lev[8 * (dlev_base(lvl) + sib) + tid];
+      }
+      if (tid < 8) o[8 + tid] = ob[8 * ch + tid];  // chunk root = outer leaf
+    } else {
+      if (tid < 8) o[8 + tid] = lds[tid][0];
+    }
+  }
+  // path_to_chunk from the stored outer tree (all levels kept)
+  uint32_t* op = o + 20 + 8 * logcl;
+  for (int lvl = 0; lvl < logChunks; lvl++) {
+    const uint64_t sib = (ch >> lvl) ^ 1;
+    if (tid < 8) op[8 * lvl + tid] = ob[8 * (tree_level_off(logChunks, 0, lvl) + sib) + tid];
   }
 }
 
@@ -1059,11 +1199,11 @@ hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, co
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
                            const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev,
-                           const DictPlan* d_plans) {
+                           const DictPlan* d_plans, const uint32_t* d_dtabs, const DictCol* d_dcols) {
   if (nreq == 0) return hipSuccess;
   if ((uint64_t)nreq > (uint64_t)P.nq * P.open_per_q) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_col_open, dim3(nreq), dim3(TR_THREADS), 0, st, T, d_tmpl, outer_nodes, outer_stride_nodes,
-                     logChunks, d_req, P, tabs, d_dlev, d_plans);
+                     logChunks, d_req, P, tabs, d_dlev, d_plans, d_dtabs, d_dcols);
   return hipGetLastError();
 }
 
