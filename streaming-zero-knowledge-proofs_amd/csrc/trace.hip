@@ -22,7 +22,7 @@ constexpr int TR_THREADS = 256;
 // One workgroup per block: row -> block id, first/last flags, and the
 // post-move head prefix sums per tape (head starts at 0 in every block).
 __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) {
-  __shared__ int64_t wsum[TR_THREADS / 64];
+  __shared__ int32_t wsum[TR_THREADS / 64];
   const uint32_t b = b0 + blockIdx.x;
   const uint64_t s = T.blk_start[b], e = T.blk_start[b + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -30,27 +30,32 @@ __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) 
     T.row_blk[r] = b;
     T.row_flags[r] = (uint8_t)((r == s ? 1 : 0) | (r + 1 == e ? 2 : 0));
   }
+  // head = block-local inclusive prefix sum of the tape's moves; two rows per
+  // lane, 32-bit scan (|sum| <= 128 * rows per iteration), 64-bit carry
   for (int tp = 0; tp < T.tau; tp++) {
     const int8_t* mv = T.mv + (uint64_t)tp * T.n;
     int64_t* hd = T.head + (uint64_t)tp * T.n;
     int64_t carry = 0;
-    for (uint64_t r0 = s; r0 < e; r0 += TR_THREADS) {
-      const uint64_t r = r0 + tid;
-      int64_t x = (r < e) ? (int64_t)mv[r] : 0;
+    for (uint64_t r0 = s; r0 < e; r0 += 2 * TR_THREADS) {
+      const uint64_t r = r0 + 2 * (uint64_t)tid;
+      const int32_t m0 = r < e ? (int32_t)mv[r] : 0, m1 = r + 1 < e ? (int32_t)mv[r + 1] : 0;
+      int32_t x = m0 + m1;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
-        int64_t y = __shfl_up(x, o, 64);
+        const int32_t y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
       }
       if (lane == 63) wsum[wave] = x;
       __syncthreads();
-      int64_t pre = carry, tot = 0;
+      int32_t pre = 0, tot = 0;
 #pragma unroll
       for (int w = 0; w < TR_THREADS / 64; w++) {
         if (w < wave) pre += wsum[w];
         tot += wsum[w];
       }
-      if (r < e) hd[r] = pre + x;
+      const int64_t h1 = carry + (int64_t)(pre + x);  // through row r + 1
+      if (r < e) hd[r] = h1 - m1;
+      if (r + 1 < e) hd[r + 1] = h1;
       carry += tot;
       __syncthreads();
     }
@@ -880,16 +885,27 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const Col
   int64_t lo = INT64_MAX, hi = INT64_MIN;
   if (r0 < row_end) {
     int64_t k[16];
-    switch (ct.kind) {
-      case 0: case 3: load_keys<int8_t, 16>(dict_keys<int8_t>(T, ct) + r0, k); break;
-      case 4: load_keys<uint8_t, 16>(dict_keys<uint8_t>(T, ct) + r0, k); break;
-      case 5: load_keys<uint16_t, 16>(dict_keys<uint16_t>(T, ct) + r0, k); break;
-      default: load_keys<int64_t, 16>(dict_keys<int64_t>(T, ct) + r0, k); break;
-    }
+    if (ct.kind == 6) {  // head: 64-bit keys
+      load_keys<int64_t, 16>(dict_keys<int64_t>(T, ct) + r0, k);
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      lo = k[i] < lo ? k[i] : lo;
-      hi = k[i] > hi ? k[i] : hi;
+      for (int i = 0; i < 16; i++) {
+        lo = k[i] < lo ? k[i] : lo;
+        hi = k[i] > hi ? k[i] : hi;
+      }
+    } else {  // narrow keys: 32-bit min / max
+      switch (ct.kind) {
+        case 0: case 3: load_keys<int8_t, 16>(dict_keys<int8_t>(T, ct) + r0, k); break;
+        case 4: load_keys<uint8_t, 16>(dict_keys<uint8_t>(T, ct) + r0, k); break;
+        default: load_keys<uint16_t, 16>(dict_keys<uint16_t>(T, ct) + r0, k); break;
+      }
+      int32_t l32 = (int32_t)k[0], h32 = (int32_t)k[0];
+#pragma unroll
+      for (int i = 1; i < 16; i++) {
+        l32 = min(l32, (int32_t)k[i]);
+        h32 = max(h32, (int32_t)k[i]);
+      }
+      lo = l32;
+      hi = h32;
     }
   }
 #pragma unroll
