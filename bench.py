@@ -102,7 +102,7 @@ def cpu_baseline(T_sample: int, tau: int, T_mt: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-t", type=int, default=21, help="trace rows T = 2^log_t (N = 8T)")
     ap.add_argument("--tau", type=int, default=8)
@@ -179,7 +179,7 @@ def main():
     # its context busy (prove_async / wait, each proof on the context's own
     # worker thread); the ctypes calls release the GIL
     total = args.steps * K
-    l0_conc = []
+    l0_conc, done_t = [], []
     import threading
     lock = threading.Lock()
     left = [total]  # shared work queue: a context takes the next proof when it is free
@@ -198,6 +198,7 @@ def main():
             ctxs[i].prove_async(roots[i])
             ctxs[i].wait_view()
             l0_conc.append(ctxs[i].stage_times_ms().get("layer0_tree", float("nan")))
+            done_t.append(time.perf_counter())
 
     barrier()
     t0 = time.perf_counter()
@@ -272,6 +273,7 @@ def main():
                        "T": T, "N": N, "tau": args.tau, "b": args.b, "proof_bytes": proof_len,
                        "proofs_in_flight_per_gpu": K,
                        "parallelism": f"replicas x{world}, {K} independent proofs in flight per GPU"},
+            "halves_ms_per_proof": halves(done_t, t0),
             "single_proof": {"value": N * args.steps / dt1, "unit": "field-elements/s",
                              "ms_per_proof": dt1 / args.steps * 1e3,
                              "note": "one proof at a time on one context (rank 0): the latency view; "
@@ -320,6 +322,16 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def halves(done_t, t0):
+    """ms per proof over the first and the second half of the timed proofs
+    (a slow first half would mean the warmup is too short)."""
+    ts = sorted(done_t)
+    if len(ts) < 4:
+        return None
+    h = len(ts) // 2
+    return [(ts[h - 1] - t0) / h * 1e3, (ts[-1] - ts[h - 1]) / (len(ts) - h) * 1e3]
 
 
 def det_vec(n: int, seed: int):

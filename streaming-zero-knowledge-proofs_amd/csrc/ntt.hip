@@ -503,6 +503,34 @@ __global__ void __launch_bounds__(256) k_bitrev_permute(const uint64_t* __restri
   out[dst] = sh[xx * 17 + zz];
 }
 
+// In-place bit-reversal permutation (optionally scaled): the WG of middle bits
+// y also owns tile rev(y) (y <= rev(y)); both 16x16 tiles are read into LDS
+// before either is written, so tile pairs swap without a second buffer.
+__global__ void __launch_bounds__(256) k_bitrev_inplace(uint64_t* __restrict__ a, int logN, uint64_t scale,
+                                                        int do_scale) {
+  __shared__ uint64_t sh[2][16 * 17];
+  const int A = 4, b = logN - 2 * A;
+  const uint32_t y = blockIdx.x;
+  const uint32_t ry = b ? (__brev(y) >> (32 - b)) : 0;
+  if (y > ry) return;
+  const int tid = threadIdx.x;
+  const int x = tid >> 4, z = tid & 15;
+  uint64_t v0 = a[((uint64_t)x << (A + b)) | ((uint64_t)y << A) | z];
+  uint64_t v1 = a[((uint64_t)x << (A + b)) | ((uint64_t)ry << A) | z];
+  if (do_scale) {
+    v0 = gl_mul(v0, scale);
+    v1 = gl_mul(v1, scale);
+  }
+  sh[0][x * 17 + z] = v0;
+  sh[1][x * 17 + z] = v1;
+  __syncthreads();
+  // destination (rz, ry', rx) <- source (rev(rx), y', rev(rz)): tile y lands in tile ry and back
+  const int rz = tid >> 4, rx = tid & 15;
+  const int zz = __brev((uint32_t)rz) >> 28, xx = __brev((uint32_t)rx) >> 28;
+  a[((uint64_t)rz << (A + b)) | ((uint64_t)ry << A) | rx] = sh[0][xx * 17 + zz];
+  if (ry != y) a[((uint64_t)rz << (A + b)) | ((uint64_t)y << A) | rx] = sh[1][xx * 17 + zz];
+}
+
 // Small transforms (logN < 8) fall back to a plain in-LDS pass per call.
 __global__ void k_bitrev_permute_small(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int logN,
                                        uint64_t scale, int do_scale) {
@@ -787,6 +815,12 @@ hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int
   } else {
     hipLaunchKernelGGL(k_bitrev_permute_small, dim3(1), dim3(256), 0, st, in, out, logN, scale, do_scale ? 1 : 0);
   }
+  return hipGetLastError();
+}
+
+hipError_t bitrev_inplace(hipStream_t st, uint64_t* a, int logN, uint64_t scale, bool do_scale) {
+  if (logN < 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bitrev_inplace, dim3(1u << (logN - 8)), dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -1309,8 +1309,12 @@ int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir
     const bool inv = dir < 0;
     if (ntt_dif(st, d, (int)log_n, inv, T) != hipSuccess) return SEZKP_E_DEVICE;
     const uint64_t scale = inv ? hgl_inv((1ULL << log_n) % GL_P_HOST) : 1;
-    if (bitrev_permute(st, d, scratch, (int)log_n, scale, inv) != hipSuccess) return SEZKP_E_DEVICE;
-    if (hipMemcpyAsync(d, scratch, 8ULL << log_n, hipMemcpyDeviceToDevice, st) != hipSuccess) return SEZKP_E_DEVICE;
+    if (log_n >= 8) {
+      if (bitrev_inplace(st, d, (int)log_n, scale, inv) != hipSuccess) return SEZKP_E_DEVICE;
+    } else {
+      if (bitrev_permute(st, d, scratch, (int)log_n, scale, inv) != hipSuccess) return SEZKP_E_DEVICE;
+      if (hipMemcpyAsync(d, scratch, 8ULL << log_n, hipMemcpyDeviceToDevice, st) != hipSuccess) return SEZKP_E_DEVICE;
+    }
     return SEZKP_OK;
   } catch (const Err& e) {
     return e.code;

@@ -65,6 +65,7 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
                    const DeepFuse* deep = nullptr, bool* fused = nullptr, const DeepPoly* dpoly = nullptr);
 hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale,
                           bool do_scale);
+hipError_t bitrev_inplace(hipStream_t st, uint64_t* a, int logN, uint64_t scale, bool do_scale);  // logN >= 8
 // distributed four-step NTT pieces (ntt.hip)
 hipError_t dntt_permute_twiddle(hipStream_t st, const uint64_t* in, uint64_t* out, int logM, const NttTables& T,
                                 uint64_t e_step, bool inverse, bool tw_src, uint64_t scale);
