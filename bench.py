@@ -180,9 +180,12 @@ def main():
     # worker thread); the ctypes calls release the GIL
     total = args.steps * K
     l0_conc, done_t = [], []
+    import gc
     import threading
     lock = threading.Lock()
     left = [total]  # shared work queue: a context takes the next proof when it is free
+    gc.collect()
+    gc.disable()  # no collector pauses in the host threads while proofs are in flight
 
     def take():
         with lock:
@@ -201,6 +204,7 @@ def main():
             done_t.append(time.perf_counter())
 
     barrier()
+    c0 = time.process_time()
     t0 = time.perf_counter()
     workers = [threading.Thread(target=pipeline, args=(i,)) for i in range(K)]
     for w in workers:
@@ -209,6 +213,8 @@ def main():
         w.join()
     barrier()
     dt = time.perf_counter() - t0
+    cpu_frac = (time.process_time() - c0) / dt  # host CPU seconds per wall second (all threads)
+    gc.enable()
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -274,6 +280,8 @@ def main():
                        "proofs_in_flight_per_gpu": K,
                        "parallelism": f"replicas x{world}, {K} independent proofs in flight per GPU"},
             "halves_ms_per_proof": halves(done_t, t0),
+            **({"done_ms": [round((t - t0) * 1e3, 3) for t in sorted(done_t)], "host_cpu_per_wall": cpu_frac}
+               if os.environ.get("SEZKP_BENCH_TIMELINE") else {}),
             "single_proof": {"value": N * args.steps / dt1, "unit": "field-elements/s",
                              "ms_per_proof": dt1 / args.steps * 1e3,
                              "note": "one proof at a time on one context (rank 0): the latency view; "
