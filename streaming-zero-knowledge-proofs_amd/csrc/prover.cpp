@@ -311,7 +311,7 @@ struct sezkp_ctx {
     if (ev_expand) (void)hipEventDestroy(ev_expand);
     if (ev_cols) (void)hipEventDestroy(ev_cols);
     if (st) (void)hipStreamDestroy(st);
-    if (st2) (void)hipStreamDestroy(st2);
+    if (st2 && st2 != st) (void)hipStreamDestroy(st2);
   }
 
   void upload(const sezkp_block_view& v);
@@ -1035,7 +1035,10 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     HIP_OR_THROW(hipSetDevice(device));
     HIP_OR_THROW(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto& e : c->ev) HIP_OR_THROW(hipEventCreate(&e));
-    HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+    // SEZKP_ONE_STREAM=1: the side-stream work runs on the main stream (one
+    // hardware queue per context when many contexts share the GPU)
+    if (getenv("SEZKP_ONE_STREAM")) c->st2 = c->st;
+    else HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));
