@@ -109,6 +109,8 @@ def main():
     ap.add_argument("--b", type=int, default=512)
     ap.add_argument("--stagger-ms", type=float, default=-1.0,
                     help="start offset between the in-flight pipelines (-1 = one proof time / inflight)")
+    ap.add_argument("--pace", type=float, default=0.0,
+                    help="minimum gap between proof starts, in units of the stagger (single proof / inflight)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="independent proofs in flight per GPU (one resident context each, sezkp_ctx_prove_async)")
     ap.add_argument("--cpu-sample-log-t", type=int, default=18)
@@ -156,11 +158,6 @@ def main():
             blocks, mroot = bl, roots[0]
         del bl
     ctx = ctxs[0]
-    for _ in range(max(1, args.warmup)):  # through the workers: threads exist and are warm before timing
-        for c, r in zip(ctxs, roots):
-            c.prove_async(r)
-        for c in ctxs:
-            c.wait_view()
 
     def barrier():
         if dist:
@@ -170,22 +167,26 @@ def main():
     # stagger: context i starts i/K of a proof later, so the K pipelines run
     # different stages (VALU-bound trees beside memory/latency-bound NTT,
     # openings, compose) instead of the same stage at the same time
+    ctx.prove_async(mroot)
+    ctx.wait_view()
     t_s = time.perf_counter()
     ctx.prove_async(mroot)
     ctx.wait_view()
     stagger = (args.stagger_ms * 1e-3 if args.stagger_ms >= 0 else (time.perf_counter() - t_s) / K)
 
-    # timed: steps x K proofs, K in flight: one host thread per context keeps
-    # its context busy (prove_async / wait, each proof on the context's own
-    # worker thread); the ctypes calls release the GIL
+    # timed: steps x K proofs, K in flight: one persistent host thread per
+    # context keeps its context busy (prove_async / wait, each proof on the
+    # context's own worker thread; the ctypes calls release the GIL). The same
+    # threads run the warmup proofs, so no first-call cost of a new thread
+    # lands in the timed region.
     total = args.steps * K
     l0_conc, done_t = [], []
     import gc
     import threading
     lock = threading.Lock()
     left = [total]  # shared work queue: a context takes the next proof when it is free
-    gc.collect()
-    gc.disable()  # no collector pauses in the host threads while proofs are in flight
+    warm = threading.Barrier(K + 1)
+    go = threading.Barrier(K + 1)
 
     def take():
         with lock:
@@ -194,21 +195,44 @@ def main():
             left[0] -= 1
             return True
 
+    # optional start pacing: a proof never starts within `pace` of the
+    # previous start (keeps the contexts out of the same stage)
+    pace = args.pace * stagger
+    last_start = [0.0]
+
+    def paced_start(i):
+        with lock:
+            wait = last_start[0] + pace - time.perf_counter()
+            if wait > 0:
+                time.sleep(wait)
+            last_start[0] = time.perf_counter()
+        ctxs[i].prove_async(roots[i])
+
     def pipeline(i):
+        for _ in range(max(1, args.warmup)):
+            ctxs[i].prove_async(roots[i])
+            ctxs[i].wait_view()
+            ctxs[i].stage_times_ms()
+        warm.wait()
+        go.wait()
         if i and stagger > 0:
             time.sleep(i * stagger)
         while take():
-            ctxs[i].prove_async(roots[i])
+            paced_start(i)
             ctxs[i].wait_view()
             l0_conc.append(ctxs[i].stage_times_ms().get("layer0_tree", float("nan")))
             done_t.append(time.perf_counter())
 
-    barrier()
-    c0 = time.process_time()
-    t0 = time.perf_counter()
     workers = [threading.Thread(target=pipeline, args=(i,)) for i in range(K)]
     for w in workers:
         w.start()
+    warm.wait()
+    gc.collect()
+    gc.disable()  # no collector pauses in the host threads while proofs are in flight
+    barrier()
+    c0 = time.process_time()
+    t0 = time.perf_counter()
+    go.wait()
     for w in workers:
         w.join()
     barrier()

@@ -379,9 +379,23 @@ __global__ void __launch_bounds__(MK_THREADS) k_fold2(const uint64_t* __restrict
 // first tail layer into LDS and replays the fold chain down to its own layer
 // (a few thousand mulmods), so the trees of all small layers are built
 // concurrently instead of as a dependent chain of tiny launches.
-constexpr int TAIL_THREADS = 1024;
+constexpr int TAIL_THREADS = 256;
+// depth-first subtree over 2^LV leaves b[i0 ..] (LDS values), leaf index i0 + j
+template <int LV>
+__device__ __forceinline__ void tail_sub(const uint64_t* b, uint64_t i0, const TreeDev& T, uint32_t (&h)[8]) {
+  if constexpr (LV == 0) {
+    b3_leaf_u64(b[i0], h);
+    store_level(T, 0, i0, h);
+  } else {
+    uint32_t l[8];
+    tail_sub<LV - 1>(b, i0, T, l);
+    tail_sub<LV - 1>(b, i0 + (1ULL << (LV - 1)), T, h);
+    b3_parent(l, h, h);
+    store_level(T, LV, i0 >> LV, h);
+  }
+}
 __global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
-  __shared__ uint64_t buf[2 * TAIL_THREADS * 2];
+  __shared__ uint64_t buf[1 << (TAIL_MAX)];  // the 2^(Ls+1) <= 4096 source values
   __shared__ uint32_t lds[8][TAIL_THREADS];
   const int tid = threadIdx.x;
   const int j = blockIdx.x;
@@ -406,30 +420,22 @@ __global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
   }
   const int len = 1 << L;
   for (int i = tid; i < len; i += TAIL_THREADS) vals[i] = buf[i];
-  int nact, lvl;
-  if (L > 10) {  // 2048 leaves: two per lane
-    uint32_t a[8], b[8], h[8];
-    b3_leaf_u64(buf[2 * tid], a);
-    b3_leaf_u64(buf[2 * tid + 1], b);
-    store_level(T, 0, 2 * tid, a);
-    store_level(T, 0, 2 * tid + 1, b);
-    b3_parent(a, b, h);
-    store_level(T, 1, tid, h);
-    lds_put(lds, tid, h);
-    nact = TAIL_THREADS;
-    lvl = 1;
-  } else {
-    if (tid < len) {
-      uint32_t h[8];
-      b3_leaf_u64(buf[tid], h);
-      store_level(T, 0, tid, h);
-      lds_put(lds, tid, h);
+  // 2^lp leaves per lane (lp <= 3), folded in registers, then LDS levels
+  const int lp = L > 8 ? L - 8 : 0;
+  const int nact = len >> lp;
+  if (tid < nact) {
+    uint32_t h[8];
+    const uint64_t i0 = (uint64_t)tid << lp;
+    switch (lp) {
+      case 0: tail_sub<0>(buf, i0, T, h); break;
+      case 1: tail_sub<1>(buf, i0, T, h); break;
+      case 2: tail_sub<2>(buf, i0, T, h); break;
+      default: tail_sub<3>(buf, i0, T, h); break;
     }
-    nact = len;
-    lvl = 0;
+    lds_put(lds, tid, h);
   }
   __syncthreads();
-  wg_reduce(lds, nact, lvl, 0, T);
+  wg_reduce(lds, nact, lp, 0, T);
 }
 
 // ------------------------------------------------ sharded layout changes
