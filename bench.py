@@ -102,7 +102,7 @@ def cpu_baseline(T_sample: int, tau: int, T_mt: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-t", type=int, default=21, help="trace rows T = 2^log_t (N = 8T)")
     ap.add_argument("--tau", type=int, default=8)
@@ -180,7 +180,8 @@ def main():
     # threads run the warmup proofs, so no first-call cost of a new thread
     # lands in the timed region.
     total = args.steps * K
-    l0_conc, done_t = [], []
+    l0_conc, done_t, per_proof = [], [], []
+    timeline = bool(os.environ.get("SEZKP_BENCH_TIMELINE"))
     import gc
     import threading
     lock = threading.Lock()
@@ -220,8 +221,11 @@ def main():
         while take():
             paced_start(i)
             ctxs[i].wait_view()
-            l0_conc.append(ctxs[i].stage_times_ms().get("layer0_tree", float("nan")))
+            st_i = ctxs[i].stage_times_ms()
+            l0_conc.append(st_i.get("layer0_tree", float("nan")))
             done_t.append(time.perf_counter())
+            if timeline:
+                per_proof.append((i, done_t[-1], st_i))
 
     workers = [threading.Thread(target=pipeline, args=(i,)) for i in range(K)]
     for w in workers:
@@ -304,8 +308,11 @@ def main():
                        "proofs_in_flight_per_gpu": K,
                        "parallelism": f"replicas x{world}, {K} independent proofs in flight per GPU"},
             "halves_ms_per_proof": halves(done_t, t0),
-            **({"done_ms": [round((t - t0) * 1e3, 3) for t in sorted(done_t)], "host_cpu_per_wall": cpu_frac}
-               if os.environ.get("SEZKP_BENCH_TIMELINE") else {}),
+            **({"done_ms": [round((t - t0) * 1e3, 3) for t in sorted(done_t)], "host_cpu_per_wall": cpu_frac,
+                "slowest": [{"ctx": i, "at_ms": round((t - t0) * 1e3, 2),
+                             **{k: round(v, 3) for k, v in st.items()}}
+                            for i, t, st in sorted(per_proof, key=lambda x: -x[2].get("host_wall", 0))[:4]]}
+               if timeline else {}),
             "single_proof": {"value": N * args.steps / dt1, "unit": "field-elements/s",
                              "ms_per_proof": dt1 / args.steps * 1e3,
                              "note": "one proof at a time on one context (rank 0): the latency view; "
