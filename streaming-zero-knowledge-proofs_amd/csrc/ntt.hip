@@ -46,7 +46,9 @@ __device__ __forceinline__ uint64_t dp_load(const NttPassArgs& P, const NttTable
   if ((p & ((1ULL << b) - 1)) == 0) {
     const uint64_t k = p >> b;
     const uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;  // = e
-    v = gl_add(v, gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk)));
+    uint64_t qv = gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk));
+    if (P.coset_e) qv = gl_mul(qv, tw_pow(T, ((uint64_t)rk * P.coset_e) & ((1ULL << T.K) - 1), false));  // (w_N^g)^e
+    v = gl_add(v, qv);
   }
   return v;
 }
@@ -772,7 +774,7 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
                    bool* fused, const DeepPoly* dpoly) {
   if (fused) *fused = false;
   if (logN == 0) return hipSuccess;
-  if (dpoly && (!src || coset_e || logN > 32 || log_src >= logN)) return hipErrorInvalidValue;
+  if (dpoly && (!src || logN > 32 || log_src > logN)) return hipErrorInvalidValue;
   int ms[8], np;
   plan_passes(logN, src ? 3 : 1, ms, &np);
   // DIT order: smallest strides first; ensure the first pass holds >= 3 stages for the LDE skip

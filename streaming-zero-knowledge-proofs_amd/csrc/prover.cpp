@@ -521,10 +521,11 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   const int k = logN;
   const uint64_t S = 1ULL << L16_LOG;
   d_base = dalloc<uint64_t>(n);
-  if (!sharded()) {
+  {  // DEEP quotient tables (sized for this rank's M = N / P LDE points)
+    const uint64_t Ml = N >> logP;
     d_dq_part = dalloc<uint64_t>(n / 4096 + 1);
     d_dq_rlo = dalloc<uint64_t>(4096);
-    d_dq_rhi = dalloc<uint64_t>(N > 4096 ? N >> 12 : 1);
+    d_dq_rhi = dalloc<uint64_t>(Ml > 4096 ? Ml >> 12 : 1);
   }
   M = N >> logP;
   logM = logN - logP;
@@ -757,14 +758,25 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   // evaluations become q(w^j) before the INTT. Not when z^n = 1 (z on the
   // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
   const uint64_t zn = hgl_pow(z, n);
-  const bool dq = !sharded && logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY");
+  const bool dq = logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY");
   DeepPoly dpoly{d_dq_rlo, d_dq_rhi};
   if (dq) {
     const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
     const uint64_t zN = hgl_pow(zn, N / n);
-    const uint64_t K2 = hgl_mul(hgl_pow(z, N - 1), hgl_inv(hgl_sub(hgl_pow(3, N), zN)));  // c' = f(z) K2
-    const uint64_t r = hgl_mul(3, hgl_inv(z));
-    ok(launch_deep_quotient(st, d_base, d_lde, d_dq_part, logn, logN, z, K1, K2, r, hgl_pow(r, 4096), d_dq_rlo,
+    uint64_t K2 = hgl_mul(hgl_pow(z, N - 1), hgl_inv(hgl_sub(hgl_pow(3, N), zN)));  // c' = f(z) K2
+    // rank g evaluates the coset 3 w_N^g <w_M>: H's N coefficients fold to M
+    // (M >= n): h'_k = [k < n] q_k (3 w_N^g)^k + c' G rho^k, rho = (3/z) w_N^g,
+    // G = sum_{t<P} rho^(tM); single device: rho = 3/z, G = 1
+    const uint64_t M_ = N >> logP;
+    const uint64_t rho = hgl_mul(hgl_mul(3, hgl_inv(z)), hgl_pow(hgl_root_2exp((uint32_t)logN), (uint64_t)rank));
+    const uint64_t rhoM = hgl_pow(rho, M_);
+    uint64_t G = 0, pw = 1;
+    for (int t = 0; t < (1 << logP); t++) {
+      G = hgl_add(G, pw);
+      pw = hgl_mul(pw, rhoM);
+    }
+    K2 = hgl_mul(K2, G);
+    ok(launch_deep_quotient(st, d_base, d_lde, d_dq_part, logn, logM, z, K1, K2, rho, hgl_pow(rho, 4096), d_dq_rlo,
                             d_dq_rhi, tw),
        "deep_quotient");
   }
@@ -778,7 +790,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   const DeepFuse dfuse{z, logN, logP, (uint32_t)rank};
   bool deep_fused = dq;
   if (dq)
-    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, 0, nullptr, nullptr, &dpoly), "lde_ntt");
+    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, nullptr, nullptr, &dpoly), "lde_ntt");
   else
     ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused), "lde_ntt");
   rec(6);

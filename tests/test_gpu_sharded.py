@@ -77,6 +77,19 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
         assert calls["alltoall"] == 2 and calls["allreduce"] == 2 and calls["allgather"] > 0
 
 
+def test_sharded_per_point_deep_matches_oracle(gpu_ok, product, oracle, monkeypatch):
+    """SEZKP_NO_DEEP_POLY=1: the sharded ranks divide every coset point by
+    (x_i - z) in the last LDE pass instead of folding the DEEP polynomial
+    (the default); same bytes either way."""
+    monkeypatch.setenv("SEZKP_NO_DEEP_POLY", "1")
+    T, b, tau, seed = 1 << 13, 512, 2, 5
+    blocks = product.synthetic_blocks(T, b, tau, seed)
+    want = hashlib.sha256(oracle.prove_v1(blocks, blocks.manifest_root())).hexdigest()
+    for rank, digest, repeat_ok, _ in _run(2, T, b, tau, seed):
+        assert digest == want, f"rank {rank}: {digest}"
+        assert repeat_ok
+
+
 def test_sharded_context_world1_is_single_gpu(gpu_ok, product, oracle):
     blocks = product.synthetic_blocks(1 << 12, 512, 2, 3)
     root = blocks.manifest_root()
