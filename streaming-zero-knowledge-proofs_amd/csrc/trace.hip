@@ -470,26 +470,14 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
       }
     }
     const uint64_t s_hr = gl_reduce128(hr_lo, hr_hi), s_sl = gl_reduce128(sl_lo, sl_hi);
-    // sum_j alpha_j s_j as an exact 192-bit sum of 128-bit products (lo, hi,
-    // top; at most 7 terms so top < 8), one reduction: 2^128 = -2^32 (mod p)
-    uint64_t a_lo = 0, a_hi = 0;
-    uint32_t a_top = 0;
-    auto madd = [&](uint64_t x, uint64_t y) {
-      uint64_t plo, phi;
-      gl_mul128(x, y, plo, phi);  // phi <= 2^64 - 2: phi + carry cannot wrap
-      uint32_t c1, c2;
-      a_lo = add64c(a_lo, plo, c1);
-      a_hi = add64c(a_hi, phi + c1, c2);
-      a_top += c2;
-    };
-    madd(A.mv_domain, gl_from_i64(s_c2));
-    madd(A.head_update, gl_from_i64(s_c3));
-    madd(A.head_reconstruct, s_hr);
-    madd(A.slack_reconstruct, s_sl);
-    madd(A.sym_reconstruct, (uint64_t)s_sy);
-    if (is_first) madd(A.boundary_first, s_bf);
-    if (is_last) madd(A.boundary_last, s_bl);
-    const uint64_t acc = gl_sub(gl_reduce128(a_lo, a_hi), (uint64_t)a_top << 32);
+    uint64_t acc = 0;
+    if (s_c2) acc = gl_mul(A.mv_domain, gl_from_i64(s_c2));
+    if (s_c3) acc = gl_add(acc, gl_mul(A.head_update, gl_from_i64(s_c3)));
+    if (s_hr) acc = gl_add(acc, gl_mul(A.head_reconstruct, s_hr));
+    if (s_sl) acc = gl_add(acc, gl_mul(A.slack_reconstruct, s_sl));
+    if (s_sy) acc = gl_add(acc, gl_mul(A.sym_reconstruct, (uint64_t)s_sy));
+    if (is_first) acc = gl_add(acc, gl_mul(A.boundary_first, s_bf));
+    if (is_last) acc = gl_add(acc, gl_mul(A.boundary_last, s_bl));
     // mask R(x) = m0 + m1 x + m2 x^2 + m3 x^3 (Horner)
     uint64_t R = gl_add(gl_mul(gl_add(gl_mul(gl_add(gl_mul(m3, x), m2), x), m1), x), m0);
     out[i] = gl_add(acc, R);
