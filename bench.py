@@ -267,9 +267,20 @@ def main():
     barrier()
     t1 = time.perf_counter()
     ctx.upload(blocks)
+    torch.cuda.synchronize()
+    t_up = time.perf_counter() - t1
     ctx.prove(mroot)
     torch.cuda.synchronize()
     t_host = time.perf_counter() - t1
+    # the same from a fresh context (stream, twiddle tables, workspace allocation)
+    t1 = time.perf_counter()
+    cold = ProverContext(dev)
+    cold.upload(blocks)
+    cold.prove(mroot)
+    torch.cuda.synchronize()
+    t_cold = time.perf_counter() - t1
+    cold.close()
+    del cold
 
     if rank == 0:
         ab = alg_bytes(T, args.tau)
@@ -319,8 +330,10 @@ def main():
                                      "stages_ms and roofline come from this pass"},
             "roofline": roof, "ntt_lde": ntt, "whole_prove_hbm": whole, "stages_ms": stages,
             "pcie_inclusive": {"value": N / t_host, "unit": "field-elements/s", "ms": t_host * 1e3,
-                               "note": "rank 0, one proof from blocks in host memory: ctx.upload (HBM "
-                                       "workspace allocation + trace image over PCIe) + prove; not `value`"},
+                               "upload_ms": t_up * 1e3, "fresh_context_ms": t_cold * 1e3,
+                               "note": "rank 0, one proof from blocks in host memory: ctx.upload on a context that "
+                                       "held a trace of this shape (workspace reused, step arrays over PCIe "
+                                       "and transposed on the device) + prove; not `value`"},
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(1 << args.cpu_sample_log_t, args.tau, 1 << args.cpu_mt_log_t)

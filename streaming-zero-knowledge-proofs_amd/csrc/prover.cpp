@@ -158,8 +158,11 @@ struct sezkp_ctx {
   hipStream_t st2 = nullptr;  // side stream: small FRI layers overlap the forest
   hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr;
   NttTables tw{};
-  std::vector<void*> dev_allocs;
-  std::vector<void*> host_allocs;
+  // workspace of the current upload, and the previous upload's blocks kept
+  // for reuse (keyed by byte size): re-uploading a trace of the same shape
+  // allocates nothing. Spares left unclaimed are freed at the end of upload.
+  std::vector<std::pair<void*, size_t>> dev_allocs, host_allocs;
+  std::multimap<size_t, void*> spare_dev, spare_host;
   // shape
   bool loaded = false;
   uint64_t n = 0, N = 0;
@@ -236,26 +239,50 @@ struct sezkp_ctx {
   double host_ms[4]{};
   bool have_times = false;
 
+  static void* take_spare(std::multimap<size_t, void*>& m, size_t bytes) {
+    auto it = m.find(bytes);
+    if (it == m.end()) return nullptr;
+    void* p = it->second;
+    m.erase(it);
+    return p;
+  }
+  // contents are undefined (as hipMalloc's): a reused block holds the previous
+  // upload's data, so every buffer is written before it is read
   template <class Tp>
   Tp* dalloc(size_t count) {
-    void* p = nullptr;
-    HIP_OR_THROW(hipMalloc(&p, count * sizeof(Tp) + 64));
-    dev_allocs.push_back(p);
+    const size_t bytes = count * sizeof(Tp) + 64;
+    void* p = take_spare(spare_dev, bytes);
+    if (!p) HIP_OR_THROW(hipMalloc(&p, bytes));
+    dev_allocs.push_back({p, bytes});
     return static_cast<Tp*>(p);
   }
   template <class Tp>
   Tp* halloc(size_t count) {
-    void* p = nullptr;
-    HIP_OR_THROW(hipHostMalloc(&p, count * sizeof(Tp) + 64, hipHostMallocDefault));
-    host_allocs.push_back(p);
+    const size_t bytes = count * sizeof(Tp) + 64;
+    void* p = take_spare(spare_host, bytes);
+    if (!p) HIP_OR_THROW(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    host_allocs.push_back({p, bytes});
     return static_cast<Tp*>(p);
   }
-  void free_all() {
-    for (void* p : dev_allocs) (void)hipFree(p);
-    for (void* p : host_allocs) (void)hipHostFree(p);
+  // keep = true: the blocks become spares for the next upload
+  void free_all(bool keep = false) {
+    for (auto& a : dev_allocs) {
+      if (keep) spare_dev.emplace(a.second, a.first);
+      else (void)hipFree(a.first);
+    }
+    for (auto& a : host_allocs) {
+      if (keep) spare_host.emplace(a.second, a.first);
+      else (void)hipHostFree(a.first);
+    }
     dev_allocs.clear();
     host_allocs.clear();
     loaded = false;
+  }
+  void release_spares() {
+    for (auto& s : spare_dev) (void)hipFree(s.second);
+    for (auto& s : spare_host) (void)hipHostFree(s.second);
+    spare_dev.clear();
+    spare_host.clear();
   }
   bool busy() {
     if (!async) return false;
@@ -302,7 +329,9 @@ struct sezkp_ctx {
       if (async->th.joinable()) async->th.join();
     }
     if (st) (void)hipStreamSynchronize(st);
+    if (st2) (void)hipStreamSynchronize(st2);
     free_all();
+    release_spares();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     if (st2) (void)hipStreamSynchronize(st2);
@@ -322,7 +351,8 @@ struct sezkp_ctx {
 void sezkp_ctx::upload(const sezkp_block_view& v) {
   HIP_OR_THROW(hipSetDevice(device));
   HIP_OR_THROW(hipStreamSynchronize(st));
-  free_all();
+  if (st2 != st) HIP_OR_THROW(hipStreamSynchronize(st2));
+  free_all(true);
   tau = v.tau;
   nblk = v.n_blocks;
   // rows: sum over blocks of (step_hi - step_lo + 1) (columns.rs:254-257)
@@ -345,17 +375,8 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   ncols = 3 + 7 * (int)tau;
   logChunks = logn > COL_CHUNK_LOG2 ? logn - COL_CHUNK_LOG2 : 0;
 
-  // ---- trace image (tape-major)
-  std::vector<int8_t> mv((size_t)tau * n);
-  std::vector<uint8_t> wf((size_t)tau * n);
-  std::vector<uint16_t> ws((size_t)tau * n);
-  for (uint64_t s = 0; s < n; s++)
-    for (uint32_t r = 0; r < tau; r++) {
-      const size_t i = (size_t)s * tau + r, o = (size_t)r * n + s;
-      mv[o] = v.mv[i];
-      wf[o] = v.has_write[i] ? 1 : 0;
-      ws[o] = v.has_write[i] ? v.wsym[i] : 0;
-    }
+  // ---- trace image (tape-major): the step arrays go over as the view holds
+  // them (row-major [n][tau]) and are transposed on the device
   std::vector<uint64_t> bw((size_t)tau * nblk), bi((size_t)tau * nblk), bo((size_t)tau * nblk);
   for (uint32_t k = 0; k < nblk; k++)
     for (uint32_t r = 0; r < tau; r++) {
@@ -377,10 +398,19 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   uint64_t* d_bw = dalloc<uint64_t>((size_t)tau * nblk);
   uint64_t* d_bi = dalloc<uint64_t>((size_t)tau * nblk);
   uint64_t* d_bo = dalloc<uint64_t>((size_t)tau * nblk);
+  {
+    const size_t cells = (size_t)tau * n;
+    // one staging block: wsym (2-byte aligned first), mv, has_write
+    uint8_t* d_raw = dalloc<uint8_t>(4 * cells);
+    uint16_t* raw_ws = reinterpret_cast<uint16_t*>(d_raw);
+    int8_t* raw_mv = reinterpret_cast<int8_t*>(d_raw + 2 * cells);
+    uint8_t* raw_hw = d_raw + 3 * cells;
+    up(raw_ws, v.wsym, cells);
+    up(raw_mv, v.mv, cells);
+    up(raw_hw, v.has_write, cells);
+    HIP_OR_THROW(launch_trace_image(st, raw_mv, raw_hw, raw_ws, n, tau, d_mv, d_wf, d_ws));
+  }
   up(d_imv, v.input_mv, n);
-  up(d_mv, mv.data(), mv.size());
-  up(d_wf, wf.data(), wf.size());
-  up(d_ws, ws.data(), ws.size());
   up(d_bs, v.step_start, nblk + 1);
   up(d_bw, bw.data(), bw.size());
   up(d_bi, bi.data(), bi.size());
@@ -656,6 +686,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     memcpy(h_proof, w.b.data(), hdr_bytes);
   }
   h_small = halloc<uint32_t>((size_t)(ncols + k + 2) * 8);
+  release_spares();
   loaded = true;
 }
 

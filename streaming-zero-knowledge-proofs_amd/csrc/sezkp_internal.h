@@ -192,6 +192,9 @@ struct ProofLayout {
 
 // kernels launched by the host orchestrator (prover.cpp)
 // blocks [blk_lo, blk_lo + blk_cnt) only (a sharded rank's rows + one row of halo)
+// row-major step arrays [n][tau] -> tape-major trace image [tau][n]
+hipError_t launch_trace_image(hipStream_t st, const int8_t* raw_mv, const uint8_t* raw_hw, const uint16_t* raw_ws,
+                              uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws);
 hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt);
 hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_tab_cols,
                              int n_tab_cols, uint64_t tab_entries, uint32_t* tabs, uint32_t blk_lo, uint32_t blk_cnt);

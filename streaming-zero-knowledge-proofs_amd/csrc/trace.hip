@@ -18,6 +18,29 @@ namespace sezkp {
 
 constexpr int TR_THREADS = 256;
 
+// ------------------------------------------------------------ trace image
+// The block view's step arrays are row-major [n][tau]; the kernels read them
+// tape-major [tau][n]. One lane per row: the lane's tau cells are adjacent on
+// the read side, and a wave's stores to one tape are 64 consecutive cells.
+// wsym is zeroed where has_write is false (the reference reads the
+// symbol only under the flag: `op.write.unwrap_or(0)`, columns.rs:71-72).
+__global__ void __launch_bounds__(TR_THREADS) k_trace_image(const int8_t* __restrict__ raw_mv,
+                                                          const uint8_t* __restrict__ raw_hw,
+                                                          const uint16_t* __restrict__ raw_ws, uint64_t n, int tau,
+                                                          int8_t* __restrict__ mv, uint8_t* __restrict__ wf,
+                                                          uint16_t* __restrict__ ws) {
+  const uint64_t s = (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
+  if (s >= n) return;
+  const size_t i0 = (size_t)s * tau;
+  for (int r = 0; r < tau; r++) {
+    const size_t o = (size_t)r * n + s;
+    const bool w = raw_hw[i0 + r] != 0;
+    mv[o] = raw_mv[i0 + r];
+    wf[o] = w ? 1 : 0;
+    ws[o] = w ? raw_ws[i0 + r] : 0;
+  }
+}
+
 // ------------------------------------------------------------ expansion
 // One workgroup per block: row -> block id, first/last flags, and the
 // post-move head prefix sums per tape (head starts at 0 in every block).
@@ -1147,6 +1170,15 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
 }
 
 // ------------------------------------------------------------------ host
+hipError_t launch_trace_image(hipStream_t st, const int8_t* raw_mv, const uint8_t* raw_hw, const uint16_t* raw_ws,
+                              uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws) {
+  if (n == 0 || tau <= 0) return hipSuccess;
+  const uint64_t g = (n + TR_THREADS - 1) / TR_THREADS;
+  if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_trace_image, dim3((unsigned)g), dim3(TR_THREADS), 0, st, raw_mv, raw_hw, raw_ws, n, tau, mv,
+                     wf, ws);
+  return hipGetLastError();
+}
 hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt) {
   if (blk_cnt == 0) return hipSuccess;
   if ((uint64_t)blk_lo + blk_cnt > T.nblk) return hipErrorInvalidValue;

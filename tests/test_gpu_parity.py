@@ -248,6 +248,30 @@ def test_prove_full_size_config3(gpu_ok, product, oracle):
     assert view.readonly and bytes(view) == art.proof_bytes
 
 
+def test_reupload_reuses_workspace_bit_exact(gpu_ok, product, oracle):
+    """upload() keeps the previous workspace for a trace of the same shape, so
+    every buffer holds the old trace's data when the new proof starts: each
+    proof still equals the oracle's. Shapes alternate so that some blocks are
+    reused and some freshly allocated."""
+    from sezkp_amd._lib import VIEW_FIELDS
+    ctx = product.ProverContext(0)
+    for T, b, tau, seed in [(1 << 14, 512, 4, 1), (1 << 14, 512, 4, 2), (1 << 12, 256, 2, 3),
+                            (1 << 14, 512, 4, 4), (1 << 14, 256, 4, 5)]:
+        blocks = product.synthetic_blocks(T, b, tau, seed)
+        mroot = blocks.manifest_root()
+        want = oracle.prove_v1(blocks, mroot)
+        ctx.upload(blocks)
+        assert ctx.prove(mroot).proof_bytes == want, (T, b, tau, seed)
+    # the device transposition reads has_write as a boolean and ignores wsym
+    # where it is clear (Option<u8> in the reference: columns.rs:71-72)
+    arrays = {f: getattr(blocks, f).copy() for f, _ in VIEW_FIELDS}
+    hw = arrays["has_write"]
+    arrays["has_write"] = np.where(hw != 0, np.uint8(7), np.uint8(0))
+    arrays["wsym"] = np.where(hw != 0, arrays["wsym"], np.uint16(0xBEEF))
+    ctx.upload(product.BlockSoA(blocks.tau, **arrays))
+    assert ctx.prove(mroot).proof_bytes == want
+
+
 def test_streaming_meta_and_verify(gpu_ok, product, oracle):
     """prove_streaming: same bytes, meta gains mode; the host verifier accepts
     proofs of a trace whose AIR holds (non-negative heads) and rejects tampering."""
