@@ -357,7 +357,13 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   nblk = v.n_blocks;
   // rows: sum over blocks of (step_hi - step_lo + 1) (columns.rs:254-257)
   uint64_t rows = 0;
+  // the kernels index the step arrays through step_start: it must start at 0
+  // and every block must hold step_hi - step_lo + 1 >= 1 steps (no wrap-around)
+  if (nblk && v.step_start[0] != 0) throw Err{SEZKP_E_INVALID, "step_start[0] must be 0"};
   for (uint32_t k = 0; k < nblk; k++) {
+    if (v.step_hi[k] < v.step_lo[k] || v.step_hi[k] - v.step_lo[k] >= (1ULL << 28))
+      throw Err{SEZKP_E_INVALID, "block " + std::to_string(k) + ": step range [" + std::to_string(v.step_lo[k]) +
+                                     ", " + std::to_string(v.step_hi[k]) + "] is empty or longer than 2^28"};
     const uint64_t len = v.step_hi[k] - v.step_lo[k] + 1;
     const uint64_t steps = v.step_start[k + 1] - v.step_start[k];
     if (len != steps)

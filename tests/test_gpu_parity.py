@@ -232,6 +232,15 @@ def test_prove_rejects_bad_shapes(gpu_ok, product):
     blocks.step_hi[0] += 1  # step count disagrees with step_lo/step_hi
     with pytest.raises(product.SezkpError):
         product.StarkV1.prove(blocks, bytes(32))
+    # step offsets that would index past the step arrays are refused on the host
+    blocks = product.synthetic_blocks(64, 32, 2)
+    blocks.step_start[:] += 32
+    with pytest.raises(product.SezkpError, match="step_start"):
+        product.StarkV1.prove(blocks, bytes(32))
+    blocks = product.synthetic_blocks(64, 32, 2)
+    blocks.step_hi[1] = blocks.step_lo[1] - 1
+    with pytest.raises(product.SezkpError, match="empty"):
+        product.StarkV1.prove(blocks, bytes(32))
 
 
 def test_prove_full_size_config3(gpu_ok, product, oracle):
