@@ -84,7 +84,9 @@ int32_t sezkp_stark_v1_verify(const uint8_t* proof_bytes, size_t len, const sezk
 
 /* ------------------------------------------------ resident-input context
  * One context = one device + one stream + a workspace sized on upload.
- * upload() builds the device trace image (HBM) from the block view;
+ * upload() builds the device trace image (HBM) from the block view; a
+ * re-upload of a trace with the same shape (n, tau, block boundaries) reuses the
+ * previous workspace and allocates nothing;
  * prove() then runs the whole prover with inputs resident in HBM. */
 typedef struct sezkp_ctx sezkp_ctx;
 sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len);
