@@ -102,8 +102,8 @@ def cpu_baseline(T_sample: int, tau: int, T_mt: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--log-t", type=int, default=21, help="trace rows T = 2^log_t (N = 8T)")
     ap.add_argument("--tau", type=int, default=8)
     ap.add_argument("--b", type=int, default=512)
