@@ -257,6 +257,29 @@ def test_prove_full_size_config3(gpu_ok, product, oracle):
     assert view.readonly and bytes(view) == art.proof_bytes
 
 
+def test_prove_headline_size_matches_openmp_oracle(gpu_ok, product):
+    """The bench workload itself: `sezkp-cli simulate --t 2097152 --b 512
+    --tau 8` blocks (T = 2^21, N = 2^24). The GPU proof equals the OpenMP build
+    of the C oracle byte for byte; the oracle runs in a child process on 16
+    threads (~10 s), so the other tests keep the single-thread build."""
+    import sys
+    T = 1 << 21
+    code = ("import sys; sys.path[:0]=[%r,%r]\n"
+            "import hashlib, oracle_ctypes as O, sezkp_amd as S\n"
+            "O.use_mt(16)\n"
+            "bl=S.reference_blocks(%d,512,8,42); print(hashlib.sha256(O.prove_v1(bl, bl.manifest_root())).hexdigest())\n"
+            % (PKG, os.path.join(ROOT, "oracle"), T))
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    blocks = product.reference_blocks(T, 512, 8, 42)
+    ctx = product.ProverContext(0)
+    ctx.upload(blocks)
+    got = hashlib.sha256(ctx.prove(blocks.manifest_root()).proof_bytes).hexdigest()
+    ctx.close()
+    out, err = child.communicate(timeout=150)
+    assert child.returncode == 0, err[-1500:]
+    assert got == out.strip()
+
+
 def test_reupload_reuses_workspace_bit_exact(gpu_ok, product, oracle):
     """upload() keeps the previous workspace for a trace of the same shape, so
     every buffer holds the old trace's data when the new proof starts: each
