@@ -77,6 +77,27 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
         assert calls["alltoall"] == 2 and calls["allreduce"] == 2 and calls["allgather"] > 0
 
 
+def test_sharded_config5_size_p8_matches_openmp_oracle(gpu_ok, product):
+    """BASELINE config 5's shape: T = 2^22 (N = 2^25), tau = 8, over P = 8
+    ranks (here sharing one GPU through host collectives). Every rank returns
+    the bytes of the OpenMP oracle, run in a child process on 16 threads."""
+    import subprocess
+    from conftest import ROOT
+    T, b, tau, seed = 1 << 22, 512, 8, 5
+    code = ("import sys; sys.path[:0]=[%r,%r]\n"
+            "import hashlib, oracle_ctypes as O, sezkp_amd as S\n"
+            "O.use_mt(16)\n"
+            "bl=S.synthetic_blocks(%d,%d,%d,%d); print(hashlib.sha256(O.prove_v1(bl, bl.manifest_root())).hexdigest())\n"
+            % (PKG, os.path.join(ROOT, "oracle"), T, b, tau, seed))
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    res = _run(8, T, b, tau, seed)
+    out, err = child.communicate(timeout=300)
+    assert child.returncode == 0, err[-1500:]
+    for rank, digest, repeat_ok, calls in res:
+        assert digest == out.strip(), f"rank {rank}: {digest}"
+        assert repeat_ok
+
+
 def test_sharded_per_point_deep_matches_oracle(gpu_ok, product, oracle, monkeypatch):
     """SEZKP_NO_DEEP_POLY=1: the sharded ranks divide every coset point by
     (x_i - z) in the last LDE pass instead of folding the DEEP polynomial
