@@ -58,6 +58,76 @@ def _worker(rank, world, port, log_n, seed, q):
         dist.destroy_process_group()
 
 
+def sampled_spectrum(x: np.ndarray, w_R: int, R: int = 256) -> dict:
+    """X[m n/R] for m < R, exactly, in O(n): X[m n/R] = sum_r w_R^(r m) S_r with
+    S_r = sum of x_j over j = r (mod R) (summed as 32-bit halves, no overflow)."""
+    P = 0xFFFFFFFF00000001
+    n = x.size
+    xr = x.reshape(n // R, R)
+    lo = (xr & np.uint64(0xFFFFFFFF)).sum(axis=0, dtype=np.uint64)
+    hi = (xr >> np.uint64(32)).sum(axis=0, dtype=np.uint64)
+    S = [((int(h) << 32) + int(lo_)) % P for h, lo_ in zip(hi, lo)]
+    wp = [pow(w_R, k, P) for k in range(R)]
+    return {m * (n // R): sum(S[r] * wp[(r * m) % R] for r in range(R)) % P for m in range(R)}
+
+
+def _worker_sampled(rank, world, port, log_n, seed, q):
+    """Config 4 size: the full oracle NTT is too slow at 2^26, so the output
+    is checked at the n/256-spaced frequencies (exact, O(n)) plus the round trip."""
+    sys.path[:0] = [PKG, ORACLE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle_ctypes as orc
+        import sezkp_amd
+        n = 1 << log_n
+        x = orc.det_vec(n, seed)
+        e = np.zeros(256, dtype=np.uint64)
+        e[1] = 1
+        want = sampled_spectrum(x, int(orc.ntt_forward(e)[1]))
+        ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
+        loc = torch.from_numpy(np.ascontiguousarray(x[rank::world]).view(np.int64)).cuda()
+        ctx.dist_ntt(loc)
+        out = loc.cpu().numpy().view(np.uint64)
+        M = n // world
+        Q = M // world
+        seen, fwd_ok = 0, True
+        for i, v in want.items():  # X[i] with i = g Q + q + M k1 sits at k1 Q + q on rank g
+            k1, rem = divmod(i, M)
+            g, qq = divmod(rem, Q)
+            if g == rank:
+                seen += 1
+                fwd_ok = fwd_ok and int(out[k1 * Q + qq]) == v
+        ctx.dist_ntt(loc, inverse=True)
+        inv_ok = np.array_equal(loc.cpu().numpy().view(np.uint64), x[rank::world])
+        ctx.close()
+        q.put((rank, fwd_ok, inv_ok, seen))
+    except Exception as e:
+        q.put((rank, f"ERR {type(e).__name__}: {e}", False, 0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dist_ntt_config4_size_p8(gpu_ok):
+    """BASELINE config 4's shape: 2^26 points over P = 8 ranks."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_sampled, args=(r, 8, port, 26, 2024, q)) for r in range(8)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert sum(r[3] for r in res) == 256  # every sampled frequency was owned by exactly one rank
+    for rank, fwd_ok, inv_ok, _ in res:
+        assert fwd_ok is True, f"rank {rank}: {fwd_ok}"
+        assert inv_ok, f"rank {rank}: inverse did not round-trip"
+
+
 @pytest.mark.parametrize("world,log_n,seed", [(2, 9, 1), (2, 16, 2), (4, 10, 3), (4, 20, 4), (8, 14, 5)])
 def test_dist_ntt_matches_oracle(gpu_ok, world, log_n, seed):
     import torch.multiprocessing as mp
