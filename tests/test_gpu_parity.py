@@ -211,6 +211,30 @@ def test_prove_dictionary_branches_bit_exact(gpu_ok, product, oracle, monkeypatc
     assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
 
 
+def test_prove_random_shapes_one_context(gpu_ok, product, oracle):
+    """64 seeded random traces through ONE resident context (each upload reuses
+    or replaces the previous workspace): T = 2^0..2^14, block length 1..1000,
+    tau 0..8, move ranges from {-1,0,1} up to the whole i8 range, write
+    probability 0..1, symbols from 1 to 16 bits. Every proof equals the oracle's."""
+    rng = np.random.default_rng(2026)
+    ctx = product.ProverContext(0)
+    for case in range(64):
+        T = 1 << int(rng.integers(0, 15))
+        tau = int(rng.integers(0, 9))
+        b = int(rng.integers(1, 1001))
+        mr = int(rng.choice([1, 1, 2, 127]))
+        imv = rng.integers(-mr, mr + 1, T, dtype=np.int8)
+        mv = rng.integers(-mr, mr + 1, (T, tau), dtype=np.int8)
+        hw = (rng.random((T, tau)) < rng.random()).astype(np.uint8)
+        ws = (rng.integers(0, 1 << int(rng.integers(1, 17)), (T, tau)) * hw).astype(np.uint16)
+        blocks = product.partition(imv, mv, hw, ws, b)
+        mroot = rng.bytes(32)
+        ctx.upload(blocks)
+        got = ctx.prove(mroot).proof_bytes
+        assert got == oracle.prove_v1(blocks, mroot), (case, T, b, tau, mr)
+    ctx.close()
+
+
 @pytest.mark.parametrize("T", [16, 1 << 12, 1 << 16])
 def test_prove_deep_paths_bit_exact(gpu_ok, product, oracle, monkeypatch, T):
     """Single device: DEEP as the LDE of q + c*S (DeepPoly, the default) and the
