@@ -11,6 +11,8 @@
 //    (masking.rs:86-103, prover.rs:142-158)
 //  * openings (openings.rs:403-497): value, chunk root, path in chunk, path of
 //    the chunk root in the outer tree.
+#include <type_traits>
+
 #include "dev_common.h"
 #include "sezkp_internal.h"
 
@@ -505,6 +507,117 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
     uint64_t R = gl_add(gl_mul(gl_add(gl_mul(gl_add(gl_mul(m3, x), m2), x), m1), x), m0);
     out[i] = gl_add(acc, R);
   }
+}
+
+// RW adjacent rows per lane (RW = 2 or 4; the same terms as k_compose): the
+// lane's mv / wflag / wsym / head cells of one tape are single 2-8 / 2-8 /
+// 4-8 / 16-32-byte loads, the next row of all but the last comes from the
+// group itself, and the outputs are 16-byte stores. Needs row0 and the row
+// count to be multiples of RW (n >= RW).
+template <int RW>
+__global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, Alphas A, uint64_t m0, uint64_t m1,
+                                                             uint64_t m2, uint64_t m3, NttTables tw, int logn,
+                                                             uint64_t* __restrict__ out, uint64_t row0,
+                                                             uint64_t row_end) {
+  static_assert(RW == 2 || RW == 4, "2 or 4 rows per lane");
+  using Narrow = typename std::conditional<RW == 2, uint16_t, uint32_t>::type;  // RW bytes
+  using Wide = typename std::conditional<RW == 2, uint32_t, uint64_t>::type;    // RW u16
+  const uint64_t n = T.n;
+  const uint64_t i = row0 + RW * ((uint64_t)blockIdx.x * TR_THREADS + threadIdx.x);
+  if (i >= row_end) return;
+  const uint64_t mask_s = (1ULL << tw.S) - 1;
+  const uint64_t e0 = i << (tw.K - logn), e1 = 1ULL << (tw.K - logn);
+  const uint64_t w = gl_mul(tw.hi[e1 >> tw.S], tw.lo[e1 & mask_s]);  // w_n
+  uint64_t x[RW];
+  x[0] = gl_mul(tw.hi[e0 >> tw.S], tw.lo[e0 & mask_s]);  // w_n^i
+#pragma unroll
+  for (int j = 1; j < RW; j++) x[j] = gl_mul(x[j - 1], w);
+  const uint64_t inx = (i + RW) & (n - 1);
+  const Narrow flw = *reinterpret_cast<const Narrow*>(T.row_flags + i);
+  uint32_t blk[RW];
+  bool is_first[RW], is_last[RW];
+#pragma unroll
+  for (int j = 0; j < RW; j += 2) {
+    const uint2 b2 = *reinterpret_cast<const uint2*>(T.row_blk + i + j);
+    blk[j] = b2.x;
+    blk[j + 1] = b2.y;
+  }
+#pragma unroll
+  for (int j = 0; j < RW; j++) {
+    is_first[j] = (flw >> (8 * j)) & 1;
+    is_last[j] = (flw >> (8 * j + 1)) & 1;
+  }
+  int32_t s_c2[RW], s_sy[RW];
+  int64_t s_c3[RW];
+  uint64_t s_bf[RW], s_bl[RW], hr_lo[RW], sl_lo[RW];
+  uint32_t hr_hi[RW], sl_hi[RW];
+#pragma unroll
+  for (int j = 0; j < RW; j++) {
+    s_c2[j] = s_sy[j] = 0;
+    s_c3[j] = 0;
+    s_bf[j] = s_bl[j] = hr_lo[j] = sl_lo[j] = 0;
+    hr_hi[j] = sl_hi[j] = 0;
+  }
+  for (int r = 0; r < T.tau; r++) {
+    const uint64_t o = (uint64_t)r * n;
+    const Narrow mvw = *reinterpret_cast<const Narrow*>(T.mv + o + i);
+    const Narrow wfw = *reinterpret_cast<const Narrow*>(T.wflag + o + i);
+    const Wide wsw = *reinterpret_cast<const Wide*>(T.wsym + o + i);
+    int64_t head[RW + 1];
+#pragma unroll
+    for (int j = 0; j < RW; j += 2) {
+      const longlong2 h2 = *reinterpret_cast<const longlong2*>(T.head + o + i + j);
+      head[j] = h2.x;
+      head[j + 1] = h2.y;
+    }
+    head[RW] = T.head[o + inx];
+    int32_t mv[RW + 1];
+#pragma unroll
+    for (int j = 0; j < RW; j++) mv[j] = (int8_t)((mvw >> (8 * j)) & 0xFF);
+    mv[RW] = T.mv[o + inx];
+#pragma unroll
+    for (int j = 0; j < RW; j++) {
+      const uint64_t head_f = gl_from_i64(head[j]);
+      s_c2[j] += mv[j] * mv[j] * mv[j] - mv[j];
+      if (!is_last[j]) s_c3[j] += head[j + 1] - head[j] - (int64_t)mv[j + 1];
+      if ((wfw >> (8 * j)) & 0xFF) {
+        uint32_t c;
+        hr_lo[j] = add64c(hr_lo[j], head_f & ~0xFFFFULL, c);
+        hr_hi[j] += c;
+        const uint64_t winlen = T.blk_winlen[(uint64_t)r * T.nblk + blk[j]];
+        const uint64_t slack = gl_sub(gl_sub(winlen, 1), head_f);
+        sl_lo[j] = add64c(sl_lo[j], slack & ~0xFFFFULL, c);
+        sl_hi[j] += c;
+        const int32_t sym = (int32_t)((wsw >> (16 * j)) & 0xFFFF);
+        s_sy[j] += sym & ~0xF;
+      }
+      if (is_first[j]) {
+        const uint64_t offin = T.blk_offin[(uint64_t)r * T.nblk + blk[j]];
+        s_bf[j] = gl_add(s_bf[j], gl_sub(gl_sub(head_f, gl_from_i64(mv[j])), offin));
+      }
+      if (is_last[j]) {
+        const uint64_t offout = T.blk_offout[(uint64_t)r * T.nblk + blk[j]];
+        s_bl[j] = gl_add(s_bl[j], gl_sub(head_f, offout));
+      }
+    }
+  }
+  uint64_t res[RW];
+#pragma unroll
+  for (int j = 0; j < RW; j++) {
+    const uint64_t s_hr = gl_reduce128(hr_lo[j], hr_hi[j]), s_sl = gl_reduce128(sl_lo[j], sl_hi[j]);
+    uint64_t acc = 0;
+    if (s_c2[j]) acc = gl_mul(A.mv_domain, gl_from_i64(s_c2[j]));
+    if (s_c3[j]) acc = gl_add(acc, gl_mul(A.head_update, gl_from_i64(s_c3[j])));
+    if (s_hr) acc = gl_add(acc, gl_mul(A.head_reconstruct, s_hr));
+    if (s_sl) acc = gl_add(acc, gl_mul(A.slack_reconstruct, s_sl));
+    if (s_sy[j]) acc = gl_add(acc, gl_mul(A.sym_reconstruct, (uint64_t)s_sy[j]));
+    if (is_first[j]) acc = gl_add(acc, gl_mul(A.boundary_first, s_bf[j]));
+    if (is_last[j]) acc = gl_add(acc, gl_mul(A.boundary_last, s_bl[j]));
+    const uint64_t R = gl_add(gl_mul(gl_add(gl_mul(gl_add(gl_mul(m3, x[j]), m2), x[j]), m1), x[j]), m0);
+    res[j] = gl_add(acc, R);
+  }
+#pragma unroll
+  for (int j = 0; j < RW; j += 2) *reinterpret_cast<ulonglong2*>(out + i + j) = make_ulonglong2(res[j], res[j + 1]);
 }
 
 // ------------------------------------------------ dictionary commitments
@@ -1238,6 +1351,20 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
                           const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows) {
   if (row0 + nrows > T.n) return hipErrorInvalidValue;
+  const char* rw_s = getenv("SEZKP_COMPOSE_ROWS");  // read per launch: tests switch it
+  const int rw_env = rw_s ? atoi(rw_s) : 2;
+  for (int rw : {4, 2}) {  // SEZKP_COMPOSE_ROWS caps the rows per lane (A/B)
+    if (rw > rw_env || T.n < (uint64_t)rw || (row0 | nrows) % rw) continue;
+    const unsigned g = (unsigned)((nrows / rw + TR_THREADS - 1) / TR_THREADS);
+    if (g == 0) return hipSuccess;
+    if (rw == 4)
+      hipLaunchKernelGGL(k_compose_rows<4>, dim3(g), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3],
+                         tw, logn, out, row0, row0 + nrows);
+    else
+      hipLaunchKernelGGL(k_compose_rows<2>, dim3(g), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3],
+                         tw, logn, out, row0, row0 + nrows);
+    return hipGetLastError();
+  }
   const unsigned grid = (unsigned)((nrows + TR_THREADS - 1) / TR_THREADS);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(k_compose, dim3(grid), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3], tw,

@@ -235,6 +235,16 @@ def test_prove_random_shapes_one_context(gpu_ok, product, oracle):
     ctx.close()
 
 
+@pytest.mark.parametrize("rows", ["1", "2", "4"])
+def test_compose_rows_per_lane_bit_exact(gpu_ok, product, oracle, monkeypatch, rows):
+    """The composition kernel with 1, 2 (default) and 4 rows per lane, on a
+    trace with ragged blocks (first/last rows inside a lane's group)."""
+    monkeypatch.setenv("SEZKP_COMPOSE_ROWS", rows)
+    blocks = product.synthetic_blocks(1 << 13, 333, 5, 31)
+    mroot = blocks.manifest_root()
+    assert product.StarkV1.prove(blocks, mroot).proof_bytes == oracle.prove_v1(blocks, mroot)
+
+
 @pytest.mark.parametrize("T", [16, 1 << 12, 1 << 16])
 def test_prove_deep_paths_bit_exact(gpu_ok, product, oracle, monkeypatch, T):
     """Single device: DEEP as the LDE of q + c*S (DeepPoly, the default) and the
