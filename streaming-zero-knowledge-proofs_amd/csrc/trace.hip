@@ -1131,57 +1131,83 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restr
   plans[blockIdx.x] = P;
 }
 
-// table level `lvl` of every dictionary column (grid.y = column)
-__global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __restrict__ tmpl,
-                                                           const DictCol* __restrict__ dcols,
-                                                           const DictPlan* __restrict__ plans,
-                                                           uint32_t* __restrict__ tabs, int lvl) {
-  const DictPlan P = plans[blockIdx.y];
-  if (lvl > P.K) return;
-  uint32_t size = 0, S = 0;  // static indices only (no scratch copy of P)
-#pragma unroll
-  for (int k = 0; k < DICT_LEVELS; k++) {
-    if (k == lvl) size = P.pw[k];
-    if (k + 1 == lvl) S = P.pw[k];
-  }
-  const DictCol dc = dcols[blockIdx.y];
+// entry e of table level `lvl` of one dictionary column
+__device__ __forceinline__ void dict_entry(const ColTemplate& ct, const DictCol& dc, const DictPlan& P, uint32_t S,
+                                           uint32_t* __restrict__ tabs, int lvl, uint32_t e) {
   uint32_t* tl = tabs + 8 * (dc.tab + (uint64_t)lvl * DICT_CAP);
-  const ColTemplate ct = tmpl[dc.col];
+  uint32_t h[8];
   if (lvl == 2 && P.delta) {  // TD: (head code, 3 move codes) -> H(T_1, T_1)
     const uint32_t* t1 = tl - 8 * (uint64_t)DICT_CAP;
     const int64_t R = P.R, dR = P.dR;
-    for (uint32_t e = blockIdx.x * TR_THREADS + threadIdx.x; e < size; e += gridDim.x * TR_THREADS) {
-      int64_t c[4];
-      c[0] = e % R;
-      int64_t rest = e / R;
-      bool ok = true;
+    int64_t c[4];
+    c[0] = e % R;
+    int64_t rest = e / R;
+    bool ok = true;
 #pragma unroll
-      for (int j = 1; j < 4; j++) {
-        c[j] = c[j - 1] + P.dmin + rest % dR;
-        rest /= dR;
-        ok = ok && c[j] >= 0 && c[j] < R;
-      }
-      if (!ok) continue;  // not a reachable group: never read
-      uint32_t a[8], b[8], h[8];
-      node_load(t1 + 8 * (uint64_t)(c[0] + R * c[1]), a);
-      node_load(t1 + 8 * (uint64_t)(c[2] + R * c[3]), b);
-      b3_parent(a, b, h);
-      node_store(tl + 8 * (uint64_t)e, h);
+    for (int j = 1; j < 4; j++) {
+      c[j] = c[j - 1] + P.dmin + rest % dR;
+      rest /= dR;
+      ok = ok && c[j] >= 0 && c[j] < R;
     }
-    return;
+    if (!ok) return;  // not a reachable group: never read
+    uint32_t a[8], b[8];
+    node_load(t1 + 8 * (uint64_t)(c[0] + R * c[1]), a);
+    node_load(t1 + 8 * (uint64_t)(c[2] + R * c[3]), b);
+    b3_parent(a, b, h);
+  } else if (lvl == 0) {
+    leaf_labeled_rt(ct, gl_from_i64(P.min + (int64_t)e), h);
+  } else {
+    const uint32_t* tp = tl - 8 * (uint64_t)DICT_CAP;
+    uint32_t a[8], b[8];
+    node_load(tp + 8 * (uint64_t)(e % S), a);
+    node_load(tp + 8 * (uint64_t)(e / S), b);
+    b3_parent(a, b, h);
   }
-  for (uint32_t e = blockIdx.x * TR_THREADS + threadIdx.x; e < size; e += gridDim.x * TR_THREADS) {
-    uint32_t h[8];
-    if (lvl == 0) {
-      leaf_labeled_rt(ct, gl_from_i64(P.min + (int64_t)e), h);
-    } else {
-      const uint32_t* tp = tl - 8 * (uint64_t)DICT_CAP;
-      uint32_t a[8], b[8];
-      node_load(tp + 8 * (uint64_t)(e % S), a);
-      node_load(tp + 8 * (uint64_t)(e / S), b);
-      b3_parent(a, b, h);
+  node_store(tl + 8 * (uint64_t)e, h);
+}
+
+// Table level `lvl` of every dictionary column in one flat index space: each
+// WG sizes the level per column from the plans (prefix sums in LDS) and
+// grid-strides over all (column, entry) pairs, so a few hundred WGs share the
+// big levels evenly and the empty ones cost one plan scan.
+constexpr int DICT_FLAT_MAX = 1024;  // columns one WG can index
+constexpr int DICT_FLAT_WGS = 2048;  // 8 waves per SIMD for the big levels
+__global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __restrict__ tmpl,
+                                                           const DictCol* __restrict__ dcols,
+                                                           const DictPlan* __restrict__ plans,
+                                                           uint32_t* __restrict__ tabs, int ndict, int lvl) {
+  // columns [0, ndict) of the arrays passed (the host offsets them per chunk)
+  __shared__ uint32_t off[DICT_FLAT_MAX + 1];
+  const int tid = threadIdx.x;
+  for (int c = tid; c < ndict; c += TR_THREADS) {
+    const DictPlan& P = plans[c];
+    uint32_t size = 0;
+#pragma unroll
+    for (int k = 0; k < DICT_LEVELS; k++)  // static indices only (no scratch copy of P)
+      if (k == lvl && lvl <= P.K) size = P.pw[k];
+    off[c + 1] = size;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    off[0] = 0;
+    for (int c = 0; c < ndict; c++) off[c + 1] += off[c];
+  }
+  __syncthreads();
+  const uint32_t total = off[ndict];
+  for (uint32_t g = blockIdx.x * TR_THREADS + tid; g < total; g += gridDim.x * TR_THREADS) {
+    int lo = 0, hi = ndict;  // column c with off[c] <= g < off[c + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (off[mid] <= g) lo = mid;
+      else hi = mid;
     }
-    node_store(tl + 8 * (uint64_t)e, h);
+    const DictPlan P = plans[lo];
+    uint32_t S = 0;
+#pragma unroll
+    for (int k = 0; k + 1 < DICT_LEVELS; k++)
+      if (k + 1 == lvl) S = P.pw[k];
+    const DictCol dc = dcols[lo];
+    dict_entry(tmpl[dc.col], dc, P, S, tabs, lvl, g - off[lo]);
   }
 }
 
@@ -1321,10 +1347,14 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
   hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_dcols, d_plans);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   for (int l = 0; l < DICT_LEVELS; l++) {
-    // grid-stride: most (column, level) pairs are empty or tiny; 64 WGs per
-    // column still spread a full 65536-entry level over every CU
-    hipLaunchKernelGGL(k_dict_level, dim3(64, ndict), dim3(TR_THREADS), 0, st, d_tmpl, d_dcols, d_plans, d_dtabs, l);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // one flat launch per level (and per DICT_FLAT_MAX columns): all WGs
+    // share every column's entries
+    for (int c0 = 0; c0 < ndict; c0 += DICT_FLAT_MAX) {
+      const int nc = ndict - c0 < DICT_FLAT_MAX ? ndict - c0 : DICT_FLAT_MAX;
+      hipLaunchKernelGGL(k_dict_level, dim3(DICT_FLAT_WGS), dim3(TR_THREADS), 0, st, d_tmpl, d_dcols + c0,
+                         d_plans + c0, d_dtabs, nc, l);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
   }
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
   hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
