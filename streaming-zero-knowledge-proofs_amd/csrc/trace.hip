@@ -47,7 +47,6 @@ __global__ void __launch_bounds__(TR_THREADS) k_trace_image(const int8_t* __rest
 // One workgroup per block: row -> block id, first/last flags, and the
 // post-move head prefix sums per tape (head starts at 0 in every block).
 __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) {
-  __shared__ int32_t wsum[TR_THREADS / 64];
   const uint32_t b = b0 + blockIdx.x;
   const uint64_t s = T.blk_start[b], e = T.blk_start[b + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -55,34 +54,41 @@ __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) 
     T.row_blk[r] = b;
     T.row_flags[r] = (uint8_t)((r == s ? 1 : 0) | (r + 1 == e ? 2 : 0));
   }
-  // head = block-local inclusive prefix sum of the tape's moves; two rows per
-  // lane, 32-bit scan (|sum| <= 128 * rows per iteration), 64-bit carry
-  for (int tp = 0; tp < T.tau; tp++) {
+  // head = block-local inclusive prefix sum of the tape's moves. One wave per
+  // tape (no WG barriers): two rows per lane, 32-bit wave scan (|sum| <= 128
+  // rows * 128), 64-bit carry from lane 63.
+  for (int tp = wave; tp < T.tau; tp += TR_THREADS / 64) {
     const int8_t* mv = T.mv + (uint64_t)tp * T.n;
     int64_t* hd = T.head + (uint64_t)tp * T.n;
     int64_t carry = 0;
-    for (uint64_t r0 = s; r0 < e; r0 += 2 * TR_THREADS) {
-      const uint64_t r = r0 + 2 * (uint64_t)tid;
-      const int32_t m0 = r < e ? (int32_t)mv[r] : 0, m1 = r + 1 < e ? (int32_t)mv[r + 1] : 0;
+    // even block start (n is even): a lane's row pair is one 2-byte load and
+    // one 16-byte store
+    const bool paired = (s & 1) == 0;
+    for (uint64_t r0 = s; r0 < e; r0 += 128) {
+      const uint64_t r = r0 + 2 * (uint64_t)lane;
+      int32_t m0 = 0, m1 = 0;
+      if (paired && r + 1 < e) {
+        const uint16_t w = *reinterpret_cast<const uint16_t*>(mv + r);
+        m0 = (int8_t)(w & 0xFF);
+        m1 = (int8_t)(w >> 8);
+      } else {
+        m0 = r < e ? (int32_t)mv[r] : 0;
+        m1 = r + 1 < e ? (int32_t)mv[r + 1] : 0;
+      }
       int32_t x = m0 + m1;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const int32_t y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
       }
-      if (lane == 63) wsum[wave] = x;
-      __syncthreads();
-      int32_t pre = 0, tot = 0;
-#pragma unroll
-      for (int w = 0; w < TR_THREADS / 64; w++) {
-        if (w < wave) pre += wsum[w];
-        tot += wsum[w];
+      const int64_t h1 = carry + (int64_t)x;  // through row r + 1
+      if (paired && r + 1 < e) {
+        *reinterpret_cast<longlong2*>(hd + r) = make_longlong2(h1 - m1, h1);
+      } else {
+        if (r < e) hd[r] = h1 - m1;
+        if (r + 1 < e) hd[r + 1] = h1;
       }
-      const int64_t h1 = carry + (int64_t)(pre + x);  // through row r + 1
-      if (r < e) hd[r] = h1 - m1;
-      if (r + 1 < e) hd[r + 1] = h1;
-      carry += tot;
-      __syncthreads();
+      carry += __shfl(x, 63, 64);
     }
   }
 }
