@@ -373,6 +373,37 @@ __global__ void __launch_bounds__(MK_THREADS) k_fold2(const uint64_t* __restrict
   *reinterpret_cast<ulonglong2*>(out2 + i) = make_ulonglong2(gl_add(y0, gl_mul(b2, z0)), gl_add(y1, gl_mul(b2, z1)));
 }
 
+// F folds per pass (F = 2..4): layer r + m (m = 1..F) at index i + j L, j <
+// 2^(F-m), L = len(layer r + F), is y_m = y_{m-1}[i + j L] + b_m
+// y_{m-1}[i + (j + 2^(F-m)) L]; a lane holds two adjacent i, reads its 2^F
+// strided pairs of layer r once and writes every intermediate layer once.
+template <int F>
+__global__ void __launch_bounds__(MK_THREADS) k_foldm(const uint64_t* __restrict__ in, FoldOuts O, int logLenF) {
+  constexpr int W = 1 << F;
+  const uint64_t L = 1ULL << logLenF;
+  const uint64_t i = ((uint64_t)blockIdx.x * MK_THREADS + threadIdx.x) * 2;
+  if (i >= L) return;
+  uint64_t x0[W], x1[W];
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(in + i + (uint64_t)j * L);
+    x0[j] = v.x;
+    x1[j] = v.y;
+  }
+#pragma unroll
+  for (int m = 1; m <= F; m++) {
+    const int half = W >> m;
+    const uint64_t b = O.beta[m - 1];
+    uint64_t* out = O.out[m - 1];
+#pragma unroll
+    for (int j = 0; j < half; j++) {
+      x0[j] = gl_add(x0[j], gl_mul(b, x0[j + half]));
+      x1[j] = gl_add(x1[j], gl_mul(b, x1[j + half]));
+      *reinterpret_cast<ulonglong2*>(out + i + (uint64_t)j * L) = make_ulonglong2(x0[j], x1[j]);
+    }
+  }
+}
+
 // ------------------------------------------------------ small FRI layers
 // All fold layers of <= 2048 leaves in one launch: WG j produces layer
 // logLen = Ls - j. Each WG reloads the (<= 4096-element) layer above the
@@ -619,6 +650,18 @@ hipError_t launch_fold2(hipStream_t st, const uint64_t* in, uint64_t* out1, uint
   const uint64_t per = (uint64_t)MK_THREADS * 2;
   const unsigned grid = (unsigned)(((1ULL << logLen2) + per - 1) / per);
   hipLaunchKernelGGL(k_fold2, dim3(grid), dim3(MK_THREADS), 0, st, in, out1, out2, logLen2, b1, b2);
+  return hipGetLastError();
+}
+
+hipError_t launch_foldm(hipStream_t st, const uint64_t* in, const FoldOuts& outs, int F, int logLenF) {
+  if (logLenF < 1 || F < 2 || F > FOLD_MAX) return hipErrorInvalidValue;
+  const uint64_t per = (uint64_t)MK_THREADS * 2;
+  const unsigned grid = (unsigned)(((1ULL << logLenF) + per - 1) / per);
+  switch (F) {
+    case 2: hipLaunchKernelGGL(k_foldm<2>, dim3(grid), dim3(MK_THREADS), 0, st, in, outs, logLenF); break;
+    case 3: hipLaunchKernelGGL(k_foldm<3>, dim3(grid), dim3(MK_THREADS), 0, st, in, outs, logLenF); break;
+    default: hipLaunchKernelGGL(k_foldm<4>, dim3(grid), dim3(MK_THREADS), 0, st, in, outs, logLenF); break;
+  }
   return hipGetLastError();
 }
 

@@ -881,11 +881,18 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     ok(launch_fri_tail(st2, ta), "fri_tail");
     HIP_OR_THROW(hipEventRecord(ev_tail, st2));
   };
-  for (int r = 0; r < rR;) {  // fold chain, two layers per pass where possible
-    if (r + 1 < rR) {
-      ok(launch_fold2(st, lvals[r], lvals[r + 1], lvals[r + 2], ltrees[r + 2].logLen, beta_of(r), beta_of(r + 1)),
-         "fri_fold2");
-      r += 2;
+  static const int fold_max = getenv("SEZKP_FOLD_MAX") ? std::max(2, std::min(FOLD_MAX, atoi(getenv("SEZKP_FOLD_MAX"))))
+                                                      : FOLD_MAX;
+  for (int r = 0; r < rR;) {  // fold chain, up to fold_max layers per pass
+    const int F = std::min(fold_max, rR - r);
+    if (F >= 2) {
+      FoldOuts fo{};
+      for (int m = 1; m <= F; m++) {
+        fo.out[m - 1] = lvals[r + m];
+        fo.beta[m - 1] = beta_of(r + m - 1);
+      }
+      ok(launch_foldm(st, lvals[r], fo, F, ltrees[r + F].logLen), "fri_foldm");
+      r += F;
     } else {
       ok(launch_fold(st, lvals[r], lvals[r + 1], ltrees[r + 1].logLen, beta_of(r)), "fri_fold");
       r += 1;
