@@ -354,25 +354,6 @@ __global__ void __launch_bounds__(MK_THREADS) k_fold(const uint64_t* __restrict_
   o[1] = make_ulonglong2(gl_add(a1.x, gl_mul(beta, b1.x)), gl_add(a1.y, gl_mul(beta, b1.y)));
 }
 
-// Two folds per pass: y1[j] = y0[j] + b1 y0[j + 2L], y2[i] = y1[i] + b2 y1[i + L]
-// (L = len(y2)); writes y1 and y2, reads y0 once (4L reads, 3L writes).
-__global__ void __launch_bounds__(MK_THREADS) k_fold2(const uint64_t* __restrict__ in, uint64_t* __restrict__ out1,
-                                                      uint64_t* __restrict__ out2, int logLen2, uint64_t b1,
-                                                      uint64_t b2) {
-  const uint64_t L = 1ULL << logLen2;
-  const uint64_t i = ((uint64_t)blockIdx.x * MK_THREADS + threadIdx.x) * 2;
-  if (i >= L) return;
-  const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(in + i);
-  const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(in + i + L);
-  const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(in + i + 2 * L);
-  const ulonglong2 d = *reinterpret_cast<const ulonglong2*>(in + i + 3 * L);
-  const uint64_t y0 = gl_add(a.x, gl_mul(b1, c.x)), y1 = gl_add(a.y, gl_mul(b1, c.y));
-  const uint64_t z0 = gl_add(b.x, gl_mul(b1, d.x)), z1 = gl_add(b.y, gl_mul(b1, d.y));
-  *reinterpret_cast<ulonglong2*>(out1 + i) = make_ulonglong2(y0, y1);
-  *reinterpret_cast<ulonglong2*>(out1 + i + L) = make_ulonglong2(z0, z1);
-  *reinterpret_cast<ulonglong2*>(out2 + i) = make_ulonglong2(gl_add(y0, gl_mul(b2, z0)), gl_add(y1, gl_mul(b2, z1)));
-}
-
 // F folds per pass (F = 2..4): layer r + m (m = 1..F) at index i + j L, j <
 // 2^(F-m), L = len(layer r + F), is y_m = y_{m-1}[i + j L] + b_m
 // y_{m-1}[i + (j + 2^(F-m)) L]; a lane holds two adjacent i, reads its 2^F
@@ -641,15 +622,6 @@ hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int lo
   const uint64_t per = (uint64_t)MK_THREADS * 4;
   const unsigned grid = (unsigned)(((1ULL << logLen) + per - 1) / per);
   hipLaunchKernelGGL(k_fold, dim3(grid), dim3(MK_THREADS), 0, st, in, out, logLen, beta);
-  return hipGetLastError();
-}
-
-hipError_t launch_fold2(hipStream_t st, const uint64_t* in, uint64_t* out1, uint64_t* out2, int logLen2, uint64_t b1,
-                        uint64_t b2) {
-  if (logLen2 < 1) return hipErrorInvalidValue;
-  const uint64_t per = (uint64_t)MK_THREADS * 2;
-  const unsigned grid = (unsigned)(((1ULL << logLen2) + per - 1) / per);
-  hipLaunchKernelGGL(k_fold2, dim3(grid), dim3(MK_THREADS), 0, st, in, out1, out2, logLen2, b1, b2);
   return hipGetLastError();
 }
 

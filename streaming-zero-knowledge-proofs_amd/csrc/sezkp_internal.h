@@ -253,7 +253,6 @@ hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals
                           TreeDev tree, int stop = L16_LOG);
 // Fold chain kernel (values only) and the one-launch forest of layer trees.
 hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta);
-// two consecutive folds in one pass; logLen2 = log2 of the second output
 // F = 2..FOLD_MAX folds in one pass (k_foldm): out[m-1] = layer r + m, beta[m-1] its challenge
 constexpr int FOLD_MAX = 4;
 struct FoldOuts {
@@ -261,8 +260,6 @@ struct FoldOuts {
   uint64_t beta[FOLD_MAX];
 };
 hipError_t launch_foldm(hipStream_t st, const uint64_t* in, const FoldOuts& outs, int F, int logLenF);
-hipError_t launch_fold2(hipStream_t st, const uint64_t* in, uint64_t* out1, uint64_t* out2, int logLen2, uint64_t b1,
-                        uint64_t b2);
 struct ForestLayer {
   const uint64_t* vals;
   TreeDev tree;
