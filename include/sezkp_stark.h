@@ -94,6 +94,21 @@ void sezkp_ctx_destroy(sezkp_ctx* ctx);
 int32_t sezkp_ctx_upload(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len);
 int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, sezkp_buf* proof_bytes,
                         char* err, size_t err_len);
+/* Pipelined upload of the NEXT trace: same shape as the uploaded one (tau,
+ * block count and block boundaries; the values may all differ). The block
+ * tables and step arrays go over PCIe on the context's copy stream into a
+ * second (spare) trace image and the call returns at once; the next prove on
+ * this context switches to it, its kernels waiting for the copy on the
+ * device. Allowed while a proof is in flight on the context (that is the
+ * point: the upload of proof i+1 overlaps proof i). The view's arrays must
+ * stay valid and unchanged until that prove has started; from pinned or
+ * registered memory (sezkp_host_register) the copies are DMA. A trace of
+ * another shape: SEZKP_E_INVALID (use sezkp_ctx_upload). */
+int32_t sezkp_ctx_stage(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len);
+/* Page-lock (hipHostRegister) / release caller memory, e.g. the SoA arrays a
+ * ProvingBackend shim fills from &[BlockSummary], so staging copies are DMA. */
+int32_t sezkp_host_register(void* p, size_t bytes);
+int32_t sezkp_host_unregister(void* p);
 /* Same proof, borrowed: *data points into the context's pinned host buffer
  * (valid until the next prove/upload/destroy of this context); no copy. */
 int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags,

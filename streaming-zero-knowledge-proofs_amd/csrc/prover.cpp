@@ -156,7 +156,26 @@ struct sezkp_ctx {
   std::unique_ptr<AsyncSlot> async;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // side stream: small FRI layers overlap the forest
+  hipStream_t stc = nullptr;  // copy stream: staged uploads (sezkp_ctx_stage)
   hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr;
+  // Trace images, double-buffered: slot[active] feeds the proofs; stage()
+  // fills slot[1 - active] on the copy stream while a proof runs, and the
+  // next prove() switches to it (its kernels wait for the copy on the device).
+  struct TraceSlot {
+    int8_t* imv = nullptr;
+    int8_t* mv = nullptr;
+    uint8_t* wf = nullptr;
+    uint16_t* ws = nullptr;
+    uint64_t *bw = nullptr, *bi = nullptr, *bo = nullptr;
+    uint8_t* raw = nullptr;     // step arrays as the view holds them (row-major), before k_trace_image
+    uint64_t* h_tab = nullptr;  // pinned staging of bw | bi | bo
+    hipEvent_t ready = nullptr;
+  };
+  TraceSlot slot[2];
+  int active = 0;
+  bool staged = false;       // slot[1 - active] holds a staged trace not yet proved
+  std::mutex stage_mu;
+  std::vector<uint64_t> cur_step_start;  // shape of the uploaded trace (block boundaries)
   NttTables tw{};
   // workspace of the current upload, and the previous upload's blocks kept
   // for reuse (keyed by byte size): re-uploading a trace of the same shape
@@ -330,6 +349,7 @@ struct sezkp_ctx {
     }
     if (st) (void)hipStreamSynchronize(st);
     if (st2) (void)hipStreamSynchronize(st2);
+    if (stc) (void)hipStreamSynchronize(stc);
     free_all();
     release_spares();
     for (auto& e : ev)
@@ -339,11 +359,22 @@ struct sezkp_ctx {
     if (ev_tail) (void)hipEventDestroy(ev_tail);
     if (ev_expand) (void)hipEventDestroy(ev_expand);
     if (ev_cols) (void)hipEventDestroy(ev_cols);
+    if (stc) (void)hipStreamSynchronize(stc);
+    for (auto& sl : slot)
+      if (sl.ready) (void)hipEventDestroy(sl.ready);
     if (st) (void)hipStreamDestroy(st);
     if (st2 && st2 != st) (void)hipStreamDestroy(st2);
+    if (stc) (void)hipStreamDestroy(stc);
   }
 
   void upload(const sezkp_block_view& v);
+  // stage the next trace (same shape) into the spare slot on the copy stream
+  void stage(const sezkp_block_view& v);
+  void alloc_slot(TraceSlot& t);
+  // block tables + step arrays of `v` into slot t, async on stream s
+  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s);
+  void check_shape_same(const sezkp_block_view& v) const;
+  void take_staged();
   // proves into the pinned staging buffer; returns its size (bytes at h_proof)
   size_t prove(const uint8_t root[32]);
 };
@@ -383,55 +414,34 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
 
   // ---- trace image (tape-major): the step arrays go over as the view holds
   // them (row-major [n][tau]) and are transposed on the device
-  std::vector<uint64_t> bw((size_t)tau * nblk), bi((size_t)tau * nblk), bo((size_t)tau * nblk);
-  for (uint32_t k = 0; k < nblk; k++)
-    for (uint32_t r = 0; r < tau; r++) {
-      const size_t i = (size_t)k * tau + r, o = (size_t)r * nblk + k;
-      const int64_t d = v.win_right[i] - v.win_left[i];
-      const uint64_t wl = (d < 0 ? 0 - (uint64_t)d : (uint64_t)d) + 1;  // openings.rs:217
-      bw[o] = wl % GL_P_HOST;
-      bi[o] = v.off_in[i];
-      bo[o] = v.off_out[i];
-    }
   auto up = [&](auto* dst, const auto* src, size_t count) {
     if (count) HIP_OR_THROW(hipMemcpy(dst, src, count * sizeof(*src), hipMemcpyHostToDevice));
   };
-  int8_t* d_imv = dalloc<int8_t>(n);
-  int8_t* d_mv = dalloc<int8_t>((size_t)tau * n);
-  uint8_t* d_wf = dalloc<uint8_t>((size_t)tau * n);
-  uint16_t* d_ws = dalloc<uint16_t>((size_t)tau * n);
-  uint64_t* d_bs = dalloc<uint64_t>(nblk + 1);
-  uint64_t* d_bw = dalloc<uint64_t>((size_t)tau * nblk);
-  uint64_t* d_bi = dalloc<uint64_t>((size_t)tau * nblk);
-  uint64_t* d_bo = dalloc<uint64_t>((size_t)tau * nblk);
+  staged = false;
+  active = 0;
   {
-    const size_t cells = (size_t)tau * n;
-    // one staging block: wsym (2-byte aligned first), mv, has_write
-    uint8_t* d_raw = dalloc<uint8_t>(4 * cells);
-    uint16_t* raw_ws = reinterpret_cast<uint16_t*>(d_raw);
-    int8_t* raw_mv = reinterpret_cast<int8_t*>(d_raw + 2 * cells);
-    uint8_t* raw_hw = d_raw + 3 * cells;
-    up(raw_ws, v.wsym, cells);
-    up(raw_mv, v.mv, cells);
-    up(raw_hw, v.has_write, cells);
-    HIP_OR_THROW(launch_trace_image(st, raw_mv, raw_hw, raw_ws, n, tau, d_mv, d_wf, d_ws));
+    hipEvent_t keep = slot[1].ready;
+    slot[1] = TraceSlot{};
+    slot[1].ready = keep;
   }
-  up(d_imv, v.input_mv, n);
+  alloc_slot(slot[0]);
+  uint64_t* d_bs = dalloc<uint64_t>(nblk + 1);
   up(d_bs, v.step_start, nblk + 1);
-  up(d_bw, bw.data(), bw.size());
-  up(d_bi, bi.data(), bi.size());
-  up(d_bo, bo.data(), bo.size());
+  cur_step_start.assign(v.step_start, v.step_start + nblk + 1);
+  write_trace(slot[0], v, st);
+  HIP_OR_THROW(hipStreamSynchronize(st));
+  TraceSlot& t0 = slot[0];
   T.n = n;
   T.tau = (int)tau;
   T.nblk = nblk;
-  T.input_mv = d_imv;
-  T.mv = d_mv;
-  T.wflag = d_wf;
-  T.wsym = d_ws;
+  T.input_mv = t0.imv;
+  T.mv = t0.mv;
+  T.wflag = t0.wf;
+  T.wsym = t0.ws;
   T.blk_start = d_bs;
-  T.blk_winlen = d_bw;
-  T.blk_offin = d_bi;
-  T.blk_offout = d_bo;
+  T.blk_winlen = t0.bw;
+  T.blk_offin = t0.bi;
+  T.blk_offout = t0.bo;
   T.row_blk = dalloc<uint32_t>(n);
   T.row_flags = dalloc<uint8_t>(n);
   T.head = dalloc<int64_t>((size_t)tau * n + 1);
@@ -518,8 +528,8 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   }
   d_tmpl = dalloc<ColTemplate>(ncols);
   up(d_tmpl, tm.data(), tm.size());
-  d_err = dalloc<uint32_t>(4);
-  HIP_OR_THROW(hipMemset(d_err, 0, 16));
+  d_err = dalloc<uint32_t>(16);  // [0] this rank's guard, [8 + r] rank r's (sharded)
+  HIP_OR_THROW(hipMemset(d_err, 0, 64));
   d_tabs = dalloc<uint32_t>(tab_nodes * 8 + 8);
   n_tab_cols = (int)tab_cols.size();
   d_tab_cols = dalloc<uint32_t>(tab_cols.size() + 1);
@@ -696,8 +706,97 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   loaded = true;
 }
 
+void sezkp_ctx::alloc_slot(TraceSlot& t) {
+  const size_t cells = (size_t)tau * n, nt = (size_t)tau * nblk;
+  t.imv = dalloc<int8_t>(n);
+  t.mv = dalloc<int8_t>(cells);
+  t.wf = dalloc<uint8_t>(cells);
+  t.ws = dalloc<uint16_t>(cells);
+  t.bw = dalloc<uint64_t>(3 * nt + 1);  // bw | bi | bo, one copy
+  t.bi = t.bw + nt;
+  t.bo = t.bi + nt;
+  t.raw = dalloc<uint8_t>(4 * cells);  // wsym (2-byte aligned first), mv, has_write
+  t.h_tab = halloc<uint64_t>(3 * nt + 1);
+  if (!t.ready) HIP_OR_THROW(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
+}
+
+// Per-block tables on the host (window lengths, head offsets: tau * n_blocks
+// values), then every array over PCIe asynchronously on `s` and the row-major
+// step arrays transposed to the tape-major image on the device.
+void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s) {
+  const size_t cells = (size_t)tau * n, nt = (size_t)tau * nblk;
+  // the previous copy out of h_tab (an earlier stage into this slot) must be done
+  HIP_OR_THROW(hipEventSynchronize(t.ready));
+  for (uint32_t k = 0; k < nblk; k++)
+    for (uint32_t r = 0; r < tau; r++) {
+      const size_t i = (size_t)k * tau + r, o = (size_t)r * nblk + k;
+      const int64_t d = v.win_right[i] - v.win_left[i];
+      const uint64_t wl = (d < 0 ? 0 - (uint64_t)d : (uint64_t)d) + 1;  // openings.rs:217
+      t.h_tab[o] = wl % GL_P_HOST;
+      t.h_tab[nt + o] = v.off_in[i];
+      t.h_tab[2 * nt + o] = v.off_out[i];
+    }
+  auto cp = [&](void* dst, const void* src, size_t bytes) {
+    if (bytes) HIP_OR_THROW(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+  };
+  uint16_t* raw_ws = reinterpret_cast<uint16_t*>(t.raw);
+  int8_t* raw_mv = reinterpret_cast<int8_t*>(t.raw + 2 * cells);
+  uint8_t* raw_hw = t.raw + 3 * cells;
+  cp(raw_ws, v.wsym, cells * 2);
+  cp(raw_mv, v.mv, cells);
+  cp(raw_hw, v.has_write, cells);
+  cp(t.imv, v.input_mv, n);
+  cp(t.bw, t.h_tab, 3 * nt * 8);
+  HIP_OR_THROW(launch_trace_image(s, raw_mv, raw_hw, raw_ws, n, tau, t.mv, t.wf, t.ws));
+  HIP_OR_THROW(hipEventRecord(t.ready, s));
+}
+
+void sezkp_ctx::check_shape_same(const sezkp_block_view& v) const {
+  if (v.tau != tau || v.n_blocks != nblk)
+    throw Err{SEZKP_E_INVALID, "staged trace has another shape (tau / block count): call sezkp_ctx_upload"};
+  if (nblk && memcmp(v.step_start, cur_step_start.data(), (size_t)(nblk + 1) * 8) != 0)
+    throw Err{SEZKP_E_INVALID, "staged trace has other block boundaries: call sezkp_ctx_upload"};
+  for (uint32_t k = 0; k < nblk; k++)  // the checks of upload()
+    if (v.step_hi[k] < v.step_lo[k] || v.step_hi[k] - v.step_lo[k] + 1 != v.step_start[k + 1] - v.step_start[k])
+      throw Err{SEZKP_E_INVALID, "block " + std::to_string(k) + ": step range does not match its steps"};
+}
+
+void sezkp_ctx::stage(const sezkp_block_view& v) {
+  if (!loaded) throw Err{SEZKP_E_INVALID, "no trace uploaded: the first trace of a shape goes through upload"};
+  check_shape_same(v);
+  HIP_OR_THROW(hipSetDevice(device));
+  std::lock_guard<std::mutex> lk(stage_mu);
+  TraceSlot& t = slot[1 - active];
+  if (!t.imv) alloc_slot(t);  // first stage on this workspace: the spare image
+  staged = false;             // (re)filling the spare slot
+  write_trace(t, v, stc);
+  staged = true;
+}
+
+// Switch to a staged trace image (the device waits for its copy). Called by
+// the thread that starts a proof (sezkp_ctx_prove_async calls it before
+// handing the proof to the worker, so a stage() right after it fills the
+// other slot, never the one this proof reads).
+void sezkp_ctx::take_staged() {
+  std::lock_guard<std::mutex> lk(stage_mu);
+  if (staged) {
+    active = 1 - active;
+    staged = false;
+    const TraceSlot& t = slot[active];
+    T.input_mv = t.imv;
+    T.mv = t.mv;
+    T.wflag = t.wf;
+    T.wsym = t.ws;
+    T.blk_winlen = t.bw;
+    T.blk_offin = t.bi;
+    T.blk_offout = t.bo;
+    HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
+  }
+}
+
 size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   if (!loaded) throw Err{SEZKP_E_INVALID, "no trace uploaded"};
+  take_staged();
   using clk = std::chrono::steady_clock;
   const auto t_enter = clk::now();
   double t_sync = 0, t_last = 0;
@@ -751,10 +850,22 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   TreeDev outer0{d_outer, d_colroots, logChunks, 0};
   ok(launch_tree_upper(st, &outer0, ncols, outer_stride, 8, 0), "col_outer");
   rec(3);
+  // guard words: sharded ranks gather every rank's word, so a trip on any
+  // rank makes ALL ranks fail here, before the next collective (no rank is
+  // left blocked in an RCCL call its peers never reach)
+  const int nguard = sharded ? comm->world : 1;
+  // test hook: SEZKP_DEBUG_TRIP_GUARD=<rank> sets that rank's guard word, to
+  // check that the failure is collective (tests/test_gpu_sharded.py)
+  static const char* trip = getenv("SEZKP_DEBUG_TRIP_GUARD");
+  if (trip && atoi(trip) == rank) HIP_OR_THROW(hipMemsetAsync(d_err, 0x7f, 1, st));
+  if (sharded) comm->allgather(d_err, d_err + 8, 4, st);
   HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
-  HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * ncols, d_err, 4, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * ncols, sharded ? d_err + 8 : d_err, 4 * nguard, hipMemcpyDeviceToHost, st));
   sync();
-  if (h_small[8 * ncols]) throw Err{SEZKP_E_DEVICE, "column commitment guard tripped (code " + std::to_string(h_small[8 * ncols]) + ")"};
+  for (int r = 0; r < nguard; r++)
+    if (h_small[8 * ncols + r])
+      throw Err{SEZKP_E_DEVICE, "column commitment guard tripped on rank " + std::to_string(sharded ? r : rank) +
+                                    " (code " + std::to_string(h_small[8 * ncols + r]) + ")"};
   std::vector<uint8_t> colroots((uint8_t*)h_small, (uint8_t*)h_small + (size_t)ncols * 32);
   for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
 
@@ -1095,6 +1206,7 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     // hardware queue per context when many contexts share the GPU)
     if (getenv("SEZKP_ONE_STREAM")) c->st2 = c->st;
     else HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+    HIP_OR_THROW(hipStreamCreateWithFlags(&c->stc, hipStreamNonBlocking));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));
@@ -1148,6 +1260,28 @@ int32_t sezkp_comm_unique_id(uint8_t out[128], char* err, size_t err_len) {
   }
 }
 void sezkp_ctx_destroy(sezkp_ctx* ctx) { delete ctx; }
+
+int32_t sezkp_ctx_stage(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len) {
+  try {
+    if (!ctx || !blocks) throw Err{SEZKP_E_INVALID, "null argument"};
+    ctx->stage(*blocks);
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+    return SEZKP_E_NOMEM;
+  }
+}
+int32_t sezkp_host_register(void* p, size_t bytes) {
+  if (!p || !bytes) return SEZKP_E_INVALID;
+  return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? SEZKP_OK : SEZKP_E_DEVICE;
+}
+int32_t sezkp_host_unregister(void* p) {
+  if (!p) return SEZKP_E_INVALID;
+  return hipHostUnregister(p) == hipSuccess ? SEZKP_OK : SEZKP_E_DEVICE;
+}
 
 int32_t sezkp_ctx_upload(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len) {
   try {
@@ -1218,6 +1352,8 @@ int32_t sezkp_ctx_prove_async(sezkp_ctx* ctx, const uint8_t manifest_root[32], u
       std::lock_guard<std::mutex> lk(a.mu);
       if (a.state != AsyncSlot::IDLE)
         throw Err{SEZKP_E_INVALID, "a proof is already in flight on this context (call sezkp_ctx_wait)"};
+      HIP_OR_THROW(hipSetDevice(ctx->device));
+      ctx->take_staged();  // this proof's trace image is fixed before the call returns
       memcpy(a.root, manifest_root, 32);
       a.state = AsyncSlot::RUNNING;
     }

@@ -239,8 +239,12 @@ void verify_v1(const uint8_t* bytes, size_t len, const sezkp_block_view* blocks)
     ENSURE(acc == 0, "AIR composition non-zero at row " + std::to_string(q.row));
   }
 
-  // FRI (fri.rs:130-222) on the transcript aligned with the prover
+  // FRI (fri.rs:130-222) on the transcript aligned with the prover. The
+  // layer count comes from the untrusted proof: it must be log2(domain_n) + 1
+  // (and so <= 64) before it sizes any shift. Stricter than the reference,
+  // same verdict on honest proofs.
   ENSURE(n_layers > 0, "no FRI roots");
+  ENSURE(n_layers <= 64 && (1ULL << (n_layers - 1)) == domain_n, "FRI layer count does not match domain_n");
   tr.absorb("fri_layer_root", roots[0].data(), 32);
   auto bb = tr.challenge("fri_betas", 8 * (n_layers - 1));
   {

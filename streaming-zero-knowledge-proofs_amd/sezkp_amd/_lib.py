@@ -29,7 +29,7 @@ EXPORTS = [
     "sezkp_comm_unique_id", "sezkp_ctx_create_sharded", "sezkp_ctx_create_sharded_host", "sezkp_ctx_prove_borrow",
     "sezkp_blocks_decode_jsonl", "sezkp_blocks_encode_jsonl", "sezkp_manifest_decode", "sezkp_ctx_dist_ntt",
     "sezkp_blocks_encode_cbor", "sezkp_simulate_trace", "sezkp_simulate_blocks",
-    "sezkp_ctx_prove_async", "sezkp_ctx_wait",
+    "sezkp_ctx_prove_async", "sezkp_ctx_wait", "sezkp_ctx_stage", "sezkp_host_register", "sezkp_host_unregister",
 ]
 
 
@@ -111,6 +111,9 @@ def _load():
     L.sezkp_simulate_blocks.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)] + E
     L.sezkp_ctx_prove_async.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32] + E
     L.sezkp_ctx_wait.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_size_t)] + E
+    L.sezkp_ctx_stage.argtypes = [C.c_void_p, C.POINTER(BlockView)] + E
+    L.sezkp_host_register.argtypes = [C.c_void_p, C.c_size_t]
+    L.sezkp_host_unregister.argtypes = [C.c_void_p]
     L.sezkp_ctx_dist_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32] + E
     return L
 

@@ -116,6 +116,15 @@ class ProverContext:
         check(lib.sezkp_ctx_upload(self._h, C.byref(blocks.view()), err, 1024), err)
         self.tau = blocks.tau
 
+    def stage(self, blocks: BlockSoA) -> None:
+        """Pipelined upload of the next trace (same shape as the uploaded one):
+        async H2D into the spare trace image, allowed while a proof is in
+        flight; the next prove uses it (sezkp_ctx_stage). `blocks` must stay
+        alive and unchanged until that prove has started."""
+        err = C.create_string_buffer(1024)
+        check(lib.sezkp_ctx_stage(self._h, C.byref(blocks.view()), err, 1024), err)
+        self._staged = blocks  # keep the arrays alive
+
     def prove(self, manifest_root: bytes, streaming: bool = False) -> ProofArtifact:
         pb = Buf()
         err = C.create_string_buffer(1024)

@@ -50,6 +50,28 @@ class BlockSoA:
         self._view = v
         return v
 
+    def pin(self) -> "BlockSoA":
+        """Page-lock the per-step arrays (sezkp_host_register) so staged uploads
+        (ProverContext.stage) are DMA that overlaps other proofs' kernels."""
+        if getattr(self, "_pinned", None) is None:
+            self._pinned = []
+            for f in ("input_mv", "mv", "has_write", "wsym"):
+                a = getattr(self, f)
+                if a.nbytes and lib.sezkp_host_register(a.ctypes.data, a.nbytes) == 0:
+                    self._pinned.append(a)
+        return self
+
+    def unpin(self) -> None:
+        for a in getattr(self, "_pinned", None) or []:
+            lib.sezkp_host_unregister(a.ctypes.data)
+        self._pinned = None
+
+    def __del__(self):
+        try:
+            self.unpin()
+        except Exception:
+            pass
+
     def manifest_root(self) -> bytes:
         out = C.create_string_buffer(32)
         lib.sezkp_manifest_root(C.byref(self.view()), out)

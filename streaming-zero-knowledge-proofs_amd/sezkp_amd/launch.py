@@ -74,6 +74,49 @@ def _worker(rank: int, world: int, port: int, args, q) -> None:
         dist.destroy_process_group()
 
 
+def _stop(ps) -> None:
+    """Terminate, then kill, every worker still alive (a rank blocked in a
+    collective whose peer failed never returns on its own)."""
+    for p in ps:
+        if p.is_alive():
+            p.terminate()
+    for p in ps:
+        p.join(timeout=10)
+        if p.is_alive():
+            p.kill()
+            p.join(timeout=10)
+
+
+def _collect(ps, q, timeout: float):
+    """Results one by one. The first error, a worker that died without
+    reporting, or the overall timeout stops the remaining ranks.
+    Returns (sorted results, None) or (partial results, error message)."""
+    import queue
+    res = []
+    deadline = time.monotonic() + timeout
+    while len(res) < len(ps):
+        left = deadline - time.monotonic()
+        if left <= 0:
+            _stop(ps)
+            return res, f"timeout after {timeout:.0f} s ({len(res)} of {len(ps)} ranks reported)"
+        try:
+            r = q.get(timeout=min(1.0, left))
+        except queue.Empty:
+            reported = {x[0] for x in res}
+            dead = [i for i, p in enumerate(ps) if i not in reported and not p.is_alive()]
+            if dead:
+                _stop(ps)
+                return res, f"rank {dead[0]} exited with code {ps[dead[0]].exitcode} without a result"
+            continue
+        res.append(r)
+        if r[1]:
+            _stop(ps)
+            return res, f"rank {r[0]}: {r[1]}"
+    for p in ps:
+        p.join(timeout=60)
+    return sorted(res), None
+
+
 def prove(args) -> int:
     if not args.out.lower().endswith(".cbor"):
         print("error: --out must be a .cbor artifact", file=sys.stderr)
@@ -96,16 +139,12 @@ def prove(args) -> int:
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, args.gpus, port, args, q)) for r in range(args.gpus)]
+    ps = [ctx.Process(target=_worker, args=(r, args.gpus, port, args, q), daemon=True) for r in range(args.gpus)]
     for p in ps:
         p.start()
-    res = sorted(q.get(timeout=args.timeout) for _ in ps)
-    for p in ps:
-        p.join(timeout=60)
-    errs = [(r, e) for r, e, *_ in res if e]
-    if errs:
-        for r, e in errs:
-            print(f"error: rank {r}: {e}", file=sys.stderr)
+    res, err = _collect(ps, q, args.timeout)
+    if err:
+        print(f"error: {err}", file=sys.stderr)
         return 1
     print(json.dumps({"gpus": args.gpus, "comm": args.comm, "proof_bytes": res[0][2],
                       "load_s": [round(x[3], 3) for x in res], "prove_s": [round(x[4], 4) for x in res]}))

@@ -413,3 +413,39 @@ def test_async_proofs_in_flight_bit_exact(gpu_ok, product, oracle):
     ctxs[1].prove_async(roots[1])  # destroy with a proof in flight waits for it
     for c in ctxs:
         c.close()
+
+
+def test_staged_uploads_pipeline_bit_exact(gpu_ok, product, oracle):
+    """sezkp_ctx_stage: the next trace (same shape, other values) goes over
+    PCIe into the spare trace image while a proof is in flight; every proof
+    equals the oracle's for ITS trace, whether staged from pinned or pageable
+    memory, staged twice before a prove, or not staged at all."""
+    T, b, tau = 1 << 13, 512, 4
+    traces = [product.synthetic_blocks(T, b, tau, s) for s in range(5)]
+    traces[1].pin()
+    traces[3].pin()
+    roots = [t.manifest_root() for t in traces]
+    want = [oracle.prove_v1(t, r) for t, r in zip(traces, roots)]
+    c = product.ProverContext(0)
+    c.upload(traces[0])
+    c.prove_async(roots[0])
+    c.stage(traces[1])                     # overlaps proof 0
+    assert bytes(c.wait_view()) == want[0]
+    c.prove_async(roots[1])
+    c.stage(traces[2])                     # pageable source
+    assert bytes(c.wait_view()) == want[1]
+    c.stage(traces[3])                     # replaces the staged trace 2
+    assert bytes(c.prove_view(roots[3])) == want[3]
+    assert bytes(c.prove_view(roots[3])) == want[3]  # nothing staged: same trace again
+    c.stage(traces[4])
+    assert c.prove(roots[4]).proof_bytes == want[4]
+    other = product.synthetic_blocks(T, 256, tau, 9)  # other block boundaries
+    with pytest.raises(product.SezkpError, match="block boundaries"):
+        c.stage(other)
+    with pytest.raises(product.SezkpError, match="another shape"):
+        c.stage(product.synthetic_blocks(T, b, tau + 1, 9))
+    c.upload(other)                        # a new shape goes through upload
+    assert c.prove(other.manifest_root()).proof_bytes == oracle.prove_v1(other, other.manifest_root())
+    c.close()
+    for t in traces:
+        t.unpin()

@@ -176,3 +176,40 @@ def test_launcher_jsonl_artifact_matches_oracle(gpu_ok, product, oracle, tmp_pat
     bad[bad.index(str(tmp_path / "m.cbor"))] = str(tmp_path / "bad.cbor")
     r = subprocess.run(bad, cwd=PKG, capture_output=True, text=True, timeout=600)
     assert r.returncode == 1 and "manifest root mismatch" in r.stderr
+
+
+def _trip_worker(rank, world, port, q):
+    sys.path[:0] = [PKG, ORACLE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SEZKP_DEBUG_TRIP_GUARD="1")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sezkp_amd
+        blocks = sezkp_amd.synthetic_blocks(1 << 13, 512, 2, 42)
+        ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
+        ctx.upload(blocks)
+        try:
+            ctx.prove(blocks.manifest_root())
+            q.put((rank, "no error"))
+        except Exception as e:
+            q.put((rank, str(e)))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_guard_trip_fails_every_rank(gpu_ok):
+    """A guard trip on ONE rank (test hook) must fail every rank at the same
+    point, so no rank blocks in a collective its peers never reach."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_trip_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for rank, msg in res:
+        assert "guard tripped on rank 1" in msg, (rank, msg)

@@ -84,6 +84,11 @@ def test_host_verifier_accepts_oracle_proof_and_rejects_tampering(product, oracl
             product.StarkV1.verify(product.ProofArtifact("stark", root, bytes(bad), {}), blocks, root)
     with pytest.raises(product.SezkpError):
         product.StarkV1.verify(product.ProofArtifact("stark", root, proof[:-7], {}), blocks, root)
+    # domain_n no longer matching the FRI layer count (untrusted sizes never size a shift)
+    bad = bytearray(proof)
+    bad[0:8] = (int.from_bytes(proof[0:8], "little") * 2).to_bytes(8, "little")
+    with pytest.raises(product.SezkpError):
+        product.StarkV1.verify(product.ProofArtifact("stark", root, bytes(bad), {}), blocks, root)
     with pytest.raises(product.SezkpError):
         product.StarkV1.verify(art, blocks, bytes(32))
     with pytest.raises(product.SezkpError):

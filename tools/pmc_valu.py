@@ -3,9 +3,12 @@
 (SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU
 SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE).
 
-valu_ms = SQ_INSTS_VALU * 4 cycles / (1024 SIMDs * 2.4 GHz): the time the
-kernel's VALU instructions need if every SIMD issued one wave64 op per
-4 cycles (the int32 VALU ceiling); valu_frac = valu_ms / kernel duration.
+valu_ms = SQ_INSTS_VALU * 2 cycles / (1024 SIMDs * 2.4 GHz): the time the
+kernel's VALU instructions need if every SIMD issued one wave64 instruction
+per 2 cycles (MI355X_MICROARCH.md: 32 lanes/cycle, 2.4 GHz max clock);
+valu_frac = valu_ms / kernel duration. Half-rate instructions (v_alignbit,
+v_add3, v_mad_u64_u32, carry ops: tools/valu_rates.hip) keep a saturated
+kernel below 1.0.
 """
 import csv
 import re
@@ -30,7 +33,7 @@ def main(path):
         avg = {n: sum(v) / len(v) for n, v in c.items()}
         d = sorted(dur[k].values())
         ms = d[len(d) // 2]
-        valu_ms = avg.get("SQ_INSTS_VALU", 0) * 4 / (1024 * 2.4e9) * 1e3
+        valu_ms = avg.get("SQ_INSTS_VALU", 0) * 2 / (1024 * 2.4e9) * 1e3
         rows.append((ms * len(d), k, len(d), ms, valu_ms, avg))
     rows.sort(reverse=True)
     print(f"{'kernel':44s} {'n':>4s} {'ms':>8s} {'valu_ms':>8s} {'frac':>5s} {'waves':>8s} {'valu/wave':>9s} {'lds/wave':>8s}")
