@@ -4,7 +4,7 @@
  * Drop-in boundary for logannye/streaming-zero-knowledge-proofs:
  *   - top level: replaces `impl ProvingBackend for StarkV1`
  *     (crates/sezkp-core/src/backend.rs:41-61, crates/sezkp-stark/src/lib.rs:126-190);
- *   - version symbols: crates/sezkp-ffi/src/lib.rs:65-79 (ABI bumped 1 -> 2);
+ *   - version symbols: crates/sezkp-ffi/src/lib.rs:65-79 (ABI bumped 1 -> 3);
  *   - kernel level: the hot loops of crates/sezkp-ffts (ntt.rs:79-177,
  *     coset.rs:85-102), crates/sezkp-stark/src/v1/{lde.rs:42-97,
  *     fri_stream.rs:37-121, merkle.rs:46-160, prover.rs:200-239}.
@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SEZKP_ABI_VERSION 2u
+#define SEZKP_ABI_VERSION 3u
 
 #define SEZKP_OK 0
 #define SEZKP_E_INVALID (-1)   /* malformed input (shape, non power-of-two n, ...) */
@@ -176,18 +176,47 @@ int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, u
 /* In-place NTT (dir=+1 forward, -1 inverse incl. n^-1), natural -> natural:
  * ntt.rs:79-155. `scratch` must hold 2^log_n elements. */
 int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir, void* stream);
-/* Coset LDE + DEEP (lde.rs:42-97): evals[2^log_n] (base-domain values) ->
- * out[2^(log_n+log_blowup)] = y_i / (shift*w^i - z), shift fixed to 3.
- * `evals` is overwritten. */
-int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_blowup, uint64_t z, uint64_t* out,
-                                void* stream);
-/* FRI fold (prover.rs:208-230): out[i] = in[i] + beta*in[i+n], i < n. Also
- * hashes the folded leaves into a Merkle tree whose root lands in root32. */
+/* Coset LDE + DEEP (deep_coset_lde_stream, lde.rs:42-97): evals[2^log_n]
+ * (base-domain values) -> interpolate (ntt.rs:117-155) -> coset evaluation
+ * on shift * <w_N> (coset.rs:85-102) -> out[i] = y_i / (shift * w_N^i - z),
+ * N = 2^(log_n + log_blowup), log_blowup <= 3 (the prover: 3, shift 3,
+ * prover.rs:119). leaves32 != NULL also writes the N layer-0 leaf digests
+ * BLAKE3(out[i] LE) (fri_stream.rs:37-41), 16-byte aligned. `evals` is
+ * overwritten. SEZKP_E_INVALID when a denominator vanishes ((z/shift)^N = 1;
+ * the prover nudges z off the coset, prover.rs:119-135) or shift = 0. */
+int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_blowup, uint64_t shift, uint64_t z,
+                                uint64_t* out, uint8_t* leaves32, void* stream);
+/* FRI fold (prover.rs:208-230): out[i] = in[i] + beta*in[i+n_out], i < n_out
+ * (a power of two); inputs canonical. */
+int32_t sezkp_fri_fold(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, void* stream);
+/* The same fold, also hashing the folded leaves into a Merkle tree whose root
+ * lands in root32 (host memory; the call synchronises `stream`). */
 int32_t sezkp_fri_fold_commit(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, uint8_t* root32,
                               void* stream);
 /* BLAKE3 leaves of 8-byte LE field values (merkle.rs:150-160) -> Merkle root
- * (merkle.rs:46-71), n a power of two. */
+ * (merkle.rs:46-71), n a power of two; root32 in host memory (synchronises). */
 int32_t sezkp_merkle_root_u64(const uint64_t* vals, uint64_t n, uint8_t* root32, void* stream);
+/* hash_field_leaves (merkle.rs:150-160): leaves32[i] = BLAKE3(vals[i] as 8 LE
+ * bytes), one 32-byte digest per value. */
+int32_t sezkp_blake3_leaves_u64(const uint64_t* vals, uint64_t n, uint8_t* leaves32, void* stream);
+/* hash_field_leaves_labeled (merkle.rs:132-147): BLAKE3("col_leaf" || u32 LE
+ * label_len || label || vals[i] LE), label_len <= 44 (one BLAKE3 block; the
+ * prover's labels are at most 20 bytes, openings.rs:89-116). */
+int32_t sezkp_blake3_leaves_labeled(const uint64_t* vals, uint64_t n, const char* label, uint32_t label_len,
+                                    uint8_t* leaves32, void* stream);
+/* MerkleTree::from_leaves (merkle.rs:46-71): nodes32 receives every level
+ * bottom -> top (level 0 = the n leaves, then ceil(len/2) per level, odd
+ * promotion carries the last node up), the root last:
+ * sezkp_merkle_node_count(n) digests. n = 0 is one all-zero leaf (merkle.rs:48-50).
+ * nodes32 may equal leaves32 when it has room for every level. */
+uint64_t sezkp_merkle_node_count(uint64_t n);
+int32_t sezkp_merkle_build(const uint8_t* leaves32, uint64_t n, uint8_t* nodes32, void* stream);
+/* MerkleTree::open (merkle.rs:80-108) of q leaf indices idx[q] (device) in the
+ * tree sezkp_merkle_build wrote for n leaves: out32[i * depth + l] = sibling at
+ * level l (bottom -> top) of leaf idx[i] % n; a node without a sibling is its
+ * own. depth = ceil(log2 n) (0 for n <= 1). */
+int32_t sezkp_merkle_paths(const uint8_t* nodes32, uint64_t n, const uint64_t* idx, uint32_t q, uint8_t* out32,
+                           void* stream);
 
 /* ------------------------------------------------ host helpers (CPU)
  * Manifest leaf_hash + merkle_root (crates/sezkp-merkle/src/lib.rs:85-157). */

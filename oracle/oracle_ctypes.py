@@ -78,6 +78,11 @@ def lib():
         L.orc_tr_absorb_u64.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64]
         L.orc_tr_challenge.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t]
         L.orc_merkle_root.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p]
+        L.orc_merkle_nodes.restype = C.c_size_t
+        L.orc_merkle_nodes.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p]
+        L.orc_merkle_open.restype = C.c_size_t
+        L.orc_merkle_open.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.orc_lde_deep_shift.argtypes = [C.c_void_p, C.c_size_t, C.c_uint, C.c_uint64, C.c_uint64, C.c_void_p]
         L.orc_manifest_leaf_hash.argtypes = [C.POINTER(_OrcBlocks), C.c_uint32, C.c_void_p]
         L.orc_manifest_root.argtypes = [C.POINTER(_OrcBlocks), C.c_void_p]
         L.orc_manifest_frontier_root.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p]
@@ -184,6 +189,38 @@ def lde_deep(base: np.ndarray, blow_log2: int, z: int) -> np.ndarray:
     out = np.zeros(b.size << blow_log2, dtype=np.uint64)
     lib().orc_lde_deep(b.ctypes.data, b.size, blow_log2, z, out.ctypes.data)
     return out
+
+
+def lde_deep_shift(base: np.ndarray, blow_log2: int, shift: int, z: int) -> np.ndarray:
+    """lde.rs:42-97 with the coset shift as a parameter."""
+    b = np.ascontiguousarray(base, dtype=np.uint64)
+    out = np.zeros(b.size << blow_log2, dtype=np.uint64)
+    lib().orc_lde_deep_shift(b.ctypes.data, b.size, blow_log2, shift, z, out.ctypes.data)
+    return out
+
+
+def merkle_nodes(leaves: bytes) -> bytes:
+    """MerkleTree::from_leaves (merkle.rs:46-71): every level, bottom -> top."""
+    n = len(leaves) // 32
+    cnt = lib().orc_merkle_nodes(leaves, n, None)
+    out = C.create_string_buffer(32 * cnt)
+    lib().orc_merkle_nodes(leaves, n, out)
+    return out.raw
+
+
+def merkle_open(leaves: bytes, idx) -> list:
+    """MerkleTree::open (merkle.rs:80-108) per index: the sibling digests."""
+    n = len(leaves) // 32
+    ix = np.ascontiguousarray(idx, dtype=np.uint64)
+    depth = 0
+    m = max(n, 1)
+    while m > 1:
+        m = (m + 1) // 2
+        depth += 1
+    out = C.create_string_buffer(32 * depth * max(ix.size, 1))
+    lib().orc_merkle_open(leaves, n, ix.ctypes.data, ix.size, out)
+    raw = out.raw
+    return [[raw[32 * (depth * i + l):32 * (depth * i + l + 1)] for l in range(depth)] for i in range(ix.size)]
 
 
 def merkle_root(leaves: bytes) -> bytes:

@@ -426,6 +426,27 @@ void orc_merkle_root(const uint8_t *leaves32, size_t n, uint8_t root[32]) {
     mtree_free(&t);
 }
 
+/* MerkleTree::from_leaves (merkle.rs:46-71): every level bottom->top into
+ * out (level 0 = the leaves; n = 0 is one zero leaf); returns the node count */
+size_t orc_merkle_nodes(const uint8_t *leaves32, size_t n, uint8_t *out) {
+    mtree t;
+    mtree_build(&t, leaves32, n);
+    size_t total = t.lvl_off[t.n_levels - 1] + 1;
+    if (out) memcpy(out, t.nodes, 32 * total);
+    mtree_free(&t);
+    return total;
+}
+
+/* MerkleTree::open (merkle.rs:80-108) for q indices: q * depth siblings */
+size_t orc_merkle_open(const uint8_t *leaves32, size_t n, const uint64_t *idx, size_t q, uint8_t *sibs) {
+    mtree t;
+    mtree_build(&t, leaves32, n);
+    size_t depth = t.n_levels - 1;
+    for (size_t i = 0; i < q; i++) mtree_open(&t, (size_t)idx[i], sibs + 32 * depth * i);
+    mtree_free(&t);
+    return depth;
+}
+
 /* StreamingLayerBuilder (fri_stream.rs:55-121) */
 typedef struct {
     uint8_t (*stack)[32];
@@ -835,6 +856,15 @@ static uint64_t *lde_deep(const uint64_t *base_vals, size_t n, unsigned blow_log
         }
     }
     return y;
+}
+
+/* lde.rs:42-97 with the coset shift as a parameter (deep_coset_lde_stream
+ * takes it from its caller; the prover passes 3, prover.rs:119) */
+void orc_lde_deep_shift(const uint64_t *base_vals, size_t n, unsigned blow_log2, uint64_t shift, uint64_t z,
+                        uint64_t *out) {
+    uint64_t *y = lde_deep(base_vals, n, blow_log2, shift, z);
+    memcpy(out, y, (n << blow_log2) * sizeof(uint64_t));
+    free(y);
 }
 
 /* lde.rs:42-97 as a standalone entry (blowup 2^blow_log2, shift 3) */

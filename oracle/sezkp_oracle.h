@@ -80,6 +80,10 @@ void orc_merkle_root(const uint8_t *leaves32, size_t n, uint8_t root[32]);      
 void orc_manifest_leaf_hash(const orc_blocks *b, uint32_t k, uint8_t out[32]);   /* sezkp-merkle leaf_hash */
 void orc_manifest_root(const orc_blocks *b, uint8_t out[32]);                    /* commit_blocks / merkle_root */
 void orc_manifest_frontier_root(const uint8_t *leaves32, size_t n, uint8_t out[32]); /* Frontier (JSONL path) */
+size_t orc_merkle_nodes(const uint8_t *leaves32, size_t n, uint8_t *out);            /* from_leaves: all levels */
+size_t orc_merkle_open(const uint8_t *leaves32, size_t n, const uint64_t *idx, size_t q, uint8_t *sibs); /* open */
+void orc_lde_deep_shift(const uint64_t *base_vals, size_t n, unsigned blow_log2, uint64_t shift, uint64_t z,
+                        uint64_t *out);                                                   /* lde.rs:42-97 */
 void orc_hash_leaf_u64(uint64_t v, uint8_t out[32]);                             /* merkle.rs:150-160 */
 void orc_hash_leaf_labeled(uint64_t v, const char *label, uint8_t out[32]);     /* merkle.rs:132-147 */
 

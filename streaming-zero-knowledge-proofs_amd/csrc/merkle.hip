@@ -74,7 +74,7 @@ __device__ __forceinline__ void wg_reduce(uint32_t (*lds)[W], int cnt, int lvl, 
 // inversion in lane 0 of wave 0.
 constexpr int DEEP_PER = 16;
 __global__ void __launch_bounds__(MK_THREADS) k_deep(uint64_t* __restrict__ y, int logN, uint64_t z, NttTables T,
-                                                     int logP, uint32_t g) {
+                                                     int logP, uint32_t g, uint64_t shift) {
   __shared__ uint64_t wtot[MK_THREADS / 64];
   __shared__ uint64_t s_inv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -84,9 +84,10 @@ __global__ void __launch_bounds__(MK_THREADS) k_deep(uint64_t* __restrict__ y, i
   uint64_t d[DEEP_PER], a[DEEP_PER];
   uint64_t P = 1;
   if (act) {
-    // x_j = 3 * w_N^(g + P j) ; first from the two-level table, then incremental
+    // x_j = shift * w_N^(g + P j) (shift = 3 in the prover); first from the
+    // two-level table, then incremental
     const uint64_t e = ((uint64_t)g + (i0 << logP)) << (T.K - logN);
-    uint64_t x = gl_mul(gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]), 3);
+    uint64_t x = gl_mul(gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]), shift);
     uint64_t wN;
     {
       const uint64_t e1 = 1ULL << (T.K - logN + logP);
@@ -94,7 +95,7 @@ __global__ void __launch_bounds__(MK_THREADS) k_deep(uint64_t* __restrict__ y, i
     }
 #pragma unroll
     for (int j = 0; j < DEEP_PER; j++) {
-      d[j] = gl_sub(x, z);
+      d[j] = i0 + j < N ? gl_sub(x, z) : 1;  // N < 16 (tiny kernel-level calls): neutral tail
       P = gl_mul(P, d[j]);
       a[j] = P;
       x = gl_mul(x, wN);
@@ -133,7 +134,7 @@ __global__ void __launch_bounds__(MK_THREADS) k_deep(uint64_t* __restrict__ y, i
   for (int j = DEEP_PER - 1; j >= 0; j--) {
     uint64_t inv_dj = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
     inv_run = gl_mul(inv_run, d[j]);
-    y[i0 + j] = gl_mul(y[i0 + j], inv_dj);
+    if (i0 + j < N) y[i0 + j] = gl_mul(y[i0 + j], inv_dj);
   }
 }
 
@@ -556,12 +557,13 @@ __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict_
 }
 
 // ------------------------------------------------------------------ host
-hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw, int logP, uint32_t g) {
+hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw, int logP, uint32_t g,
+                       uint64_t shift) {
   if (logP > logN) return hipErrorInvalidValue;
   const uint64_t N = 1ULL << (logN - logP);
   const uint64_t per_wg = (uint64_t)MK_THREADS * DEEP_PER;
   const unsigned grid = (unsigned)((N + per_wg - 1) / per_wg);
-  hipLaunchKernelGGL(k_deep, dim3(grid), dim3(MK_THREADS), 0, st, y, logN, z, tw, logP, g);
+  hipLaunchKernelGGL(k_deep, dim3(grid), dim3(MK_THREADS), 0, st, y, logN, z, tw, logP, g, shift);
   return hipGetLastError();
 }
 

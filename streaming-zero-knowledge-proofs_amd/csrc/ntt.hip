@@ -686,6 +686,36 @@ __device__ __forceinline__ uint64_t gl_pow_dev(uint64_t b, uint64_t e) {
   return r;
 }
 
+// Coset scaling for a shift other than the prover's 3 (kernel-level ABI):
+// a[p] *= base^e, e = bitrev_logn(p), from base^e = lo[e & 2047] hi[e >> 11].
+__global__ void __launch_bounds__(NTT_THREADS) k_pow_tables(uint64_t* __restrict__ lo, uint64_t* __restrict__ hi,
+                                                            uint64_t base, uint32_t nhi) {
+  const uint32_t t = blockIdx.x * NTT_THREADS + threadIdx.x;
+  if (t < 2048) lo[t] = gl_pow_dev(base, t);
+  if (t < nhi) hi[t] = gl_pow_dev(base, 2048ull * t);
+}
+__global__ void __launch_bounds__(NTT_THREADS) k_scale_pow_bitrev(uint64_t* __restrict__ a, int logn,
+                                                                  const uint64_t* __restrict__ lo,
+                                                                  const uint64_t* __restrict__ hi) {
+  const uint64_t p = blockIdx.x * (uint64_t)NTT_THREADS + threadIdx.x;
+  if (p >> logn) return;
+  const uint32_t e = logn ? __brev((uint32_t)p) >> (32 - logn) : 0;
+  a[p] = gl_mul(a[p], gl_mul(lo[e & 2047], hi[e >> 11]));
+}
+hipError_t launch_scale_pow_bitrev(hipStream_t st, uint64_t* a, int logn, uint64_t base, uint64_t* scratch) {
+  if (logn > 31) return hipErrorInvalidValue;
+  const uint32_t nhi = logn > 11 ? 1u << (logn - 11) : 1u;
+  uint64_t* lo = scratch;
+  uint64_t* hi = scratch + 2048;
+  const uint32_t nt = std::max<uint32_t>(2048, nhi);
+  hipLaunchKernelGGL(k_pow_tables, dim3((nt + NTT_THREADS - 1) / NTT_THREADS), dim3(NTT_THREADS), 0, st, lo, hi, base,
+                     nhi);
+  const uint64_t n = 1ULL << logn;
+  hipLaunchKernelGGL(k_scale_pow_bitrev, dim3((unsigned)((n + NTT_THREADS - 1) / NTT_THREADS)), dim3(NTT_THREADS), 0,
+                     st, a, logn, lo, hi);
+  return hipGetLastError();
+}
+
 // Every WG reduces the partials (f(z) = K1 S, c' = f(z) K2), then grid-
 // strides: C_j <- (C_j - f(z)) inv_j (= q(w^j)), rlo[t] = r^t, rhi[t] = c' r^(4096 t).
 __global__ void __launch_bounds__(NTT_THREADS) k_q_tables(uint64_t* __restrict__ C, const uint64_t* __restrict__ inv,

@@ -766,6 +766,10 @@ void sezkp_ctx::stage(const sezkp_block_view& v) {
   check_shape_same(v);
   HIP_OR_THROW(hipSetDevice(device));
   std::lock_guard<std::mutex> lk(stage_mu);
+  // the copy stream is created by the first stage(): streams map to the
+  // device's hardware queues round-robin in creation order, so a context that
+  // never stages keeps the (main, side) queue layout of the proofs in flight
+  if (!stc) HIP_OR_THROW(hipStreamCreateWithFlags(&stc, hipStreamNonBlocking));
   TraceSlot& t = slot[1 - active];
   if (!t.imv) alloc_slot(t);  // first stage on this workspace: the spare image
   staged = false;             // (re)filling the spare slot
@@ -1206,7 +1210,6 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     // hardware queue per context when many contexts share the GPU)
     if (getenv("SEZKP_ONE_STREAM")) c->st2 = c->st;
     else HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
-    HIP_OR_THROW(hipStreamCreateWithFlags(&c->stc, hipStreamNonBlocking));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));
@@ -1516,26 +1519,118 @@ int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir
   }
 }
 
-int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_blowup, uint64_t z, uint64_t* out,
-                                void* stream) {
+int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_blowup, uint64_t shift, uint64_t z,
+                                uint64_t* out, uint8_t* leaves32, void* stream) {
   try {
     int dev = 0;
     HIP_OR_THROW(hipGetDevice(&dev));
     const NttTables& T = tables_for_device(dev);
     hipStream_t st = (hipStream_t)stream;
-    if (log_blowup != 3 || log_n + log_blowup > 31) return SEZKP_E_INVALID;
+    shift %= GL_P_HOST;
+    z %= GL_P_HOST;
+    if (log_blowup > 3 || log_n + log_blowup > 28 || shift == 0) return SEZKP_E_INVALID;
+    if (leaves32 && (reinterpret_cast<uintptr_t>(leaves32) & 15)) return SEZKP_E_INVALID;
     const int logN = (int)(log_n + log_blowup);
+    // every denominator shift w^i - z must be nonzero: (z / shift)^N != 1
+    {
+      uint64_t t = hgl_mul(z, hgl_inv(shift));
+      for (int i = 0; i < logN; i++) t = hgl_mul(t, t);
+      if (t == 1) return SEZKP_E_INVALID;
+    }
     if (ntt_dif(st, evals, (int)log_n, true, T) != hipSuccess) return SEZKP_E_DEVICE;
+    uint64_t* scratch = nullptr;
+    if (shift != 3) {  // the LDE load applies 3^j n^-1: pre-scale the coefficients by (shift / 3)^j
+      const size_t cnt = 2048 + (log_n > 11 ? (1ULL << (log_n - 11)) : 1);
+      HIP_OR_THROW(hipMallocAsync(reinterpret_cast<void**>(&scratch), cnt * 8, st));
+      if (launch_scale_pow_bitrev(st, evals, (int)log_n, hgl_mul(shift, hgl_inv(3)), scratch) != hipSuccess)
+        return SEZKP_E_DEVICE;
+    }
     const uint64_t inv_n = hgl_inv((1ULL << log_n) % GL_P_HOST);
     const DeepFuse dfuse{z, logN, 0, 0};
     bool deep_fused = false;
-    if (ntt_dit(st, out, logN, false, T, evals, (int)log_n, inv_n, 0, &dfuse, &deep_fused) != hipSuccess)
+    if (ntt_dit(st, out, logN, false, T, evals, (int)log_n, inv_n, 0, shift == 3 ? &dfuse : nullptr, &deep_fused) !=
+        hipSuccess)
       return SEZKP_E_DEVICE;
-    if (!deep_fused && launch_deep(st, out, logN, z, T) != hipSuccess) return SEZKP_E_DEVICE;
+    if (!deep_fused && launch_deep(st, out, logN, z, T, 0, 0, shift) != hipSuccess) return SEZKP_E_DEVICE;
+    if (leaves32 && launch_leaves_u64(st, out, 1ULL << logN, reinterpret_cast<uint32_t*>(leaves32)) != hipSuccess)
+      return SEZKP_E_DEVICE;
+    if (scratch) HIP_OR_THROW(hipFreeAsync(scratch, st));
     return SEZKP_OK;
   } catch (const Err& e) {
     return e.code;
   }
+}
+
+int32_t sezkp_fri_fold(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, void* stream) {
+  if (n_out == 0 || (n_out & (n_out - 1))) return SEZKP_E_INVALID;
+  if (launch_fold_any((hipStream_t)stream, in, out, n_out, beta % GL_P_HOST) != hipSuccess)
+    return SEZKP_E_DEVICE;
+  return SEZKP_OK;
+}
+
+int32_t sezkp_blake3_leaves_u64(const uint64_t* vals, uint64_t n, uint8_t* leaves32, void* stream) {
+  if (reinterpret_cast<uintptr_t>(leaves32) & 15) return SEZKP_E_INVALID;
+  if (launch_leaves_u64((hipStream_t)stream, vals, n, reinterpret_cast<uint32_t*>(leaves32)) != hipSuccess)
+    return SEZKP_E_DEVICE;
+  return SEZKP_OK;
+}
+
+int32_t sezkp_blake3_leaves_labeled(const uint64_t* vals, uint64_t n, const char* label, uint32_t label_len,
+                                    uint8_t* leaves32, void* stream) {
+  if (label_len > 44 || (label_len && !label) || (reinterpret_cast<uintptr_t>(leaves32) & 15))
+    return SEZKP_E_INVALID;
+  const ColTemplate ct = make_template(0, 1, std::string(label ? label : "", label_len));
+  if (launch_leaves_labeled((hipStream_t)stream, vals, n, ct, reinterpret_cast<uint32_t*>(leaves32)) != hipSuccess)
+    return SEZKP_E_DEVICE;
+  return SEZKP_OK;
+}
+
+// MerkleTree level table (merkle.rs:46-71): n = 0 is one zero leaf
+static MerkleLevels merkle_levels(uint64_t n) {
+  MerkleLevels L{};
+  uint64_t len = n ? n : 1, off = 0;
+  int l = 0;
+  for (;;) {
+    L.off[l] = off;
+    L.len[l] = len;
+    if (len == 1) break;
+    off += len;
+    len = (len + 1) / 2;
+    l++;
+  }
+  L.depth = l;
+  return L;
+}
+
+uint64_t sezkp_merkle_node_count(uint64_t n) {
+  const MerkleLevels L = merkle_levels(n);
+  return L.off[L.depth] + 1;
+}
+
+int32_t sezkp_merkle_build(const uint8_t* leaves32, uint64_t n, uint8_t* nodes32, void* stream) {
+  if ((reinterpret_cast<uintptr_t>(nodes32) & 15) || (n && (reinterpret_cast<uintptr_t>(leaves32) & 15)))
+    return SEZKP_E_INVALID;
+  hipStream_t st = (hipStream_t)stream;
+  const MerkleLevels L = merkle_levels(n);
+  uint32_t* nodes = reinterpret_cast<uint32_t*>(nodes32);
+  if (n == 0) return hipMemsetAsync(nodes32, 0, 32, st) == hipSuccess ? SEZKP_OK : SEZKP_E_DEVICE;
+  if (nodes32 != leaves32 && hipMemcpyAsync(nodes32, leaves32, 32 * n, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return SEZKP_E_DEVICE;
+  for (int l = 1; l <= L.depth; l++)
+    if (launch_merkle_level(st, nodes + 8 * L.off[l - 1], L.len[l - 1], nodes + 8 * L.off[l]) != hipSuccess)
+      return SEZKP_E_DEVICE;
+  return SEZKP_OK;
+}
+
+int32_t sezkp_merkle_paths(const uint8_t* nodes32, uint64_t n, const uint64_t* idx, uint32_t q, uint8_t* out32,
+                           void* stream) {
+  if ((reinterpret_cast<uintptr_t>(nodes32) & 15) || (reinterpret_cast<uintptr_t>(out32) & 15))
+    return SEZKP_E_INVALID;
+  const MerkleLevels L = merkle_levels(n);
+  if (launch_merkle_paths((hipStream_t)stream, reinterpret_cast<const uint32_t*>(nodes32), L, idx, q,
+                          reinterpret_cast<uint32_t*>(out32)) != hipSuccess)
+    return SEZKP_E_DEVICE;
+  return SEZKP_OK;
 }
 
 int32_t sezkp_fri_fold_commit(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, uint8_t* root32,

@@ -210,9 +210,25 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
 // rows [row0, row0 + nrows) (nrows = n for the whole trace)
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
                           const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows);
-// DEEP divide of y[j] at x = 3 * w_{2^logN}^(g + (j << logP)) (logP = 0, g = 0: natural layout)
+// DEEP divide of y[j] at x = shift * w_{2^logN}^(g + (j << logP)) (logP = 0, g = 0: natural layout)
 hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw, int logP = 0,
-                       uint32_t g = 0);
+                       uint32_t g = 0, uint64_t shift = 3);
+// a[p] *= base^bitrev_logn(p) (tables lo[2048] | hi[max(1, n >> 11)] in `scratch`)
+hipError_t launch_scale_pow_bitrev(hipStream_t st, uint64_t* a, int logn, uint64_t base, uint64_t* scratch);
+// kernel-level ABI helpers (api_kernels.hip); digests are 8 u32 words
+hipError_t launch_fold_any(hipStream_t st, const uint64_t* in, uint64_t* out, uint64_t n_out, uint64_t beta);
+hipError_t launch_leaves_u64(hipStream_t st, const uint64_t* v, uint64_t n, uint32_t* out);
+hipError_t launch_leaves_labeled(hipStream_t st, const uint64_t* v, uint64_t n, const ColTemplate& ct, uint32_t* out);
+// one MerkleTree level with odd promotion: out[i] = H(in[2i] || in[2i+1]), or in[2i] when 2i+1 == len
+hipError_t launch_merkle_level(hipStream_t st, const uint32_t* in, uint64_t len, uint32_t* out);
+struct MerkleLevels {
+  uint64_t off[64];  // node offset of level l (level 0 = the leaves)
+  uint64_t len[64];
+  int depth;         // levels above the leaves
+};
+// q paths of `depth` siblings: path i, level l = sibling of (idx[i] % len[0]) >> l
+hipError_t launch_merkle_paths(hipStream_t st, const uint32_t* nodes, const MerkleLevels& L, const uint64_t* idx,
+                               uint32_t q, uint32_t* out);
 // Sharded LDE layout change (see prover.cpp, prove_sharded): cyclic coset
 // values of rank g (index g + P*j) <-> runs of S = 2^12 consecutive indices.
 hipError_t launch_cyc_pack(hipStream_t st, const uint64_t* cyc, uint64_t* send, uint64_t M, int logP);

@@ -30,6 +30,8 @@ EXPORTS = [
     "sezkp_blocks_decode_jsonl", "sezkp_blocks_encode_jsonl", "sezkp_manifest_decode", "sezkp_ctx_dist_ntt",
     "sezkp_blocks_encode_cbor", "sezkp_simulate_trace", "sezkp_simulate_blocks",
     "sezkp_ctx_prove_async", "sezkp_ctx_wait", "sezkp_ctx_stage", "sezkp_host_register", "sezkp_host_unregister",
+    "sezkp_fri_fold", "sezkp_blake3_leaves_u64", "sezkp_blake3_leaves_labeled", "sezkp_merkle_node_count",
+    "sezkp_merkle_build", "sezkp_merkle_paths",
 ]
 
 
@@ -67,7 +69,22 @@ class BlockView(C.Structure):
     _fields_ = [("n_blocks", C.c_uint32), ("tau", C.c_uint32)] + [(f, C.POINTER(t)) for f, t in VIEW_FIELDS]
 
 
+def _one_hip_runtime() -> None:
+    """PyTorch-ROCm wheels bundle their own libamdhip64 / libhsa-runtime64
+    (same SONAMEs as /opt/rocm's). If this library is loaded first, torch later
+    maps a second copy of the runtime by path, and whichever copy initialises
+    second finds no device. Importing torch first makes the dynamic linker
+    resolve this library's libamdhip64.so.7 to the copy torch already mapped,
+    so the process has one HIP runtime and torch tensors share its context.
+    Without torch installed there is only /opt/rocm's runtime."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load():
+    _one_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` (or __graft_entry__.build())")
     L = C.CDLL(LIB_PATH)
@@ -89,7 +106,15 @@ def _load():
     L.sezkp_ctx_stream.restype = C.c_void_p
     L.sezkp_ctx_stream.argtypes = [C.c_void_p]
     L.sezkp_gl_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p]
-    L.sezkp_gl_coset_lde_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.sezkp_gl_coset_lde_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p,
+                                          C.c_void_p, C.c_void_p]
+    L.sezkp_fri_fold.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.sezkp_blake3_leaves_u64.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.sezkp_blake3_leaves_labeled.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.sezkp_merkle_node_count.restype = C.c_uint64
+    L.sezkp_merkle_node_count.argtypes = [C.c_uint64]
+    L.sezkp_merkle_build.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.sezkp_merkle_paths.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
     L.sezkp_fri_fold_commit.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_char_p, C.c_void_p]
     L.sezkp_merkle_root_u64.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p, C.c_void_p]
     L.sezkp_manifest_root.argtypes = [C.POINTER(BlockView), C.c_char_p]

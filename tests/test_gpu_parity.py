@@ -73,7 +73,7 @@ def test_coset_lde_deep_matches_oracle(gpu_ok, product, oracle, log_n):
     want = oracle.lde_deep(base, 3, z)
     d_in = _dev(torch, base)
     d_out = torch.empty(8 * n, dtype=torch.int64, device="cuda")
-    assert product.lib.sezkp_gl_coset_lde_deep(d_in.data_ptr(), log_n, 3, z, d_out.data_ptr(), None) == 0
+    assert product.lib.sezkp_gl_coset_lde_deep(d_in.data_ptr(), log_n, 3, 3, z, d_out.data_ptr(), None, None) == 0
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_host(d_out), want)
 
@@ -439,9 +439,11 @@ def test_staged_uploads_pipeline_bit_exact(gpu_ok, product, oracle):
     assert bytes(c.prove_view(roots[3])) == want[3]  # nothing staged: same trace again
     c.stage(traces[4])
     assert c.prove(roots[4]).proof_bytes == want[4]
-    other = product.synthetic_blocks(T, 256, tau, 9)  # other block boundaries
+    other = product.synthetic_blocks(T, 520, tau, 9)  # 16 blocks again, other boundaries
     with pytest.raises(product.SezkpError, match="block boundaries"):
         c.stage(other)
+    with pytest.raises(product.SezkpError, match="another shape"):
+        c.stage(product.synthetic_blocks(T, 256, tau, 9))  # other block count
     with pytest.raises(product.SezkpError, match="another shape"):
         c.stage(product.synthetic_blocks(T, b, tau + 1, 9))
     c.upload(other)                        # a new shape goes through upload

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol(product):
     missing = [s for s in sorted(declared) if not hasattr(lib, s)]
     assert not missing, missing
     assert declared == set(product._lib.EXPORTS)
-    assert lib.sezkp_abi_version() == 2
+    assert lib.sezkp_abi_version() == 3
 
 
 def test_cbor_decode_matches_oracle_decode(product, oracle):

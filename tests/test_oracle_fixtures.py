@@ -214,3 +214,35 @@ def test_openmp_oracle_matches_single_thread(oracle):
         bl = S.synthetic_blocks(T, b, tau, 3)
         want.append(hashlib.sha256(oracle.prove_v1(bl, bl.manifest_root())).hexdigest())
     assert r.stdout.split() == want
+
+
+def test_merkle_nodes_and_open_two_oracles(oracle):
+    """C oracle MerkleTree::from_leaves / open (every level, odd promotion,
+    idx %= n) against the independent Python restatement (merkle.rs:46-108),
+    the checker of the kernel-level sezkp_merkle_build / sezkp_merkle_paths."""
+    import sezkp_oracle_py as PY
+    for n in [0, 1, 2, 3, 5, 6, 7, 11, 13, 16, 33]:
+        leaves = [PY.leaf(i * 7919 + n) for i in range(n)]
+        levels = PY.tree_levels(leaves)
+        assert oracle.merkle_nodes(b"".join(leaves)) == b"".join(b"".join(l) for l in levels)
+        idx = list(range(n + 3)) + [2 ** 40 + 5]
+        got = oracle.merkle_open(b"".join(leaves), idx)
+        assert got == [PY.tree_open(levels, i) for i in idx]
+
+
+def test_lde_deep_shift_matches_python(oracle):
+    """lde.rs:42-97 with a shift other than 3: C oracle vs a direct
+    evaluation (interpolate by the naive inverse DFT, evaluate on shift*<w_N>,
+    divide by x - z)."""
+    import sezkp_oracle_py as PY
+    n, blow, shift, z = 8, 2, 7, 123456789
+    base = [int(v) for v in oracle.det_vec(n, 5)]
+    coeffs = PY.idft(base, PY.root_2exp(3))
+    N = n << blow
+    w = PY.root_2exp(5)
+    want = []
+    for i in range(N):
+        x = shift * pow(w, i, P) % P
+        y = sum(c * pow(x, j, P) for j, c in enumerate(coeffs)) % P
+        want.append(y * PY.inv((x - z) % P) % P)
+    assert [int(v) for v in oracle.lde_deep_shift(np.array(base, np.uint64), blow, shift, z)] == want
