@@ -315,9 +315,37 @@ __device__ __forceinline__ void deep_tile(uint64_t x, uint64_t z, Emit emit) {
   }
 }
 
-template <bool DIF, bool INV, int M1, int M2, int SKIP, bool DEEP = false>
+// NARROW (sL = 0, the first DIT / last DIF pass): a tile is 16 contiguous
+// sub-transforms of R elements, so a thread's R points are consecutive and
+// the lanes of one load or store instruction are R elements apart (64 cache
+// lines per wave instruction). Those passes move the tile between HBM and the
+// LDS image with lane-consecutive addresses (element e = j * 256 + tid of the
+// tile: row e mod R, column e / R) and the register FFTs read / write the LDS.
+template <int R>
+__device__ __forceinline__ void narrow_to_lds(uint64_t* sh, const uint64_t* __restrict__ a, uint64_t tile) {
+  constexpr int m = __builtin_ctz(R);
+  const uint64_t* src = a + tile * (uint64_t)(NTT_CMAX * R);
+#pragma unroll
+  for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
+    const int e = j * NTT_THREADS + threadIdx.x;
+    sh[(e & (R - 1)) * NTT_PADC + (e >> m)] = src[e];
+  }
+}
+template <int R>
+__device__ __forceinline__ void lds_to_narrow(const uint64_t* sh, uint64_t* __restrict__ a, uint64_t tile) {
+  constexpr int m = __builtin_ctz(R);
+  uint64_t* dst = a + tile * (uint64_t)(NTT_CMAX * R);
+#pragma unroll
+  for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
+    const int e = j * NTT_THREADS + threadIdx.x;
+    dst[e] = sh[(e & (R - 1)) * NTT_PADC + (e >> m)];
+  }
+}
+
+template <bool DIF, bool INV, int M1, int M2, int SKIP, bool DEEP = false, bool NARROW = false>
 __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   constexpr int F1 = 1 << M1, F2 = 1 << M2, m = M1 + M2, R = 1 << m;
+  static_assert(!(NARROW && DEEP), "the fused DEEP pass is a wide pass");
   __shared__ uint64_t sh[R * NTT_PADC];
   __shared__ uint64_t W[R];
   const int tid = threadIdx.x;
@@ -337,11 +365,14 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   }
   const int tw_shift = T.K - m - G.sL;
   const int c = tid & (NTT_CMAX - 1), g = tid / NTT_CMAX;
+  // a plain NARROW load stages the tile through the LDS image first
+  const bool staged_load = NARROW && !P.dp_rlo && !P.src;
+  if (staged_load) narrow_to_lds<R>(sh, P.a, G.tile);
   __syncthreads();
   if constexpr (!DIF) {
+    uint64_t x[F1];
     if (g < F2) {  // step 1: thread (c, u), registers r
       const int u = g;
-      uint64_t x[F1];
       uint64_t low = 0;
       if (P.dp_rlo) {  // DEEP-quotient LDE load (first pass, sL = 0, low = 0, SKIP = 0)
         const uint64_t p0 = tile_pos(G, F1 * u, c, low);
@@ -359,6 +390,9 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
 #pragma unroll
           for (int s = 0; s < (1 << SKIP); s++) x[r + s] = v;
         }
+      } else if (NARROW) {
+#pragma unroll
+        for (int r = 0; r < F1; r++) x[r] = sh[(F1 * u + r) * NTT_PADC + c];
       } else {
 #pragma unroll
         for (int r = 0; r < F1; r++) x[r] = P.a[tile_pos(G, F1 * u + r, c, low)];
@@ -366,18 +400,18 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
           const int j1 = rev<M2>(u);
           uint64_t t = tw_pow(T, (low * (uint64_t)j1) << tw_shift, INV);
           const uint64_t s1 = tw_pow(T, (low * (uint64_t)F2) << tw_shift, INV);
-          uint64_t tw[F1];
 #pragma unroll
-          for (int q = 0; q < F1; q++) {
-            tw[q] = t;
-            t = gl_mul(t, s1);
+          for (int q = 0; q < F1; q++) {  // x[rev(q)] *= t s1^q, the chain applied as it goes
+            x[rev<M1>(q)] = gl_mul(x[rev<M1>(q)], t);
+            if (q + 1 < F1) t = gl_mul(t, s1);
           }
-#pragma unroll
-          for (int r = 0; r < F1; r++) x[r] = gl_mul(x[r], tw[rev<M1>(r)]);
         }
       }
       fft_dit_regs<M1, INV, SKIP>(x);
-      const int j1 = rev<M2>(u);
+    }
+    if (staged_load) __syncthreads();  // every thread has read its points from the image
+    if (g < F2) {
+      const int u = g, j1 = rev<M2>(u);
 #pragma unroll
       for (int k2 = 0; k2 < F1; k2++) {
         const uint64_t v = k2 && j1 ? gl_mul(x[k2], W[j1 * k2]) : x[k2];
@@ -385,9 +419,9 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
       }
     }
     __syncthreads();
+    uint64_t y[F2];
     if (g < F1) {  // step 2: thread (c, k2), registers u
       const int k2 = g;
-      uint64_t y[F2];
 #pragma unroll
       for (int u = 0; u < F2; u++) y[u] = sh[(u * F1 + k2) * NTT_PADC + c];
       fft_dit_regs<M2, INV, 0>(y);
@@ -403,19 +437,33 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
         deep_tile<F2>(x0, P.deep_z, [&](int k1, uint64_t inv) {
           P.a[tile_pos(G, k2 + F1 * k1, c, low)] = gl_mul(sh[(k1 * F1 + k2) * NTT_PADC + c], inv);
         });
-      } else {
+      } else if (!NARROW) {
 #pragma unroll
         for (int k1 = 0; k1 < F2; k1++) P.a[tile_pos(G, k2 + F1 * k1, c, low)] = y[k1];
       }
     }
+    if constexpr (NARROW) {  // rows k2 + F1 k1 back through the image, lane-consecutive stores
+      __syncthreads();
+      if (g < F1) {
+#pragma unroll
+        for (int k1 = 0; k1 < F2; k1++) sh[(g + F1 * k1) * NTT_PADC + c] = y[k1];
+      }
+      __syncthreads();
+      lds_to_narrow<R>(sh, P.a, G.tile);
+    }
   } else {
+    uint64_t x[F2];
     if (g < F1) {  // step 1: thread (c, r), registers u (natural)
       const int r = g;
-      uint64_t x[F2];
       uint64_t low;
 #pragma unroll
-      for (int u = 0; u < F2; u++) x[u] = P.a[tile_pos(G, F1 * u + r, c, low)];
+      for (int u = 0; u < F2; u++)
+        x[u] = NARROW ? sh[(F1 * u + r) * NTT_PADC + c] : P.a[tile_pos(G, F1 * u + r, c, low)];
       fft_dif_regs<M2, INV>(x);
+    }
+    if (NARROW) __syncthreads();
+    if (g < F1) {
+      const int r = g;
 #pragma unroll
       for (int q = 0; q < F2; q++) {
         const int klo = rev<M2>(q);
@@ -424,9 +472,9 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
       }
     }
     __syncthreads();
+    uint64_t y[F1];
     if (g < F2) {  // step 2: thread (c, q), registers r
       const int q = g;
-      uint64_t y[F1];
 #pragma unroll
       for (int r = 0; r < F1; r++) y[r] = sh[(q * F1 + r) * NTT_PADC + c];
       fft_dif_regs<M1, INV>(y);
@@ -435,19 +483,33 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
       if (low != 0) {  // post-twiddle w^(low * (k_lo + F2 k_hi)), k_hi = rev(q')
         uint64_t t = tw_pow(T, (low * (uint64_t)rev<M2>(q)) << tw_shift, INV);
         const uint64_t s1 = tw_pow(T, (low * (uint64_t)F2) << tw_shift, INV);
-        uint64_t tw[F1];
 #pragma unroll
         for (int kh = 0; kh < F1; kh++) {
-          tw[kh] = t;
-          t = gl_mul(t, s1);
+          y[rev<M1>(kh)] = gl_mul(y[rev<M1>(kh)], t);
+          if (kh + 1 < F1) t = gl_mul(t, s1);
         }
-#pragma unroll
-        for (int qq = 0; qq < F1; qq++) y[qq] = gl_mul(y[qq], tw[rev<M1>(qq)]);
       }
+      if (!NARROW) {
 #pragma unroll
-      for (int qq = 0; qq < F1; qq++) P.a[tile_pos(G, q * F1 + qq, c, low)] = y[qq];
+        for (int qq = 0; qq < F1; qq++) P.a[tile_pos(G, q * F1 + qq, c, low)] = y[qq];
+      }
+    }
+    if constexpr (NARROW) {
+      __syncthreads();
+      if (g < F2) {
+#pragma unroll
+        for (int qq = 0; qq < F1; qq++) sh[(g * F1 + qq) * NTT_PADC + c] = y[qq];
+      }
+      __syncthreads();
+      lds_to_narrow<R>(sh, P.a, G.tile);
     }
   }
+}
+
+// SEZKP_NTT_NO_NARROW=1: sL = 0 passes load and store their rows directly (A/B comparison)
+static bool narrow_disabled() {
+  static const bool off = getenv("SEZKP_NTT_NO_NARROW") != nullptr;
+  return off;
 }
 
 // launch one pass with the register kernel when its shape allows, else false
@@ -456,8 +518,14 @@ static bool launch_ntt4(hipStream_t st, const NttPassArgs& P, unsigned tiles) {
   if (P.logC != 4) return false;
   const int skip = P.src ? P.skip : 0;
   if (DIF && skip) return false;
-#define SEZKP_NTT4(M1, M2, SK) \
-  hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, SK>), dim3(tiles), dim3(NTT_THREADS), 0, st, P)
+  // sL = 0 passes stage their tile through the LDS image (k_ntt4 NARROW)
+#define SEZKP_NTT4(M1, M2, SK)                                                                                \
+  do {                                                                                                         \
+    if (P.sL == 0 && !narrow_disabled())                                                                     \
+      hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, SK, false, true>), dim3(tiles), dim3(NTT_THREADS), 0, st, P); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, SK>), dim3(tiles), dim3(NTT_THREADS), 0, st, P);           \
+  } while (0)
   switch (P.m * 4 + skip) {
     case 8 * 4 + 0: SEZKP_NTT4(4, 4, 0); return true;
     case 7 * 4 + 0: SEZKP_NTT4(4, 3, 0); return true;

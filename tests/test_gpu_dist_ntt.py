@@ -71,9 +71,11 @@ def sampled_spectrum(x: np.ndarray, w_R: int, R: int = 256) -> dict:
     return {m * (n // R): sum(S[r] * wp[(r * m) % R] for r in range(R)) % P for m in range(R)}
 
 
-def _worker_sampled(rank, world, port, log_n, seed, q):
-    """Config 4 size: the full oracle NTT is too slow at 2^26, so the output
-    is checked at the n/256-spaced frequencies (exact, O(n)) plus the round trip."""
+def _worker_full(rank, world, port, log_n, seed, want_path, q):
+    """Config 4 size: every one of the 2^26 outputs against the OpenMP
+    oracle's NTT (ntt.rs:79-111 restated, computed once by the parent and
+    memory-mapped here), plus an independent O(n) check of the n/256-spaced
+    frequencies (residue-class sums, no NTT) and the round trip."""
     sys.path[:0] = [PKG, ORACLE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
@@ -86,45 +88,55 @@ def _worker_sampled(rank, world, port, log_n, seed, q):
         x = orc.det_vec(n, seed)
         e = np.zeros(256, dtype=np.uint64)
         e[1] = 1
-        want = sampled_spectrum(x, int(orc.ntt_forward(e)[1]))
+        sampled = sampled_spectrum(x, int(orc.ntt_forward(e)[1]))
+        X = np.load(want_path, mmap_mode="r")
         ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
         loc = torch.from_numpy(np.ascontiguousarray(x[rank::world]).view(np.int64)).cuda()
         ctx.dist_ntt(loc)
         out = loc.cpu().numpy().view(np.uint64)
+        full_ok = np.array_equal(out, expected_local(X, rank, world))
         M = n // world
         Q = M // world
-        seen, fwd_ok = 0, True
-        for i, v in want.items():  # X[i] with i = g Q + q + M k1 sits at k1 Q + q on rank g
+        seen, samp_ok = 0, True
+        for i, v in sampled.items():  # X[i] with i = g Q + q + M k1 sits at k1 Q + q on rank g
             k1, rem = divmod(i, M)
             g, qq = divmod(rem, Q)
             if g == rank:
                 seen += 1
-                fwd_ok = fwd_ok and int(out[k1 * Q + qq]) == v
+                samp_ok = samp_ok and int(out[k1 * Q + qq]) == v
         ctx.dist_ntt(loc, inverse=True)
         inv_ok = np.array_equal(loc.cpu().numpy().view(np.uint64), x[rank::world])
         ctx.close()
-        q.put((rank, fwd_ok, inv_ok, seen))
+        q.put((rank, full_ok, samp_ok, inv_ok, seen))
     except Exception as e:
-        q.put((rank, f"ERR {type(e).__name__}: {e}", False, 0))
+        q.put((rank, f"ERR {type(e).__name__}: {e}", False, False, 0))
     finally:
         dist.destroy_process_group()
 
 
-def test_dist_ntt_config4_size_p8(gpu_ok):
-    """BASELINE config 4's shape: 2^26 points over P = 8 ranks."""
+def test_dist_ntt_config4_size_p8(gpu_ok, oracle, tmp_path):
+    """BASELINE config 4's shape: 2^26 points over P = 8 ranks, every output
+    compared with the oracle (OpenMP build, same restated ntt.rs:79-111)."""
     import torch.multiprocessing as mp
+    log_n, seed = 26, 2024
+    x = oracle.det_vec(1 << log_n, seed)
+    oracle.use_mt(int(os.environ.get("OMP_NUM_THREADS", "8")))
+    want_path = str(tmp_path / "ntt_2e26.npy")
+    np.save(want_path, oracle.ntt_forward(x))
+    del x
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker_sampled, args=(r, 8, port, 26, 2024, q)) for r in range(8)]
+    ps = [ctx.Process(target=_worker_full, args=(r, 8, port, log_n, seed, want_path, q)) for r in range(8)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=600) for _ in ps)
     for p in ps:
         p.join(timeout=60)
-    assert sum(r[3] for r in res) == 256  # every sampled frequency was owned by exactly one rank
-    for rank, fwd_ok, inv_ok, _ in res:
-        assert fwd_ok is True, f"rank {rank}: {fwd_ok}"
+    assert sum(r[4] for r in res) == 256  # every sampled frequency was owned by exactly one rank
+    for rank, full_ok, samp_ok, inv_ok, _ in res:
+        assert full_ok is True, f"rank {rank}: {full_ok}"
+        assert samp_ok, f"rank {rank}: sampled frequencies differ"
         assert inv_ok, f"rank {rank}: inverse did not round-trip"
 
 

@@ -48,6 +48,24 @@ def test_ntt_roundtrip_matches_oracle(gpu_ok, product, oracle, log_n):
     np.testing.assert_array_equal(_host(d), x)
 
 
+@pytest.mark.parametrize("log_n", [22, 24, 26])
+def test_ntt_large_matches_openmp_oracle(gpu_ok, product, oracle, log_n):
+    """The headline LDE size (2^24) and config 4's 2^26 on one device: every
+    output of sezkp_gl_ntt against the OpenMP oracle (ntt.rs:79-155), and the
+    inverse round trip."""
+    torch = gpu_ok
+    oracle.use_mt(int(os.environ.get("OMP_NUM_THREADS", "8")))
+    x = oracle.det_vec(1 << log_n, 2024 + log_n)
+    d = _dev(torch, x)
+    scratch = torch.empty_like(d)
+    assert product.lib.sezkp_gl_ntt(d.data_ptr(), scratch.data_ptr(), log_n, 1, None) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d), oracle.ntt_forward(x))
+    assert product.lib.sezkp_gl_ntt(d.data_ptr(), scratch.data_ptr(), log_n, -1, None) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d), x)
+
+
 @pytest.mark.parametrize("vec", ["zeros", "delta", "ap"])
 def test_ntt_special_vectors(gpu_ok, product, oracle, vec):
     torch = gpu_ok
