@@ -1,0 +1,35 @@
+#!/bin/bash
+# Build the NTT component-timing variants (see tools/ntt_parts_main.hip) into
+# tools/ntt_parts/: a copy of csrc/ntt.hip with VAR_TW / VAR_W / VAR_FFT hooks
+# around the pass twiddles, the W twiddle and the register FFTs. Run each
+# binary on the GPU box; DESIGN.md §3 quotes the result.
+set -euo pipefail
+D=tools/ntt_parts
+mkdir -p $D
+python3 - <<'PY'
+s = open("streaming-zero-knowledge-proofs_amd/csrc/ntt.hip").read()
+rep = [
+    ("if (low != 0) {  // pre-twiddle", "if (VAR_TW && low != 0) {  // pre-twiddle"),
+    ("if (low != 0) {  // post-twiddle", "if (VAR_TW && low != 0) {  // post-twiddle"),
+    ("const uint64_t v = k2 && j1 ? gl_mul(x[k2], W[j1 * k2]) : x[k2];",
+     "const uint64_t v = k2 && j1 ? (VAR_W ? gl_mul(x[k2], W[j1 * k2]) : x[k2] ^ W[j1 * k2]) : x[k2];"),
+    ("const uint64_t v = klo && r ? gl_mul(x[q], W[r * klo]) : x[q];",
+     "const uint64_t v = klo && r ? (VAR_W ? gl_mul(x[q], W[r * klo]) : x[q] ^ W[r * klo]) : x[q];"),
+    ("      fft_dit_regs<M1, INV, SKIP>(x);", "      if (VAR_FFT) fft_dit_regs<M1, INV, SKIP>(x);"),
+    ("      fft_dit_regs<M2, INV, 0>(y);", "      if (VAR_FFT) fft_dit_regs<M2, INV, 0>(y);"),
+    ("      fft_dif_regs<M2, INV>(x);", "      if (VAR_FFT) fft_dif_regs<M2, INV>(x);"),
+    ("      fft_dif_regs<M1, INV>(y);", "      if (VAR_FFT) fft_dif_regs<M1, INV>(y);"),
+]
+for a, b in rep:
+    assert a in s, a
+    s = s.replace(a, b)
+s = s.replace('#include "dev_common.h"', '#include "../../streaming-zero-knowledge-proofs_amd/csrc/dev_common.h"')
+s = s.replace('#include "sezkp_internal.h"', '#include "../../streaming-zero-knowledge-proofs_amd/csrc/sezkp_internal.h"')
+open("tools/ntt_parts/ntt_var.hip", "w").write(s)
+PY
+cp tools/ntt_parts_main.hip $D/main.hip
+for v in "1 1 1" "0 1 1" "1 0 1" "1 1 0" "0 0 0"; do
+  set -- $v
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DVAR_TW=$1 -DVAR_W=$2 -DVAR_FFT=$3 -o $D/nv_$1$2$3 $D/main.hip
+done
+echo built $D
