@@ -1222,33 +1222,27 @@ __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const
 // 64-lane WG = 4096 rows of one dictionary column (4 chunks): each lane folds
 // 64 rows to a level-6 node, 4 LDS levels give the 4 chunk roots, written as
 // leaves of the column's outer tree. Requires n >= 1024 (n % 64 == 0).
-// XCD-aware order: WG b runs on XCD b % 8, so the (column, row block) items
-// are dealt out in 8 contiguous column-major ranges, one per XCD: a column's
-// gathered tables are fetched into about one XCD's L2 instead of all eight.
 __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                         const DictCol* __restrict__ dcols,
                                                         const DictPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ tabs, uint32_t* __restrict__ outer,
                                                         uint64_t outer_stride, uint64_t row0, uint64_t row_end,
-                                                        uint32_t* __restrict__ dlev, uint32_t gx) {
+                                                        uint32_t* __restrict__ dlev) {
   __shared__ uint32_t lds[8][64];
-  const uint32_t nwg = gridDim.x;
-  const uint32_t item = (nwg & 7) == 0 ? (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-  const uint32_t bx = item % gx, by = item / gx;
-  const DictCol dc = dcols[by];
+  const DictCol dc = dcols[blockIdx.y];
   const ColTemplate* ctp = tmpl + dc.col;
   const ColTemplate ct = *ctp;
-  const DictPlan P = plans[by];
+  const DictPlan P = plans[blockIdx.y];
   const uint32_t* tab = tabs + 8 * dc.tab;
   const int lane = threadIdx.x;
   // high-K columns give each lane more rows (fewer LDS levels per row)
   const int a = dict_extra(P.K);
   const int llog = DICT_LANE_LOG + a;  // rows per lane (log2)
-  const uint64_t wg_row = row0 + ((uint64_t)bx << (llog + 6));
+  const uint64_t wg_row = row0 + ((uint64_t)blockIdx.x << (llog + 6));
   if (wg_row >= row_end) return;  // grid is sized for a = 0
   const uint64_t lrow = wg_row + ((uint64_t)lane << llog);
   const uint64_t nch_all = T.n >> COL_CHUNK_LOG2;
-  uint32_t* dl = dlev + 8 * (uint64_t)by * nch_all * DLEV_NODES;
+  uint32_t* dl = dlev + 8 * (uint64_t)blockIdx.y * nch_all * DLEV_NODES;
   if (lrow < row_end) {
     uint32_t h[8];
     switch (ct.kind) {
@@ -1357,8 +1351,8 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
     }
   }
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
-  hipLaunchKernelGGL(k_col_commit_dict, dim3(gx * ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
-                     outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev, gx);
+  hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
+                     outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev);
   return hipGetLastError();
 }
 
