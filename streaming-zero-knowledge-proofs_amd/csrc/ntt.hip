@@ -667,18 +667,19 @@ __global__ void __launch_bounds__(256) k_dntt_dft(uint64_t* __restrict__ r, uint
 
 // ------------------------------------------- DEEP quotient (base domain)
 // See DeepPoly (sezkp_internal.h). k_inv_base: inv_j = 1 / (w_n^j - z) for
-// the n base points (16 per lane, one Montgomery batch per 4096) and the
-// per-WG partial sums of C_j w_n^j inv_j.
+// the base points j in [row0, row0 + nrows) (16 per lane, one Montgomery
+// batch per 4096) and the per-WG partial sums of C_j w_n^j inv_j; WG b of the
+// range writes partial[b] (sharded ranks each own a block of rows and then
+// allgather their partials, so every rank reduces the same sum).
 constexpr int DQ_PER = 16;
 __global__ void __launch_bounds__(NTT_THREADS) k_inv_base(const uint64_t* __restrict__ C, uint64_t* __restrict__ inv,
                                                           uint64_t* __restrict__ partial, int logn, uint64_t z,
-                                                          NttTables T) {
+                                                          NttTables T, uint64_t row0, uint64_t nrows) {
   __shared__ uint64_t wtot[NTT_THREADS / 64];
   __shared__ uint64_t s_inv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t n = 1ULL << logn;
-  const uint64_t i0 = ((uint64_t)blockIdx.x * NTT_THREADS + tid) * DQ_PER;
-  const bool act = i0 < n;  // n >= 16 > DQ_PER: a lane's points are all in or all out
+  const uint64_t i0 = row0 + ((uint64_t)blockIdx.x * NTT_THREADS + tid) * DQ_PER;
+  const bool act = i0 < row0 + nrows;  // nrows % 16 == 0: a lane's points are all in or all out
   uint64_t d[DQ_PER], a[DQ_PER];
   uint64_t Pp = 1;
   if (act) {
@@ -785,11 +786,12 @@ hipError_t launch_scale_pow_bitrev(hipStream_t st, uint64_t* a, int logn, uint64
 }
 
 // Every WG reduces the partials (f(z) = K1 S, c' = f(z) K2), then grid-
-// strides: C_j <- (C_j - f(z)) inv_j (= q(w^j)), rlo[t] = r^t, rhi[t] = c' r^(4096 t).
+// strides: C_j <- (C_j - f(z)) inv_j (= q(w^j), j in [row0, row0 + nrows)),
+// rlo[t] = r^t, rhi[t] = c' r^(4096 t).
 __global__ void __launch_bounds__(NTT_THREADS) k_q_tables(uint64_t* __restrict__ C, const uint64_t* __restrict__ inv,
                                                           const uint64_t* __restrict__ partial, uint32_t nparts,
-                                                          uint64_t n, uint64_t K1, uint64_t K2, uint64_t r,
-                                                          uint64_t r4096, uint64_t* __restrict__ rlo,
+                                                          uint64_t row0, uint64_t nrows, uint64_t K1, uint64_t K2,
+                                                          uint64_t r, uint64_t r4096, uint64_t* __restrict__ rlo,
                                                           uint64_t* __restrict__ rhi, uint32_t nhi) {
   __shared__ uint64_t wsum[NTT_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -804,9 +806,33 @@ __global__ void __launch_bounds__(NTT_THREADS) k_q_tables(uint64_t* __restrict__
   for (int w = 1; w < NTT_THREADS / 64; w++) S = gl_add(S, wsum[w]);
   const uint64_t fz = gl_mul(K1, S), cp = gl_mul(fz, K2);
   const uint64_t g0 = (uint64_t)blockIdx.x * NTT_THREADS + tid, gs = (uint64_t)gridDim.x * NTT_THREADS;
-  for (uint64_t j = g0; j < n; j += gs) C[j] = gl_mul(gl_sub(C[j], fz), inv[j]);
+  for (uint64_t j = row0 + g0; j < row0 + nrows; j += gs) C[j] = gl_mul(gl_sub(C[j], fz), inv[j]);
   for (uint64_t t = g0; t < 4096; t += gs) rlo[t] = gl_pow_dev(r, t);
   for (uint64_t t = g0; t < nhi; t += gs) rhi[t] = gl_mul(cp, gl_pow_dev(r4096, t));
+}
+
+hipError_t launch_inv_base(hipStream_t st, const uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
+                           uint64_t z, const NttTables& T, uint64_t row0, uint64_t nrows) {
+  const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
+  if (logn < 4 || nrows % DQ_PER || row0 % per || row0 + nrows > (1ULL << logn)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_inv_base, dim3((unsigned)((nrows + per - 1) / per)), dim3(NTT_THREADS), 0, st, C, inv_scratch,
+                     partial + row0 / per, logn, z, T, row0, nrows);
+  return hipGetLastError();
+}
+
+hipError_t launch_q_tables(hipStream_t st, uint64_t* C, const uint64_t* inv_scratch, const uint64_t* partial, int logn,
+                           int logN, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096, uint64_t* rlo, uint64_t* rhi,
+                           uint64_t row0, uint64_t nrows) {
+  if (logn < 4 || logN < logn || logN > 32) return hipErrorInvalidValue;
+  const uint64_t n = 1ULL << logn;
+  const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
+  const uint32_t nparts = (uint32_t)((n + per - 1) / per);
+  const uint32_t nhi = logN > 12 ? (1u << (logN - 12)) : 1u;
+  const uint64_t work = std::max<uint64_t>(nrows, std::max<uint64_t>(4096, nhi));
+  const unsigned grid = (unsigned)std::min<uint64_t>(1024, (work + NTT_THREADS - 1) / NTT_THREADS);
+  hipLaunchKernelGGL(k_q_tables, dim3(grid), dim3(NTT_THREADS), 0, st, C, inv_scratch, partial, nparts, row0, nrows, K1,
+                     K2, r, r4096, rlo, rhi, nhi);
+  return hipGetLastError();
 }
 
 hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
@@ -814,16 +840,9 @@ hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scrat
                                 uint64_t* rlo, uint64_t* rhi, const NttTables& T) {
   if (logn < 4 || logN < logn || logN > 32) return hipErrorInvalidValue;
   const uint64_t n = 1ULL << logn;
-  const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
-  const uint32_t nparts = (uint32_t)((n + per - 1) / per);
-  hipLaunchKernelGGL(k_inv_base, dim3(nparts), dim3(NTT_THREADS), 0, st, C, inv_scratch, partial, logn, z, T);
-  hipError_t e = hipGetLastError();
+  hipError_t e = launch_inv_base(st, C, inv_scratch, partial, logn, z, T, 0, n);
   if (e != hipSuccess) return e;
-  const uint32_t nhi = logN > 12 ? (1u << (logN - 12)) : 1u;
-  const unsigned grid = (unsigned)std::min<uint64_t>(1024, (n + NTT_THREADS - 1) / NTT_THREADS);
-  hipLaunchKernelGGL(k_q_tables, dim3(grid), dim3(NTT_THREADS), 0, st, C, inv_scratch, partial, nparts, n, K1, K2, r,
-                     r4096, rlo, rhi, nhi);
-  return hipGetLastError();
+  return launch_q_tables(st, C, inv_scratch, partial, logn, logN, K1, K2, r, r4096, rlo, rhi, 0, n);
 }
 
 // ------------------------------------------------------------------ host side

@@ -902,15 +902,19 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     z = hgl_add(z, 1);
   }
 
-  // ---- composition (this rank's rows, then allgather) + INTT (replicated)
+  // ---- composition (this rank's rows), DEEP quotient, INTT
   ok(launch_compose(st, T, A, mask, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
-  if (sharded) comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st);
-  rec(4);
   // single device: DEEP as the LDE of H = q + c S (DeepPoly); the base
   // evaluations become q(w^j) before the INTT. Not when z^n = 1 (z on the
   // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
   const uint64_t zn = hgl_pow(z, n);
   const bool dq = logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY");
+  // sharded: each rank turns its own rows into q(w^j) (the partial sums of
+  // f(z) are allgathered in between), then the q values are allgathered for
+  // the n-point INTT every rank's coset needs; without the quotient the
+  // composition values are allgathered as they are
+  if (sharded && !dq) comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st);
+  rec(4);
   DeepPoly dpoly{d_dq_rlo, d_dq_rhi};
   if (dq) {
     const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
@@ -928,9 +932,19 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
       pw = hgl_mul(pw, rhoM);
     }
     K2 = hgl_mul(K2, G);
-    ok(launch_deep_quotient(st, d_base, d_lde, d_dq_part, logn, logM, z, K1, K2, rho, hgl_pow(rho, 4096), d_dq_rlo,
-                            d_dq_rhi, tw),
-       "deep_quotient");
+    if (sharded) {
+      const uint64_t nrows = row_hi - row_lo, per = 4096;
+      ok(launch_inv_base(st, d_base, d_lde, d_dq_part, logn, z, tw, row_lo, nrows), "inv_base");
+      comm->allgather(d_dq_part + row_lo / per, d_dq_part, (size_t)(nrows / per) * 8, st);
+      ok(launch_q_tables(st, d_base, d_lde, d_dq_part, logn, logM, K1, K2, rho, hgl_pow(rho, 4096), d_dq_rlo, d_dq_rhi,
+                         row_lo, nrows),
+         "q_tables");
+      comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st);
+    } else {
+      ok(launch_deep_quotient(st, d_base, d_lde, d_dq_part, logn, logM, z, K1, K2, rho, hgl_pow(rho, 4096), d_dq_rlo,
+                              d_dq_rhi, tw),
+         "deep_quotient");
+    }
   }
   ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
   rec(5);

@@ -56,6 +56,15 @@ struct DeepPoly {
 hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
                                 int logN, uint64_t z, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096,
                                 uint64_t* rlo, uint64_t* rhi, const NttTables& T);
+// the two halves of launch_deep_quotient over a block of base rows [row0,
+// row0 + nrows) (row0 a multiple of 4096): inverses + this block's partial
+// sums (at partial[row0 / 4096 ...]), then q(w^j) of the block once every
+// partial of the n rows is in `partial` (sharded ranks allgather them between)
+hipError_t launch_inv_base(hipStream_t st, const uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
+                           uint64_t z, const NttTables& T, uint64_t row0, uint64_t nrows);
+hipError_t launch_q_tables(hipStream_t st, uint64_t* C, const uint64_t* inv_scratch, const uint64_t* partial, int logn,
+                           int logN, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096, uint64_t* rlo, uint64_t* rhi,
+                           uint64_t row0, uint64_t nrows);
 
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
 // deep != nullptr: fuse the DEEP division into the last pass when its shape
