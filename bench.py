@@ -232,6 +232,53 @@ class Pipeline:
             t.join()
 
 
+def measure_host_rows(args, blocks, root: bytes, proof: bytes) -> dict:
+    """SURVEY 8(f) rows either side of the GPU path, on this host at the
+    headline size (T = 2^21, b = 512, tau = 8; one host thread each, as the
+    reference runs them): the trace generator + partition (`sezkp-cli
+    simulate`, generator.rs:38-73 + partition.rs:43-150), the block file
+    formats (CBOR io.rs:57-65 / 176-183, JSONL io_jsonl.rs:43-106), the
+    manifest root of the CLI's precheck (sezkp-merkle lib.rs:85-157) and the
+    verifier (v1/verify.rs:60-196) on the bench's own proof. Each output is
+    checked (round trips, the generator's blocks against the bench trace,
+    verification accepted)."""
+    from sezkp_amd import BlockSoA, ProofArtifact, StarkV1, reference_blocks
+    T = blocks.n_rows
+    nb = int(blocks.n_blocks)
+    out = {"T": T, "blocks": nb, "threads": 1}
+
+    def timed(fn, reps=1):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        return r, (time.perf_counter() - t0) / reps
+
+    gen, dt = timed(lambda: reference_blocks(T, args.b, args.tau, 42))
+    same = gen.to_cbor() == blocks.to_cbor()
+    out["simulate"] = {"seconds": dt, "steps_per_s": T / dt, "same_as_bench_trace": same}
+    cb, dt = timed(lambda: blocks.to_cbor())
+    out["cbor_encode"] = {"seconds": dt, "MB": len(cb) / 1e6, "MB_per_s": len(cb) / dt / 1e6}
+    back, dt = timed(lambda: BlockSoA.from_cbor(cb))
+    out["cbor_decode"] = {"seconds": dt, "MB_per_s": len(cb) / dt / 1e6, "blocks_per_s": nb / dt,
+                          "round_trip": back.to_cbor() == cb}
+    jl, dt = timed(lambda: blocks.to_jsonl())
+    out["jsonl_encode"] = {"seconds": dt, "MB": len(jl) / 1e6, "MB_per_s": len(jl) / dt / 1e6}
+    back, dt = timed(lambda: BlockSoA.from_jsonl(jl))
+    out["jsonl_decode"] = {"seconds": dt, "MB_per_s": len(jl) / dt / 1e6, "blocks_per_s": nb / dt,
+                           "round_trip": back.to_cbor() == cb}
+    del back, jl, cb
+    mr, dt = timed(lambda: blocks.manifest_root(), 5)
+    out["manifest_root"] = {"seconds": dt, "blocks_per_s": nb / dt, "matches": mr == root}
+    art = ProofArtifact("stark", root, proof, {})
+    ok = True
+    try:
+        _, dt = timed(lambda: StarkV1.verify(art, blocks, root), 3)
+    except Exception as e:  # reported, never fatal
+        ok, dt = f"{type(e).__name__}: {e}", float("nan")
+    out["verify"] = {"seconds": dt, "accepted": ok, "proof_bytes": len(proof)}
+    return out
+
+
 def high_entropy_blocks(T: int, b: int, tau: int, seed: int):
     """Worst-case input for the dictionary commitments: full-range i8 moves,
     16-bit symbols written with p = 1/2, full-range input moves."""
@@ -260,11 +307,13 @@ def main():
     ap.add_argument("--traces-per-ctx", type=int, default=2, help="distinct pinned traces each context cycles through")
     ap.add_argument("--cpu-mt-log-t", type=int, default=21)
     ap.add_argument("--cpu-single-log-t", type=int, default=16)
-    ap.add_argument("--cpu-faithful-log-t", type=int, default=10,
-                    help="reference-faithful (recomputing) oracle run size; 12 = config 1 (~1 min, 1 thread)")
+    ap.add_argument("--cpu-faithful-log-t", type=int, default=12,
+                    help="reference-faithful (recomputing) oracle run size; 12 = config 1 (T = 4096, ~35 s, 1 thread)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-to-proof", action="store_true", help="skip the staged-upload (host blocks) run")
     ap.add_argument("--no-worst-case", action="store_true")
+    ap.add_argument("--no-host-rows", action="store_true",
+                    help="skip the SURVEY 8(f) host-side rows (ingest, manifest, trace generator, verifier)")
     ap.add_argument("--worst-steps", type=int, default=10)
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the BASELINE config 2 (2^20 NTT) and config 3 (T=2^18 prove) objects")
@@ -392,6 +441,7 @@ def main():
     barrier()
     dt1 = time.perf_counter() - t1
     proof_len = len(proof)
+    single_pb = bytes(proof)  # trace holds[0]'s proof, for the host verifier timing (outside every bracket)
     stages = {k: v / nsp for k, v in stage_sum.items()}
     # the staged upload alone: pinned host -> HBM image (copy stream)
     st = torch.cuda.ExternalStream(ctx.stream)
@@ -464,11 +514,15 @@ def main():
     worst = None
     if rank == 0 and not args.no_worst_case:
         worst = measure_worst_case(args, T)
+    host_rows = None
+    if rank == 0 and not args.no_host_rows:
+        host_rows = measure_host_rows(args, traces[holds[0]], roots[holds[0]], single_pb)
     for c in ctxs:
         c.close()
     del ctxs, ctx
     if rank == 0:
         out["worst_case"] = worst
+        out["host_rows"] = host_rows
         if not args.no_cpu_baseline and world == 1:
             chk = None
             if args.cpu_mt_log_t == args.log_t:
