@@ -232,7 +232,7 @@ class Pipeline:
             t.join()
 
 
-def measure_host_rows(args, blocks, root: bytes, proof: bytes) -> dict:
+def measure_host_rows(args, blocks, root: bytes, proof: bytes, seed: int) -> dict:
     """SURVEY 8(f) rows either side of the GPU path, on this host at the
     headline size (T = 2^21, b = 512, tau = 8; one host thread each, as the
     reference runs them): the trace generator + partition (`sezkp-cli
@@ -253,9 +253,9 @@ def measure_host_rows(args, blocks, root: bytes, proof: bytes) -> dict:
             r = fn()
         return r, (time.perf_counter() - t0) / reps
 
-    gen, dt = timed(lambda: reference_blocks(T, args.b, args.tau, 42))
+    gen, dt = timed(lambda: reference_blocks(T, args.b, args.tau, seed))
     same = gen.to_cbor() == blocks.to_cbor()
-    out["simulate"] = {"seconds": dt, "steps_per_s": T / dt, "same_as_bench_trace": same}
+    out["simulate"] = {"seconds": dt, "steps_per_s": T / dt, "seed": seed, "same_as_bench_trace": same}
     cb, dt = timed(lambda: blocks.to_cbor())
     out["cbor_encode"] = {"seconds": dt, "MB": len(cb) / 1e6, "MB_per_s": len(cb) / dt / 1e6}
     back, dt = timed(lambda: BlockSoA.from_cbor(cb))
@@ -516,7 +516,7 @@ def main():
         worst = measure_worst_case(args, T)
     host_rows = None
     if rank == 0 and not args.no_host_rows:
-        host_rows = measure_host_rows(args, traces[holds[0]], roots[holds[0]], single_pb)
+        host_rows = measure_host_rows(args, traces[holds[0]], roots[holds[0]], single_pb, 42 + holds[0])
     for c in ctxs:
         c.close()
     del ctxs, ctx
