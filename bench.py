@@ -57,6 +57,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # MI355X_MICROARCH.md: 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over
 # 2 cycles (32 lanes/cycle); 2.4 GHz max clock -> 1.2288e12 wave64 instr/s.
 VALU_PEAK = 256 * 4 * 2.4e9 / 2
+# k_layer16's static VALU mix (tools/isa_hist.py on merkle.hip, profiles/r02_isa_k_layer16.txt):
+# 12177 full-rate (v_xor_b32, v_add_u32) and 9594 half-rate instructions (v_alignbit_b32,
+# v_add3_u32, carry / 64-bit ops), i.e. 2 and 4 cycles per wave64 instruction
+L16_FULL, L16_HALF = 12177, 9594
+VALU_PEAK_L16_MIX = VALU_PEAK * 2 * (L16_FULL + L16_HALF) / (2 * L16_FULL + 4 * L16_HALF)
 
 
 def alg_bytes(n: int, tau: int) -> dict:
@@ -465,6 +470,11 @@ def main():
                 "unit": "wave64 VALU instr/s", "frac": (valu_instr / t_l0 / VALU_PEAK) if valu_instr else None,
                 "traffic": traffic, "mean_launch_ms": t_l0 * 1e3,
                 "valu_instr_per_launch": valu_instr,
+                "peak_mix": VALU_PEAK_L16_MIX,
+                "frac_mix": (valu_instr / t_l0 / VALU_PEAK_L16_MIX) if valu_instr else None,
+                "peak_mix_basis": "the same peak with the kernel's static instruction mix priced at 2 cycles "
+                                  "(full rate) / 4 cycles (half rate) per wave64 instruction "
+                                  "(profiles/r02_isa_k_layer16.txt)",
                 "peak_basis": "MI355X_MICROARCH.md: 256 CU x 4 SIMD, one wave64 VALU instruction per 2 cycles per "
                               "SIMD, 2.4 GHz. BLAKE3's rotates (v_alignbit) and 3-input adds issue at half rate "
                               "on gfx950 (tools/valu_rates.hip), so a saturated tree kernel stays below 1.0",
