@@ -591,14 +591,24 @@ def halves(done_t, t0):
             "fill_ms": (ts[0] - t0) * 1e3}
 
 
+# k_ntt4's static VALU mix (the plain 256-point pass, tools/isa_hist.py on ntt.hip):
+# 2142 full-rate and 6510 half-rate instructions (v_cndmask, v_mad_u64_u32, carry
+# and 64-bit ops), priced at 2 / 4 cycles per wave64 instruction
+NTT_FULL, NTT_HALF = 2142, 6510
+VALU_PEAK_NTT_MIX = VALU_PEAK * 2 * (NTT_FULL + NTT_HALF) / (2 * NTT_FULL + 4 * NTT_HALF)
+LDE_WIDE = "k_ntt4<false, false, 4, 4, 0, false, false>"    # passes 2.. of the LDE
+LDE_NARROW = "k_ntt4<false, false, 4, 4, 0, false, true>"   # pass 1: DEEP-polynomial coefficients, staged stores
+
+
 def roofline_ntt(args, torch, stages, N, T):
-    """HBM roofline of the LDE NTT (the HBM-bound kernel family): algorithmic
-    bytes = 16 B per point per pass read+write, the first pass writing only
-    (its input is generated from the n coefficients); traffic from PMC."""
+    """Roofline of the LDE NTT (3 passes over N = 2^24, the DEEP polynomial's
+    coefficients generated in the first pass): bytes moved = 16 B per point per
+    pass (the first pass reads only the n coefficients); traffic and VALU
+    instructions per proof from the per-template PMC summary (the first pass is
+    the NARROW instance, the others the wide one)."""
     t_lde = stages.get("lde_ntt", float("nan")) * 1e-3
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     allp = json.load(open(p)) if os.path.exists(p) else {}
-    prof = {k: v for k, v in allp.items() if k.startswith(("k_ntt", "k_lde"))}
     from sezkp_amd._lib import lib
     passes = getattr(lib, "sezkp_gl_lde_passes", None)
     np_ = int(passes(N.bit_length() - 1)) if passes else 3
@@ -606,11 +616,21 @@ def roofline_ntt(args, torch, stages, N, T):
     out = {"bound": "hbm", "kernel": f"LDE NTT, {np_} passes over N=2^{N.bit_length() - 1} (DEEP included)",
            "achieved": moved / t_lde / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": moved / t_lde / 1e9 / HBM_PEAK_GBS, "traffic": None, "ms": t_lde * 1e3, "moved_bytes": moved,
-           "alg_bytes_survey": 9 * N, "pmc": prof or None,
+           "alg_bytes_survey": 9 * N,
            "measured_on": "single-proof pass: HIP events around the LDE launches on the prover stream"}
-    tr = [v.get("hbm_bytes_per_launch") for v in prof.values() if v.get("hbm_bytes_per_launch")]
-    if prof and all(tr):
-        out["traffic"] = sum(v["hbm_bytes_per_launch"] * v.get("launches_per_proof", 1) for v in prof.values())
+    wide, narrow = allp.get(LDE_WIDE, {}), allp.get(LDE_NARROW, {})
+    if wide.get("hbm_bytes_per_launch") and narrow.get("hbm_bytes_per_launch"):
+        out["traffic"] = (np_ - 1) * wide["hbm_bytes_per_launch"] + narrow["hbm_bytes_per_launch"]
+        out["pmc"] = {LDE_WIDE: wide, LDE_NARROW: narrow}
+    out["binding_resource"] = "valu (see valu.frac_mix); HBM frac is what the passes move over their duration"
+    if wide.get("valu_instr_per_launch") and narrow.get("valu_instr_per_launch"):
+        vi = (np_ - 1) * wide["valu_instr_per_launch"] + narrow["valu_instr_per_launch"]
+        out["valu"] = {"instr_per_proof": vi, "achieved": vi / t_lde, "unit": "wave64 VALU instr/s",
+                       "peak": VALU_PEAK, "frac": vi / t_lde / VALU_PEAK,
+                       "peak_mix": VALU_PEAK_NTT_MIX, "frac_mix": vi / t_lde / VALU_PEAK_NTT_MIX,
+                       "note": "the passes are VALU-bound: canonical Goldilocks on 32-bit lanes is mostly "
+                               "half-rate instructions (carry chains, v_mad_u64_u32, selects); peak_mix prices "
+                               "the kernel's static mix at 2 / 4 cycles per wave64 instruction"}
     return out
 
 

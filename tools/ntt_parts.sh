@@ -21,7 +21,7 @@ rep = [
     ("      fft_dif_regs<M1, INV>(y);", "      if (VAR_FFT) fft_dif_regs<M1, INV>(y);"),
 ]
 rep.append(("  const int c = tid & (NTT_CMAX - 1), g = tid / NTT_CMAX;\n  // a plain NARROW load",
-            "  const int c = tid & (NTT_CMAX - 1), g = tid / NTT_CMAX;\n#if VAR_SLEEP\n  if (blockIdx.x & 1) for (int i = 0; i < VAR_SLEEP; i++) __builtin_amdgcn_s_sleep(127);\n#endif\n  // a plain NARROW load"))
+            "  const int c = tid & (NTT_CMAX - 1), g = tid / NTT_CMAX;\n#if VAR_SLEEP\n  if ((blockIdx.x & 1) && blockIdx.x < 1024) for (int i = 0; i < VAR_SLEEP; i++) __builtin_amdgcn_s_sleep(127);\n#endif\n  // a plain NARROW load"))
 for a, b in rep:
     assert a in s, a
     s = s.replace(a, b)
@@ -34,7 +34,8 @@ for v in "1 1 1" "0 1 1" "1 0 1" "1 1 0" "0 0 0"; do
   set -- $v
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DVAR_TW=$1 -DVAR_W=$2 -DVAR_FFT=$3 -o $D/nv_$1$2$3 $D/main.hip
 done
-# odd workgroups start later (s_sleep), to offset the phases of the workgroups sharing a CU
+# odd workgroups of the first round (blockIdx < 4 x 256 CUs) start later (s_sleep), to offset the
+# phases of the workgroups sharing a CU
 for sl in 1 2 4; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DVAR_SLEEP=$sl -o $D/nv_sleep$sl $D/main.hip
 done

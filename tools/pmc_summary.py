@@ -23,8 +23,9 @@ from collections import defaultdict
 
 
 def _short(name: str) -> str:
-    m = re.search(r"sezkp::(k_[A-Za-z0-9_]+)", name)
-    return m.group(1) if m else name.split("(")[0]
+    """kernel name with its template arguments (k_ntt4<...> instances differ)"""
+    m = re.search(r"sezkp::(k_[A-Za-z0-9_]+)(<[^(]*>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name.split("(")[0]
 
 
 def _load(d: str, counter: str) -> dict:
