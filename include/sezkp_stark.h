@@ -171,8 +171,9 @@ int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, u
                            char* err, size_t err_len);
 
 /* ------------------------------------------------ kernel-level entry points
- * Device pointers (u64 canonical Goldilocks, natural order), 32-byte digests,
- * stream = hipStream_t (NULL = default stream). Asynchronous on `stream`. */
+ * Device pointers (u64 canonical Goldilocks, natural order), 32-byte digests
+ * (16-byte aligned), stream = hipStream_t (NULL = default stream).
+ * Asynchronous on `stream`. Digest counts and lengths up to 2^38. */
 /* In-place NTT (dir=+1 forward, -1 inverse incl. n^-1), natural -> natural:
  * ntt.rs:79-155. `scratch` must hold 2^log_n elements. */
 int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir, void* stream);

@@ -1553,37 +1553,39 @@ int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_bl
     }
     if (ntt_dif(st, evals, (int)log_n, true, T) != hipSuccess) return SEZKP_E_DEVICE;
     uint64_t* scratch = nullptr;
+    bool ok = true;
     if (shift != 3) {  // the LDE load applies 3^j n^-1: pre-scale the coefficients by (shift / 3)^j
       const size_t cnt = 2048 + (log_n > 11 ? (1ULL << (log_n - 11)) : 1);
       HIP_OR_THROW(hipMallocAsync(reinterpret_cast<void**>(&scratch), cnt * 8, st));
-      if (launch_scale_pow_bitrev(st, evals, (int)log_n, hgl_mul(shift, hgl_inv(3)), scratch) != hipSuccess)
-        return SEZKP_E_DEVICE;
+      ok = launch_scale_pow_bitrev(st, evals, (int)log_n, hgl_mul(shift, hgl_inv(3)), scratch) == hipSuccess;
     }
     const uint64_t inv_n = hgl_inv((1ULL << log_n) % GL_P_HOST);
     const DeepFuse dfuse{z, logN, 0, 0};
     bool deep_fused = false;
-    if (ntt_dit(st, out, logN, false, T, evals, (int)log_n, inv_n, 0, shift == 3 ? &dfuse : nullptr, &deep_fused) !=
-        hipSuccess)
-      return SEZKP_E_DEVICE;
-    if (!deep_fused && launch_deep(st, out, logN, z, T, 0, 0, shift) != hipSuccess) return SEZKP_E_DEVICE;
-    if (leaves32 && launch_leaves_u64(st, out, 1ULL << logN, reinterpret_cast<uint32_t*>(leaves32)) != hipSuccess)
-      return SEZKP_E_DEVICE;
-    if (scratch) HIP_OR_THROW(hipFreeAsync(scratch, st));
-    return SEZKP_OK;
+    ok = ok && ntt_dit(st, out, logN, false, T, evals, (int)log_n, inv_n, 0, shift == 3 ? &dfuse : nullptr,
+                       &deep_fused) == hipSuccess;
+    ok = ok && (deep_fused || launch_deep(st, out, logN, z, T, 0, 0, shift) == hipSuccess);
+    ok = ok && (!leaves32 ||
+                launch_leaves_u64(st, out, 1ULL << logN, reinterpret_cast<uint32_t*>(leaves32)) == hipSuccess);
+    if (scratch) (void)hipFreeAsync(scratch, st);  // stream-ordered: after the launches above
+    return ok ? SEZKP_OK : SEZKP_E_DEVICE;
   } catch (const Err& e) {
     return e.code;
   }
 }
 
 int32_t sezkp_fri_fold(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, void* stream) {
-  if (n_out == 0 || (n_out & (n_out - 1))) return SEZKP_E_INVALID;
+  if (n_out == 0 || (n_out & (n_out - 1)) || n_out > KABI_MAX_N) return SEZKP_E_INVALID;
   if (launch_fold_any((hipStream_t)stream, in, out, n_out, beta % GL_P_HOST) != hipSuccess)
     return SEZKP_E_DEVICE;
   return SEZKP_OK;
 }
 
+// one lane per digest: grids stay below 2^31 workgroups
+constexpr uint64_t KABI_MAX_N = 1ULL << 38;
+
 int32_t sezkp_blake3_leaves_u64(const uint64_t* vals, uint64_t n, uint8_t* leaves32, void* stream) {
-  if (reinterpret_cast<uintptr_t>(leaves32) & 15) return SEZKP_E_INVALID;
+  if (n > KABI_MAX_N || (reinterpret_cast<uintptr_t>(leaves32) & 15)) return SEZKP_E_INVALID;
   if (launch_leaves_u64((hipStream_t)stream, vals, n, reinterpret_cast<uint32_t*>(leaves32)) != hipSuccess)
     return SEZKP_E_DEVICE;
   return SEZKP_OK;
@@ -1591,7 +1593,7 @@ int32_t sezkp_blake3_leaves_u64(const uint64_t* vals, uint64_t n, uint8_t* leave
 
 int32_t sezkp_blake3_leaves_labeled(const uint64_t* vals, uint64_t n, const char* label, uint32_t label_len,
                                     uint8_t* leaves32, void* stream) {
-  if (label_len > 44 || (label_len && !label) || (reinterpret_cast<uintptr_t>(leaves32) & 15))
+  if (n > KABI_MAX_N || label_len > 44 || (label_len && !label) || (reinterpret_cast<uintptr_t>(leaves32) & 15))
     return SEZKP_E_INVALID;
   const ColTemplate ct = make_template(0, 1, std::string(label ? label : "", label_len));
   if (launch_leaves_labeled((hipStream_t)stream, vals, n, ct, reinterpret_cast<uint32_t*>(leaves32)) != hipSuccess)
@@ -1617,12 +1619,14 @@ static MerkleLevels merkle_levels(uint64_t n) {
 }
 
 uint64_t sezkp_merkle_node_count(uint64_t n) {
+  if (n > KABI_MAX_N) return 0;
   const MerkleLevels L = merkle_levels(n);
   return L.off[L.depth] + 1;
 }
 
 int32_t sezkp_merkle_build(const uint8_t* leaves32, uint64_t n, uint8_t* nodes32, void* stream) {
-  if ((reinterpret_cast<uintptr_t>(nodes32) & 15) || (n && (reinterpret_cast<uintptr_t>(leaves32) & 15)))
+  if (n > KABI_MAX_N || (reinterpret_cast<uintptr_t>(nodes32) & 15) ||
+      (n && (reinterpret_cast<uintptr_t>(leaves32) & 15)))
     return SEZKP_E_INVALID;
   hipStream_t st = (hipStream_t)stream;
   const MerkleLevels L = merkle_levels(n);
@@ -1638,7 +1642,8 @@ int32_t sezkp_merkle_build(const uint8_t* leaves32, uint64_t n, uint8_t* nodes32
 
 int32_t sezkp_merkle_paths(const uint8_t* nodes32, uint64_t n, const uint64_t* idx, uint32_t q, uint8_t* out32,
                            void* stream) {
-  if ((reinterpret_cast<uintptr_t>(nodes32) & 15) || (reinterpret_cast<uintptr_t>(out32) & 15))
+  if (n > KABI_MAX_N || (uint64_t)q * 64 > KABI_MAX_N || (reinterpret_cast<uintptr_t>(nodes32) & 15) ||
+      (reinterpret_cast<uintptr_t>(out32) & 15))
     return SEZKP_E_INVALID;
   const MerkleLevels L = merkle_levels(n);
   if (launch_merkle_paths((hipStream_t)stream, reinterpret_cast<const uint32_t*>(nodes32), L, idx, q,
