@@ -1533,6 +1533,9 @@ int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir
   }
 }
 
+// kernel-level ABI: one lane per digest / element, so grids stay below 2^31 workgroups
+constexpr uint64_t KABI_MAX_N = 1ULL << 38;
+
 int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_blowup, uint64_t shift, uint64_t z,
                                 uint64_t* out, uint8_t* leaves32, void* stream) {
   try {
@@ -1580,9 +1583,6 @@ int32_t sezkp_fri_fold(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64
     return SEZKP_E_DEVICE;
   return SEZKP_OK;
 }
-
-// one lane per digest: grids stay below 2^31 workgroups
-constexpr uint64_t KABI_MAX_N = 1ULL << 38;
 
 int32_t sezkp_blake3_leaves_u64(const uint64_t* vals, uint64_t n, uint8_t* leaves32, void* stream) {
   if (n > KABI_MAX_N || (reinterpret_cast<uintptr_t>(leaves32) & 15)) return SEZKP_E_INVALID;
