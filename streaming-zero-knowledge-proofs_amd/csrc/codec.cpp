@@ -3,10 +3,12 @@
 // into the struct-of-arrays store (no DOM), so multi-GB block files stream.
 #include "codec.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <stdexcept>
+#include <thread>
 
 #include "host_crypto.h"
 
@@ -40,6 +42,14 @@ struct DecodeError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+// A map key as it lies in the input (no allocation): compared with literals.
+struct Key {
+  const char* p = nullptr;
+  size_t n = 0;
+  bool operator==(const char* lit) const { return strlen(lit) == n && !memcmp(p, lit, n); }
+  bool operator!=(const char* lit) const { return !(*this == lit); }
+};
+
 // ------------------------------------------------------------- CBOR pull
 class Cbor {
  public:
@@ -54,14 +64,14 @@ class Cbor {
     if (*p_ == 0xff) { p_++; return false; }
     return true;
   }
-  std::string key() {
+  Key key() {
     int mj; uint64_t v; bool ind;
     head(mj, v, ind);
     if (mj != 3 || ind) throw DecodeError("expected text key");
     need(v);
-    std::string s((const char*)p_, (size_t)v);
+    Key k{(const char*)p_, (size_t)v};
     p_ += v;
-    return s;
+    return k;
   }
   bool null() {
     need(1);
@@ -81,7 +91,7 @@ class Cbor {
     if (mj != 0) throw DecodeError("expected unsigned integer");
     return v;
   }
-  std::string text() { return key(); }
+  std::string text() { const Key k = key(); return std::string(k.p, k.n); }
   void skip() {
     int mj; uint64_t v; bool ind;
     head(mj, v, ind);
@@ -128,6 +138,8 @@ class Cbor {
 };
 
 // ------------------------------------------------------------- JSON pull
+inline bool js_space(char c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t'; }
+inline bool js_digit(char c) { return c >= '0' && c <= '9'; }
 class Json {
  public:
   Json(const char* p, size_t n) : p_(p), e_(p + n) {}
@@ -141,8 +153,21 @@ class Json {
     first_ = false;
     return true;
   }
-  std::string key() {
-    std::string k = str();
+  Key key() {
+    ws();
+    expect('"');
+    const char* b = p_;
+    while (p_ < e_ && *p_ != '"' && *p_ != '\\') p_++;
+    Key k{b, (size_t)(p_ - b)};
+    if (p_ < e_ && *p_ == '\\') {  // escaped key: decode into this parser's buffer
+      keybuf_.assign(b, k.n);
+      while (p_ < e_ && *p_ != '"') {
+        if (*p_ == '\\') { p_++; if (p_ >= e_) break; }
+        keybuf_.push_back(*p_++);
+      }
+      k = Key{keybuf_.data(), keybuf_.size()};
+    }
+    expect('"');
     ws();
     expect(':');
     first_ = false;
@@ -170,23 +195,23 @@ class Json {
     if (c == '"') { str(); return; }
     if (c == '[' || c == '{') {
       int64_t r = c == '[' ? begin_array() : begin_map();
-      while (more(r)) { if (c == '{') key(); skip(); }
+      while (more(r)) { if (c == '{') (void)key(); skip(); }
       return;
     }
-    while (p_ < e_ && *p_ != ',' && *p_ != ']' && *p_ != '}' && !isspace((unsigned char)*p_)) p_++;
+    while (p_ < e_ && *p_ != ',' && *p_ != ']' && *p_ != '}' && !js_space(*p_)) p_++;
   }
 
  private:
-  void ws() { while (p_ < e_ && isspace((unsigned char)*p_)) p_++; }
+  void ws() { while (p_ < e_ && js_space(*p_)) p_++; }
   void expect(char c) {
     ws();
     if (p_ >= e_ || *p_ != c) throw DecodeError(std::string("JSON: expected '") + c + "'");
     p_++;
   }
   uint64_t digits() {
-    if (p_ >= e_ || !isdigit((unsigned char)*p_)) throw DecodeError("JSON: expected number");
+    if (p_ >= e_ || !js_digit(*p_)) throw DecodeError("JSON: expected number");
     uint64_t v = 0;
-    while (p_ < e_ && isdigit((unsigned char)*p_)) {
+    while (p_ < e_ && js_digit(*p_)) {
       uint64_t d = *p_++ - '0';
       if (v > (UINT64_MAX - d) / 10) throw DecodeError("JSON: number overflow");
       v = v * 10 + d;
@@ -208,6 +233,7 @@ class Json {
   const char* p_;
   const char* e_;
   bool first_ = false;
+  std::string keybuf_;
 };
 
 template <class P>
@@ -217,7 +243,7 @@ void decode_tape_op(P& d, BlockStore& s) {
   uint64_t sym = 0;
   int64_t mv = 0;
   while (d.more(r)) {
-    std::string k = d.key();
+    const Key k = d.key();
     if (k == "write") {
       if (!d.null()) { has = true; sym = d.uint(); if (sym > 0xffff) throw DecodeError("write symbol > u16"); }
     } else if (k == "mv") {
@@ -245,7 +271,7 @@ void decode_block(P& d, BlockStore& s, BlockShape& sh) {
   s.version.push_back(0); s.block_id.push_back(0); s.step_lo.push_back(0); s.step_hi.push_back(0);
   s.ctrl_in.push_back(0); s.ctrl_out.push_back(0); s.in_head_in.push_back(0); s.in_head_out.push_back(0);
   while (d.more(r)) {
-    std::string k = d.key();
+    const Key k = d.key();
     if (k == "version") s.version.back() = (uint16_t)d.uint();
     else if (k == "block_id") s.block_id.back() = (uint32_t)d.uint();
     else if (k == "step_lo") s.step_lo.back() = d.uint();
@@ -260,7 +286,7 @@ void decode_block(P& d, BlockStore& s, BlockShape& sh) {
         int64_t m = d.begin_map();
         int64_t left = 0, right = 0;
         while (d.more(m)) {
-          std::string wk = d.key();
+          const Key wk = d.key();
           if (wk == "left") left = d.sint();
           else if (wk == "right") right = d.sint();
           else d.skip();
@@ -281,7 +307,7 @@ void decode_block(P& d, BlockStore& s, BlockShape& sh) {
     } else if (k == "movement_log") {
       int64_t m = d.begin_map();
       while (d.more(m)) {
-        std::string mk = d.key();
+        const Key mk = d.key();
         if (mk != "steps") { d.skip(); continue; }
         int64_t a = d.begin_array();
         while (d.more(a)) {
@@ -289,7 +315,7 @@ void decode_block(P& d, BlockStore& s, BlockShape& sh) {
           int64_t imv = 0;
           uint32_t ntape = 0;
           while (d.more(sm)) {
-            std::string sk = d.key();
+            const Key sk = d.key();
             if (sk == "input_mv") {
               imv = d.sint();
               if (imv < -128 || imv > 127) throw DecodeError("input_mv out of i8 range");
@@ -343,7 +369,7 @@ void decode_manifest(P& d, uint8_t root[32], uint32_t* n_leaves) {
   int64_t r = d.begin_map();
   bool got = false;
   while (d.more(r)) {
-    std::string k = d.key();
+    const Key k = d.key();
     if (k == "root") {
       int64_t a = d.begin_array();
       int i = 0;
@@ -389,6 +415,49 @@ void sort_meta(std::vector<MetaEntry>& meta) {
 
 }  // namespace
 
+// Host threads for block-file decoding: SEZKP_HOST_THREADS, else the
+// OpenMP budget of the process (OMP_NUM_THREADS), else the hardware, at most
+// 64; one thread per >= 4 MB of input.
+static unsigned decode_threads(size_t len) {
+  unsigned t = 0;
+  for (const char* v : {"SEZKP_HOST_THREADS", "OMP_NUM_THREADS"})
+    if (!t && getenv(v)) t = (unsigned)atoi(getenv(v));
+  if (!t) t = std::thread::hardware_concurrency();
+  t = std::min<unsigned>(std::max<unsigned>(t, 1), 64);
+  return (unsigned)std::min<size_t>(t, std::max<size_t>(1, len >> 22));
+}
+
+// Concatenate the per-range stores (blocks in range order) into `out`.
+static void merge_stores(std::vector<BlockStore>& parts, std::vector<BlockShape>& shapes, BlockStore& out, BlockShape& sh) {
+  auto cat = [&](auto field, auto shape_field) {
+    size_t total = 0;
+    for (auto& b : parts) total += (b.*field).size();
+    (out.*field).reserve(total);
+    for (auto& b : parts) (out.*field).insert((out.*field).end(), (b.*field).begin(), (b.*field).end());
+    (void)shape_field;
+  };
+  cat(&BlockStore::version, 0); cat(&BlockStore::ctrl_in, 0); cat(&BlockStore::ctrl_out, 0);
+  cat(&BlockStore::block_id, 0); cat(&BlockStore::off_in, 0); cat(&BlockStore::off_out, 0);
+  cat(&BlockStore::step_lo, 0); cat(&BlockStore::step_hi, 0);
+  cat(&BlockStore::in_head_in, 0); cat(&BlockStore::in_head_out, 0);
+  cat(&BlockStore::win_left, 0); cat(&BlockStore::win_right, 0);
+  cat(&BlockStore::input_mv, 0); cat(&BlockStore::mv, 0); cat(&BlockStore::has_write, 0); cat(&BlockStore::wsym, 0);
+  out.step_start.assign(1, 0);
+  for (auto& b : parts) {
+    const uint64_t base = out.step_start.back();
+    for (size_t k = 1; k < b.step_start.size(); k++) out.step_start.push_back(base + b.step_start[k]);
+  }
+  for (auto& x : shapes) {
+    sh.nwin.insert(sh.nwin.end(), x.nwin.begin(), x.nwin.end());
+    sh.nin.insert(sh.nin.end(), x.nin.begin(), x.nin.end());
+    sh.nout.insert(sh.nout.end(), x.nout.begin(), x.nout.end());
+    sh.ntape.insert(sh.ntape.end(), x.ntape.begin(), x.ntape.end());
+  }
+}
+
+// CBOR Vec<BlockSummary> (io.rs:57-65), one thread: finding the block
+// boundaries of a CBOR array takes a pass as long as decoding it (measured:
+// a skip pass + 8 decode threads 1.4 s against 0.65 s sequential at T = 2^21).
 bool decode_blocks_cbor(const uint8_t* data, size_t len, BlockStore& out, std::string& err) {
   try {
     Cbor d(data, len);
@@ -411,31 +480,66 @@ bool decode_blocks_json(const char* data, size_t len, BlockStore& out, std::stri
 }
 // JSON Lines: one BlockSummary object per line (io_jsonl.rs:43-84); a
 // trailing "\r" is trimmed, an empty line is an error naming its line number.
+// The file is cut at line ends into one range per host thread; each range
+// decodes into its own store, and the stores are concatenated in order. The
+// error reported is the one of the lowest failing line, as a sequential
+// reader would stop there.
 bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::string& err) {
-  size_t line_no = 0;
-  try {
-    out.step_start.assign(1, 0);
-    BlockShape sh;
-    const char* p = data;
-    const char* e = data + len;
-    while (p < e) {
-      const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(e - p)));
-      const char* end = nl ? nl : e;
-      line_no++;
-      const char* le = end;
-      if (le > p && le[-1] == '\r') le--;
-      if (le == p) throw DecodeError("empty line");
-      Json d(p, (size_t)(le - p));
-      decode_block(d, out, sh);
-      if (!d.done()) throw DecodeError("trailing bytes after the block object");
-      p = nl ? nl + 1 : e;
+  const unsigned T = decode_threads(len);
+  std::vector<const char*> cut(T + 1, data + len);
+  cut[0] = data;
+  for (unsigned t = 1; t < T; t++) {
+    const char* p = std::max(cut[t - 1], data + len / T * t);
+    const char* nl = p < data + len ? static_cast<const char*>(memchr(p, '\n', (size_t)(data + len - p))) : nullptr;
+    cut[t] = nl ? nl + 1 : data + len;
+  }
+  std::vector<BlockStore> parts(T);
+  std::vector<BlockShape> shapes(T);
+  std::vector<size_t> lines(T, 0), bad_line(T, 0);
+  std::vector<std::string> msg(T);
+  auto run = [&](unsigned t) {
+    BlockStore& s = parts[t];
+    s.step_start.assign(1, 0);
+    const char* p = cut[t];
+    const char* e = cut[t + 1];
+    try {
+      while (p < e) {
+        const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(e - p)));
+        const char* end = nl ? nl : e;
+        lines[t]++;
+        const char* le = end;
+        if (le > p && le[-1] == '\r') le--;
+        if (le == p) throw DecodeError("empty line");
+        Json d(p, (size_t)(le - p));
+        decode_block(d, s, shapes[t]);
+        if (!d.done()) throw DecodeError("trailing bytes after the block object");
+        p = nl ? nl + 1 : e;
+      }
+    } catch (const std::exception& ex) {
+      bad_line[t] = lines[t];
+      msg[t] = ex.what();
     }
-    line_no = 0;
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < T; t++) th.emplace_back(run, t);
+  run(0);
+  for (auto& x : th) x.join();
+  size_t before = 0;
+  for (unsigned t = 0; t < T; t++) {
+    if (bad_line[t]) {
+      err = "parse jsonl line " + std::to_string(before + bad_line[t]) + ": " + msg[t];
+      return false;
+    }
+    before += lines[t];
+  }
+  try {
+    BlockShape sh;
+    merge_stores(parts, shapes, out, sh);
+    parts.clear();
     finish_blocks(out, sh);
     return true;
   } catch (const std::exception& ex) {
-    err = line_no ? "parse jsonl line " + std::to_string(line_no) + ": " + ex.what()
-                  : std::string("deserialize JSONL block summaries: ") + ex.what();
+    err = std::string("deserialize JSONL block summaries: ") + ex.what();
     return false;
   }
 }
@@ -572,7 +676,7 @@ bool decode_artifact_cbor(const uint8_t* data, size_t len, Artifact& out, std::s
     Cbor d(data, len);
     int64_t r = d.begin_map();
     while (d.more(r)) {
-      std::string k = d.key();
+      const Key k = d.key();
       if (k == "backend") out.backend = d.text();
       else if (k == "manifest_root" || k == "proof_bytes") {
         auto& v = k == "proof_bytes" ? out.proof_bytes : out.manifest_root;

@@ -49,3 +49,28 @@ def test_jsonl_synthetic_roundtrip(product):
     assert r.manifest_root() == b.manifest_root()
     for f in _fields(product):
         np.testing.assert_array_equal(getattr(r, f), getattr(b, f))
+
+
+def test_jsonl_parallel_ranges_match_sequential(product, monkeypatch):
+    """The reader cuts the file at line ends into one range per host thread
+    (>= 4 MB each) and concatenates the ranges in order: the same blocks as
+    one thread, and an error still names the first failing line of the file."""
+    b = product.synthetic_blocks(1 << 18, 100, 4, 7)  # ~30 MB of JSONL, ragged last block
+    data = b.to_jsonl()
+    assert len(data) > 6 * (4 << 20)
+    outs = []
+    for threads in ("1", "3", "6", "64"):
+        monkeypatch.setenv("SEZKP_HOST_THREADS", threads)
+        outs.append(product.BlockSoA.from_jsonl(data))
+    for r in outs:
+        assert r.tau == b.tau
+        for f in _fields(product):
+            np.testing.assert_array_equal(getattr(r, f), getattr(b, f))
+    lines = data.split(b"\n")
+    n = len(lines) - 1  # trailing newline
+    bad = list(lines)
+    bad[n - 2] = b"{\"version\": x}"   # in the last range
+    bad[n // 3] = b""                   # in an earlier range: reported first
+    monkeypatch.setenv("SEZKP_HOST_THREADS", "6")
+    with pytest.raises(product.SezkpError, match=f"line {n // 3 + 1}: empty line"):
+        product.BlockSoA.from_jsonl(b"\n".join(bad))
