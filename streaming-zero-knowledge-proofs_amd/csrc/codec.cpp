@@ -429,19 +429,18 @@ static unsigned decode_threads(size_t len) {
 
 // Concatenate the per-range stores (blocks in range order) into `out`.
 static void merge_stores(std::vector<BlockStore>& parts, std::vector<BlockShape>& shapes, BlockStore& out, BlockShape& sh) {
-  auto cat = [&](auto field, auto shape_field) {
+  auto cat = [&](auto field) {
     size_t total = 0;
     for (auto& b : parts) total += (b.*field).size();
     (out.*field).reserve(total);
     for (auto& b : parts) (out.*field).insert((out.*field).end(), (b.*field).begin(), (b.*field).end());
-    (void)shape_field;
   };
-  cat(&BlockStore::version, 0); cat(&BlockStore::ctrl_in, 0); cat(&BlockStore::ctrl_out, 0);
-  cat(&BlockStore::block_id, 0); cat(&BlockStore::off_in, 0); cat(&BlockStore::off_out, 0);
-  cat(&BlockStore::step_lo, 0); cat(&BlockStore::step_hi, 0);
-  cat(&BlockStore::in_head_in, 0); cat(&BlockStore::in_head_out, 0);
-  cat(&BlockStore::win_left, 0); cat(&BlockStore::win_right, 0);
-  cat(&BlockStore::input_mv, 0); cat(&BlockStore::mv, 0); cat(&BlockStore::has_write, 0); cat(&BlockStore::wsym, 0);
+  cat(&BlockStore::version); cat(&BlockStore::ctrl_in); cat(&BlockStore::ctrl_out);
+  cat(&BlockStore::block_id); cat(&BlockStore::off_in); cat(&BlockStore::off_out);
+  cat(&BlockStore::step_lo); cat(&BlockStore::step_hi);
+  cat(&BlockStore::in_head_in); cat(&BlockStore::in_head_out);
+  cat(&BlockStore::win_left); cat(&BlockStore::win_right);
+  cat(&BlockStore::input_mv); cat(&BlockStore::mv); cat(&BlockStore::has_write); cat(&BlockStore::wsym);
   out.step_start.assign(1, 0);
   for (auto& b : parts) {
     const uint64_t base = out.step_start.back();
