@@ -887,9 +887,9 @@ def measure_dist_ntt(args, world, rank, local, dist, torch):
     n = 1 << log_n
     per = dt / (2 * args.dntt_steps)
     alg = 16 * M / per / 1e9  # read + write each local element once, per GPU
-    return {"workload": f"2^{log_n}-point Goldilocks NTT over {world} GPU(s), forward + inverse (four-step: "
-                        f"local 2^{log_n - (world.bit_length() - 1)} NTT, twiddle, "
-                        f"{'1 RCCL all-to-all' if world > 1 else 'no exchange'}, {world}-point DFTs)",
+    shape = (f"four-step: local 2^{log_n - (world.bit_length() - 1)} NTT, twiddle, 1 RCCL all-to-all, "
+             f"{world}-point DFTs" if world > 1 else "one rank: local NTT + in-place bit reversal, no exchange")
+    return {"workload": f"2^{log_n}-point Goldilocks NTT over {world} GPU(s), forward + inverse ({shape})",
             "value": n / per, "unit": "field-elements/s", "ms_per_transform": per * 1e3, "steps": args.dntt_steps,
             "scaling": "strong", "roundtrip_ok": ok, "alg_GBs_per_gpu": alg, "frac_hbm_alg": alg / HBM_PEAK_GBS}
 

@@ -617,28 +617,44 @@ __global__ void k_bitrev_permute_small(const uint64_t* __restrict__ in, uint64_t
 // x[g + P j] (j < M) and, after a local M-point NTT Y_g (bit-reversed), this
 // kernel writes s[k2] = Y_g[k2] * w_N^(+-g k2) (* scale) in natural k2 order:
 // s is already the all-to-all send image (peer d gets k2 in [d M/P, (d+1) M/P)).
-// Same 16x16 LDS tile as k_bitrev_permute. The inverse transform runs the
+// 16x16 LDS tiles as k_bitrev_permute, TPW adjacent tiles per WG: a source
+// row of the WG is then 16 * TPW contiguous elements (512 B at TPW = 4), and
+// every lane has TPW loads in flight before the exchange. The inverse runs the
 // pipeline backwards and twiddles by the SOURCE index (tw_src = 1).
+template <int TPW>
 __global__ void __launch_bounds__(256) k_dntt_permute_twiddle(const uint64_t* __restrict__ in,
                                                                uint64_t* __restrict__ out, int logM, NttTables T,
                                                                uint64_t e_step, int inverse, int tw_src,
                                                                uint64_t scale) {
-  __shared__ uint64_t sh[16 * 17];
+  __shared__ uint64_t sh[TPW][16 * 17];
   const int a = 4, b = logM - 2 * a;
-  const uint32_t y = blockIdx.x;
+  const uint32_t y0 = blockIdx.x * TPW;
   const int tid = threadIdx.x;
-  const int x = tid >> 4, z = tid & 15;
-  const uint32_t ry = b ? (__brev(y) >> (32 - b)) : 0;
-  sh[x * 17 + z] = in[((uint64_t)x << (a + b)) | ((uint64_t)y << a) | z];
+  uint64_t v[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; i++) {  // element e = i*256 + tid: row x, tile y0 + t, column z
+    const int e = i * 256 + tid, x = e / (16 * TPW), t = (e / 16) % TPW, z = e & 15;
+    v[i] = in[((uint64_t)x << (a + b)) | ((uint64_t)(y0 + t) << a) | z];
+  }
+#pragma unroll
+  for (int i = 0; i < TPW; i++) {
+    const int e = i * 256 + tid, x = e / (16 * TPW), t = (e / 16) % TPW, z = e & 15;
+    sh[t][x * 17 + z] = v[i];
+  }
   __syncthreads();
   const int rz = tid >> 4, rx = tid & 15;
   const int zz = __brev((uint32_t)rz) >> 28, xx = __brev((uint32_t)rx) >> 28;
-  const uint64_t k2 = ((uint64_t)rz << (a + b)) | ((uint64_t)ry << a) | rx;
-  const uint64_t src = ((uint64_t)xx << (a + b)) | ((uint64_t)y << a) | zz;
-  uint64_t v = sh[xx * 17 + zz];
-  if (e_step) v = gl_mul(v, tw_pow(T, (tw_src ? src : k2) * e_step, inverse != 0));
-  if (scale != 1) v = gl_mul(v, scale);
-  out[k2] = v;
+#pragma unroll
+  for (int t = 0; t < TPW; t++) {
+    const uint32_t y = y0 + t;
+    const uint32_t ry = b ? (__brev(y) >> (32 - b)) : 0;
+    const uint64_t k2 = ((uint64_t)rz << (a + b)) | ((uint64_t)ry << a) | rx;
+    const uint64_t src = ((uint64_t)xx << (a + b)) | ((uint64_t)y << a) | zz;
+    uint64_t w = sh[t][xx * 17 + zz];
+    if (e_step) w = gl_mul(w, tw_pow(T, (tw_src ? src : k2) * e_step, inverse != 0));
+    if (scale != 1) w = gl_mul(w, scale);
+    out[k2] = w;
+  }
 }
 
 // After the all-to-all r[g * Q + q] = rank g's s[d Q + q] (Q = M/P). In place:
@@ -946,8 +962,12 @@ hipError_t bitrev_inplace(hipStream_t st, uint64_t* a, int logN, uint64_t scale,
 hipError_t dntt_permute_twiddle(hipStream_t st, const uint64_t* in, uint64_t* out, int logM, const NttTables& T,
                                 uint64_t e_step, bool inverse, bool tw_src, uint64_t scale) {
   if (logM < 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_dntt_permute_twiddle, dim3(1u << (logM - 8)), dim3(256), 0, st, in, out, logM, T, e_step,
-                     inverse ? 1 : 0, tw_src ? 1 : 0, scale);
+  if (logM >= 10)
+    hipLaunchKernelGGL(k_dntt_permute_twiddle<4>, dim3(1u << (logM - 10)), dim3(256), 0, st, in, out, logM, T, e_step,
+                       inverse ? 1 : 0, tw_src ? 1 : 0, scale);
+  else
+    hipLaunchKernelGGL(k_dntt_permute_twiddle<1>, dim3(1u << (logM - 8)), dim3(256), 0, st, in, out, logM, T, e_step,
+                       inverse ? 1 : 0, tw_src ? 1 : 0, scale);
   return hipGetLastError();
 }
 hipError_t dntt_dft(hipStream_t st, uint64_t* r, int P, uint64_t Q, bool inverse) {

@@ -1423,7 +1423,8 @@ void* sezkp_ctx_stream(const sezkp_ctx* ctx) { return ctx ? (void*)ctx->st : nul
 // Distributed four-step NTT over the context's ranks (BASELINE
 // config 4). Forward: local M-point NTT (DIF) -> bit-reverse + w_N^(g k2)
 // twiddle into the send image -> one all-to-all -> in-place P-point DFTs.
-// Inverse: the same pipeline backwards, so the two round-trip in place.
+// Inverse: the same pipeline backwards, so the two round-trip in place. One
+// rank needs no send image: the transform is bit-reversed in place.
 int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, uint32_t log_n, int32_t dir,
                            char* err, size_t err_len) {
   try {
@@ -1443,17 +1444,23 @@ int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, u
     auto ok = [](hipError_t e, const char* what) {
       if (e != hipSuccess) throw Err{SEZKP_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
     };
-    if (!inv) {
+    const uint64_t inv_n = inv ? hgl_inv((1ULL << log_n) % GL_P_HOST) : 1;
+    if (P == 1) {  // no exchange: the twiddle is 1 and the permutation swaps tile pairs in place
+      if (!inv) {
+        ok(ntt_dif(st, local, logM, false, ctx->tw), "dist_ntt local");
+        ok(bitrev_inplace(st, local, logM, 1, false), "dist_ntt bitrev");
+      } else {
+        ok(bitrev_inplace(st, local, logM, inv_n, true), "dist_ntt bitrev");
+        ok(ntt_dit(st, local, logM, true, ctx->tw, nullptr, 0, 1), "dist_ntt local");
+      }
+    } else if (!inv) {
       ok(ntt_dif(st, local, logM, false, ctx->tw), "dist_ntt local");
       ok(dntt_permute_twiddle(st, local, scratch, logM, ctx->tw, e_step, false, false, 1), "dist_ntt twiddle");
-      if (P > 1) ctx->comm->alltoall(scratch, local, Q * 8, st);
-      else HIP_OR_THROW(hipMemcpyAsync(local, scratch, M * 8, hipMemcpyDeviceToDevice, st));
+      ctx->comm->alltoall(scratch, local, Q * 8, st);
       ok(dntt_dft(st, local, P, Q, false), "dist_ntt dft");
     } else {
-      const uint64_t inv_n = hgl_inv((1ULL << log_n) % GL_P_HOST);
       ok(dntt_dft(st, local, P, Q, true), "dist_ntt dft");
-      if (P > 1) ctx->comm->alltoall(local, scratch, Q * 8, st);
-      else HIP_OR_THROW(hipMemcpyAsync(scratch, local, M * 8, hipMemcpyDeviceToDevice, st));
+      ctx->comm->alltoall(local, scratch, Q * 8, st);
       ok(dntt_permute_twiddle(st, scratch, local, logM, ctx->tw, e_step, true, true, inv_n), "dist_ntt twiddle");
       ok(ntt_dit(st, local, logM, true, ctx->tw, nullptr, 0, 1), "dist_ntt local");
     }
