@@ -342,10 +342,42 @@ __device__ __forceinline__ void lds_to_narrow(const uint64_t* sh, uint64_t* __re
   }
 }
 
-template <bool DIF, bool INV, int M1, int M2, int SKIP, bool DEEP = false, bool NARROW = false>
+// X16 (a NARROW pass extended by one radix-16 step inside its tile): a
+// NARROW tile is 16 * R contiguous points, so it also holds every 16-point
+// sub-transform {row + R t : t < 16} of the neighbouring pass with sL = log R.
+// One thread per row runs it on the LDS image (element (row, t) at
+// sh[row * NTT_PADC + t]) with the pass twiddle w_{16R}^(row * rev4(t)),
+// pre-multiplied for DIT (after the R-point stages), post-multiplied for DIF
+// (before them). A 2^12 tile then does 12 stages with one HBM round trip.
+template <int R, bool DIF, bool INV>
+__device__ __forceinline__ void tile_radix16(uint64_t* sh, const NttTables& T) {
+  constexpr int m = __builtin_ctz(R);
+  const int row = threadIdx.x;
+  if (row >= R) return;
+  uint64_t x[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) x[t] = sh[row * NTT_PADC + t];
+  if constexpr (DIF) fft_dif_regs<4, INV>(x);
+  if (row) {  // x[rev4(q)] *= w^(row q), the chain applied as it goes
+    const uint64_t s1 = tw_pow(T, (uint64_t)row << (T.K - m - 4), INV);
+    uint64_t t = s1;
+#pragma unroll
+    for (int q = 1; q < 16; q++) {
+      x[rev<4>(q)] = gl_mul(x[rev<4>(q)], t);
+      if (q + 1 < 16) t = gl_mul(t, s1);
+    }
+  }
+  if constexpr (!DIF) fft_dit_regs<4, INV, 0>(x);
+#pragma unroll
+  for (int t = 0; t < 16; t++) sh[row * NTT_PADC + t] = x[t];
+}
+
+template <bool DIF, bool INV, int M1, int M2, int SKIP, bool DEEP = false, bool NARROW = false,
+          bool X16 = false>
 __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   constexpr int F1 = 1 << M1, F2 = 1 << M2, m = M1 + M2, R = 1 << m;
   static_assert(!(NARROW && DEEP), "the fused DEEP pass is a wide pass");
+  static_assert(!X16 || (NARROW && SKIP == 0), "the in-tile radix-16 step extends a plain NARROW pass");
   __shared__ uint64_t sh[R * NTT_PADC];
   __shared__ uint64_t W[R];
   const int tid = threadIdx.x;
@@ -369,6 +401,10 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   const bool staged_load = NARROW && !P.dp_rlo && !P.src;
   if (staged_load) narrow_to_lds<R>(sh, P.a, G.tile);
   __syncthreads();
+  if constexpr (X16 && DIF) {  // the previous DIF pass's 4 stages, in the tile
+    tile_radix16<R, true, INV>(sh, T);
+    __syncthreads();
+  }
   if constexpr (!DIF) {
     uint64_t x[F1];
     if (g < F2) {  // step 1: thread (c, u), registers r
@@ -449,6 +485,10 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
         for (int k1 = 0; k1 < F2; k1++) sh[(g + F1 * k1) * NTT_PADC + c] = y[k1];
       }
       __syncthreads();
+      if constexpr (X16) {  // the next DIT pass's 4 stages, in the tile
+        tile_radix16<R, false, INV>(sh, T);
+        __syncthreads();
+      }
       lds_to_narrow<R>(sh, P.a, G.tile);
     }
   } else {
@@ -526,6 +566,18 @@ static bool launch_ntt4(hipStream_t st, const NttPassArgs& P, unsigned tiles) {
     else                                                                                                       \
       hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, SK>), dim3(tiles), dim3(NTT_THREADS), 0, st, P);           \
   } while (0)
+  if (P.m > NTT_MMAX) {  // NARROW + in-tile radix-16 (plan_passes_x16)
+    if (P.sL != 0 || skip || P.src || P.dp_rlo || narrow_disabled()) return false;
+#define SEZKP_NTT4X(M1, M2) \
+  hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, 0, false, true, true>), dim3(tiles), dim3(NTT_THREADS), 0, st, P)
+    switch (P.m) {
+      case 12: SEZKP_NTT4X(4, 4); return true;
+      case 11: SEZKP_NTT4X(4, 3); return true;
+      case 10: SEZKP_NTT4X(3, 3); return true;
+      default: return false;
+    }
+#undef SEZKP_NTT4X
+  }
   switch (P.m * 4 + skip) {
     case 8 * 4 + 0: SEZKP_NTT4(4, 4, 0); return true;
     case 7 * 4 + 0: SEZKP_NTT4(4, 3, 0); return true;
@@ -574,31 +626,43 @@ __global__ void __launch_bounds__(256) k_bitrev_permute(const uint64_t* __restri
 }
 
 // In-place bit-reversal permutation (optionally scaled): the WG of middle bits
-// y also owns tile rev(y) (y <= rev(y)); both 16x16 tiles are read into LDS
-// before either is written, so tile pairs swap without a second buffer.
+// y also owns tile rev(y) (y <= rev(y)); both S x S tiles (S = 2^A) are read
+// into LDS before either is written, so tile pairs swap without a second
+// buffer. p = x 2^(A+b) + y 2^A + z -> rev_A(z) 2^(A+b) + rev_b(y) 2^A + rev_A(x):
+// reads and writes are S-element row segments (A = 4: 128 B, A = 5: 256 B;
+// the wider segments pay once the array no longer sits in the MALL).
+template <int A>
 __global__ void __launch_bounds__(256) k_bitrev_inplace(uint64_t* __restrict__ a, int logN, uint64_t scale,
                                                         int do_scale) {
-  __shared__ uint64_t sh[2][16 * 17];
-  const int A = 4, b = logN - 2 * A;
+  constexpr int S = 1 << A, PER = S * S / 256;
+  __shared__ uint64_t sh[2][S * (S + 1)];
+  const int b = logN - 2 * A;
   const uint32_t y = blockIdx.x;
   const uint32_t ry = b ? (__brev(y) >> (32 - b)) : 0;
   if (y > ry) return;
   const int tid = threadIdx.x;
-  const int x = tid >> 4, z = tid & 15;
-  uint64_t v0 = a[((uint64_t)x << (A + b)) | ((uint64_t)y << A) | z];
-  uint64_t v1 = a[((uint64_t)x << (A + b)) | ((uint64_t)ry << A) | z];
-  if (do_scale) {
-    v0 = gl_mul(v0, scale);
-    v1 = gl_mul(v1, scale);
+  uint64_t v0[PER], v1[PER];
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const int e = j * 256 + tid, x = e >> A, z = e & (S - 1);
+    v0[j] = a[((uint64_t)x << (A + b)) | ((uint64_t)y << A) | z];
+    v1[j] = a[((uint64_t)x << (A + b)) | ((uint64_t)ry << A) | z];
   }
-  sh[0][x * 17 + z] = v0;
-  sh[1][x * 17 + z] = v1;
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const int e = j * 256 + tid, x = e >> A, z = e & (S - 1);
+    sh[0][x * (S + 1) + z] = do_scale ? gl_mul(v0[j], scale) : v0[j];
+    sh[1][x * (S + 1) + z] = do_scale ? gl_mul(v1[j], scale) : v1[j];
+  }
   __syncthreads();
   // destination (rz, ry', rx) <- source (rev(rx), y', rev(rz)): tile y lands in tile ry and back
-  const int rz = tid >> 4, rx = tid & 15;
-  const int zz = __brev((uint32_t)rz) >> 28, xx = __brev((uint32_t)rx) >> 28;
-  a[((uint64_t)rz << (A + b)) | ((uint64_t)ry << A) | rx] = sh[0][xx * 17 + zz];
-  if (ry != y) a[((uint64_t)rz << (A + b)) | ((uint64_t)y << A) | rx] = sh[1][xx * 17 + zz];
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const int e = j * 256 + tid, rz = e >> A, rx = e & (S - 1);
+    const int zz = __brev((uint32_t)rz) >> (32 - A), xx = __brev((uint32_t)rx) >> (32 - A);
+    a[((uint64_t)rz << (A + b)) | ((uint64_t)ry << A) | rx] = sh[0][xx * (S + 1) + zz];
+    if (ry != y) a[((uint64_t)rz << (A + b)) | ((uint64_t)y << A) | rx] = sh[1][xx * (S + 1) + zz];
+  }
 }
 
 // Small transforms (logN < 8) fall back to a plain in-LDS pass per call.
@@ -876,10 +940,35 @@ static void plan_passes(int logN, int first_min, int* ms, int* np) {
   *np = passes;
 }
 
+// Plan with the sL = 0 pass extended by an in-tile radix-16 step (X16: m =
+// 10..12 in one 2^m-point tile) when that saves a pass: 2^17..2^20 take 2
+// passes instead of 3, 2^25..2^28 take 3 instead of 4. The other passes keep
+// m in [6, 8] (the register kernels). Returns false when it saves nothing.
+// The sL = 0 pass is first for DIT and last for DIF.
+static bool plan_passes_x16(int logN, bool dif, int* ms, int* np) {
+  if (ntt4_disabled() || narrow_disabled()) return false;
+  const int cur = std::max(1, (logN + NTT_MMAX - 1) / NTT_MMAX);
+  for (int f = 12; f >= 10; f--) {
+    const int r = logN - f;
+    if (r < 0) continue;
+    const int k = (r + 7) / 8;  // passes for the rest, each m in [6, 8]
+    if (6 * k > r || 1 + k >= cur || 1 + k > 8) continue;
+    const int base = k ? r / k : 0, rem = k ? r % k : 0;
+    int o = 0;
+    if (!dif) ms[o++] = f;
+    for (int i = 0; i < k; i++) ms[o++] = base + (i < rem ? 1 : 0);
+    if (dif) ms[o++] = f;
+    *np = o;
+    return true;
+  }
+  return false;
+}
+
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T) {
   if (logN == 0) return hipSuccess;
   int ms[8], np;
-  plan_passes(logN, 1, ms, &np);
+  const bool x16 = plan_passes_x16(logN, true, ms, &np);
+  if (!x16) plan_passes(logN, 1, ms, &np);
   int sL = logN;
   for (int i = 0; i < np; i++) {
     NttPassArgs P{};
@@ -887,6 +976,14 @@ hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     P.inverse = inverse ? 1 : 0; P.skip = 0;
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
     uint64_t tiles = (1ULL << logN) >> (P.m + logC);
+    if (P.m > NTT_MMAX) {  // X16 tile: 2^m contiguous points
+      P.logC = 4;
+      tiles = (1ULL << logN) >> P.m;
+      const bool ok = inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
+                              : launch_ntt4<true, false>(st, P, (unsigned)tiles);
+      if (!ok) return hipErrorInvalidValue;
+      continue;
+    }
     const bool fast = !ntt4_disabled() &&
                       (inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
                                : launch_ntt4<true, false>(st, P, (unsigned)tiles));
@@ -909,7 +1006,8 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
   if (logN == 0) return hipSuccess;
   if (dpoly && (!src || logN > 32 || log_src > logN)) return hipErrorInvalidValue;
   int ms[8], np;
-  plan_passes(logN, src ? 3 : 1, ms, &np);
+  const bool x16 = !src && plan_passes_x16(logN, false, ms, &np);  // the LDE's first pass loads src
+  if (!x16) plan_passes(logN, src ? 3 : 1, ms, &np);
   // DIT order: smallest strides first; ensure the first pass holds >= 3 stages for the LDE skip
   if (src && ms[0] < logN - log_src) return hipErrorInvalidValue;
   int sL = 0;
@@ -922,6 +1020,15 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     if (i == 0 && dpoly) { P.dp_rlo = dpoly->rlo; P.dp_rhi = dpoly->rhi; P.dp_logN = logN; }
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
     uint64_t tiles = (1ULL << logN) >> (P.m + logC);
+    if (P.m > NTT_MMAX) {  // X16 tile: 2^m contiguous points
+      P.logC = 4;
+      tiles = (1ULL << logN) >> P.m;
+      const bool ok = inverse ? launch_ntt4<false, true>(st, P, (unsigned)tiles)
+                              : launch_ntt4<false, false>(st, P, (unsigned)tiles);
+      if (!ok) return hipErrorInvalidValue;
+      sL += ms[i];
+      continue;
+    }
     // last pass, forward, 16 wide columns, M1 = 4 (m = 7 or 8), not the replicated first pass
     if (deep && fused && i == np - 1 && i > 0 && !inverse && !ntt4_disabled() && !deep_fused_disabled() &&
         logC == 4 && P.sL >= 4 && (P.m == 8 || P.m == 7)) {
@@ -953,9 +1060,21 @@ hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int
   return hipGetLastError();
 }
 
+// SEZKP_BITREV_A=4|5|6 overrides the tile side 2^A (A/B measurements)
+static int bitrev_tile_log(int logN) {
+  static const int forced = getenv("SEZKP_BITREV_A") ? atoi(getenv("SEZKP_BITREV_A")) : 0;
+  // measured (round 2): 2^26 round trip 2910 / 2782 / 2819 us at A = 4 / 5 / 6; 2^24 (MALL-resident) best at 4
+  int A = forced >= 4 && forced <= 6 ? forced : (logN >= 25 ? 5 : 4);
+  while (A > 4 && logN < 2 * A) A--;
+  return A;
+}
 hipError_t bitrev_inplace(hipStream_t st, uint64_t* a, int logN, uint64_t scale, bool do_scale) {
   if (logN < 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_bitrev_inplace, dim3(1u << (logN - 8)), dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
+  const int A = bitrev_tile_log(logN);
+  const dim3 grid(1u << (logN - 2 * A));
+  if (A == 6) hipLaunchKernelGGL(k_bitrev_inplace<6>, grid, dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
+  else if (A == 5) hipLaunchKernelGGL(k_bitrev_inplace<5>, grid, dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
+  else hipLaunchKernelGGL(k_bitrev_inplace<4>, grid, dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -158,9 +158,13 @@ def test_dist_ntt_matches_oracle(gpu_ok, world, log_n, seed):
         assert calls["alltoall"] == 2  # one transpose per direction
 
 
-@pytest.mark.parametrize("log_n", [8, 12, 20, 22])
+@pytest.mark.parametrize("log_n", [8, 12, 18, 20, 22, 25])
 def test_dist_ntt_one_rank_is_plain_ntt(gpu_ok, product, oracle, log_n):
+    """One rank: DIF forward + in-place bit reversal, and the inverse through
+    the DIT passes (12, 18, 20 and 25 take the in-tile radix-16 pass)."""
     torch = gpu_ok
+    if log_n >= 24:
+        oracle.use_mt(int(os.environ.get("OMP_NUM_THREADS", "8")))
     x = oracle.det_vec(1 << log_n, 40 + log_n)
     ctx = product.ProverContext(0)
     d = torch.from_numpy(x.view(np.int64).copy()).cuda()

@@ -32,9 +32,10 @@ def _host(t) -> np.ndarray:
     return t.cpu().numpy().view(np.uint64)
 
 
-@pytest.mark.parametrize("log_n", list(range(1, 13)) + [14, 16, 20])
+@pytest.mark.parametrize("log_n", list(range(1, 13)) + [14, 16, 17, 18, 19, 20])
 def test_ntt_roundtrip_matches_oracle(gpu_ok, product, oracle, log_n):
-    """ntt_roundtrip.rs:29-81 + exact forward values vs sezkp-ffts (config 2 at 2^20)."""
+    """ntt_roundtrip.rs:29-81 + exact forward values vs sezkp-ffts (config 2 at
+    2^20). 2^10..2^12 and 2^17..2^20 run the in-tile radix-16 (X16) pass."""
     torch = gpu_ok
     n = 1 << log_n
     x = oracle.det_vec(n, 2024)
@@ -48,7 +49,7 @@ def test_ntt_roundtrip_matches_oracle(gpu_ok, product, oracle, log_n):
     np.testing.assert_array_equal(_host(d), x)
 
 
-@pytest.mark.parametrize("log_n", [22, 24, 26])
+@pytest.mark.parametrize("log_n", [22, 24, 25, 26])
 def test_ntt_large_matches_openmp_oracle(gpu_ok, product, oracle, log_n):
     """The headline LDE size (2^24) and config 4's 2^26 on one device: every
     output of sezkp_gl_ntt against the OpenMP oracle (ntt.rs:79-155), and the
