@@ -627,8 +627,8 @@ def halves(done_t, t0):
 # and 64-bit ops), priced at 2 / 4 cycles per wave64 instruction
 NTT_FULL, NTT_HALF = 2142, 6510
 VALU_PEAK_NTT_MIX = VALU_PEAK * 2 * (NTT_FULL + NTT_HALF) / (2 * NTT_FULL + 4 * NTT_HALF)
-LDE_WIDE = "k_ntt4<false, false, 4, 4, 0, false, false>"    # passes 2.. of the LDE
-LDE_NARROW = "k_ntt4<false, false, 4, 4, 0, false, true>"   # pass 1: DEEP-polynomial coefficients, staged stores
+LDE_WIDE = "k_ntt4<false, false, 4, 4, 0, false, false, false>"    # passes 2.. of the LDE
+LDE_NARROW = "k_ntt4<false, false, 4, 4, 0, false, true, false>"   # pass 1: DEEP-polynomial coefficients, staged stores
 
 
 def roofline_ntt(args, torch, stages, N, T):
