@@ -1523,7 +1523,7 @@ int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir
     HIP_OR_THROW(hipGetDevice(&dev));
     const NttTables& T = tables_for_device(dev);
     hipStream_t st = (hipStream_t)stream;
-    if (log_n > 28 || (dir != 1 && dir != -1)) return SEZKP_E_INVALID;
+    if (log_n > 28 || (dir != 1 && dir != -1) || !d || (log_n < 8 && !scratch)) return SEZKP_E_INVALID;
     if (log_n == 0) return SEZKP_OK;
     const bool inv = dir < 0;
     if (ntt_dif(st, d, (int)log_n, inv, T) != hipSuccess) return SEZKP_E_DEVICE;
@@ -1552,7 +1552,7 @@ int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_bl
     hipStream_t st = (hipStream_t)stream;
     shift %= GL_P_HOST;
     z %= GL_P_HOST;
-    if (log_blowup > 3 || log_n + log_blowup > 28 || shift == 0) return SEZKP_E_INVALID;
+    if (log_blowup > 3 || log_n + log_blowup > 28 || shift == 0 || !evals || !out) return SEZKP_E_INVALID;
     if (leaves32 && (reinterpret_cast<uintptr_t>(leaves32) & 15)) return SEZKP_E_INVALID;
     const int logN = (int)(log_n + log_blowup);
     // every denominator shift w^i - z must be nonzero: (z / shift)^N != 1
@@ -1585,14 +1585,15 @@ int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_bl
 }
 
 int32_t sezkp_fri_fold(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, void* stream) {
-  if (n_out == 0 || (n_out & (n_out - 1)) || n_out > KABI_MAX_N) return SEZKP_E_INVALID;
+  if (n_out == 0 || (n_out & (n_out - 1)) || n_out > KABI_MAX_N || !in || !out) return SEZKP_E_INVALID;
   if (launch_fold_any((hipStream_t)stream, in, out, n_out, beta % GL_P_HOST) != hipSuccess)
     return SEZKP_E_DEVICE;
   return SEZKP_OK;
 }
 
 int32_t sezkp_blake3_leaves_u64(const uint64_t* vals, uint64_t n, uint8_t* leaves32, void* stream) {
-  if (n > KABI_MAX_N || (reinterpret_cast<uintptr_t>(leaves32) & 15)) return SEZKP_E_INVALID;
+  if (n > KABI_MAX_N || (reinterpret_cast<uintptr_t>(leaves32) & 15) || (n && (!vals || !leaves32)))
+    return SEZKP_E_INVALID;
   if (launch_leaves_u64((hipStream_t)stream, vals, n, reinterpret_cast<uint32_t*>(leaves32)) != hipSuccess)
     return SEZKP_E_DEVICE;
   return SEZKP_OK;
@@ -1600,7 +1601,8 @@ int32_t sezkp_blake3_leaves_u64(const uint64_t* vals, uint64_t n, uint8_t* leave
 
 int32_t sezkp_blake3_leaves_labeled(const uint64_t* vals, uint64_t n, const char* label, uint32_t label_len,
                                     uint8_t* leaves32, void* stream) {
-  if (n > KABI_MAX_N || label_len > 44 || (label_len && !label) || (reinterpret_cast<uintptr_t>(leaves32) & 15))
+  if (n > KABI_MAX_N || label_len > 44 || (label_len && !label) || (reinterpret_cast<uintptr_t>(leaves32) & 15) ||
+      (n && (!vals || !leaves32)))
     return SEZKP_E_INVALID;
   const ColTemplate ct = make_template(0, 1, std::string(label ? label : "", label_len));
   if (launch_leaves_labeled((hipStream_t)stream, vals, n, ct, reinterpret_cast<uint32_t*>(leaves32)) != hipSuccess)
@@ -1632,8 +1634,8 @@ uint64_t sezkp_merkle_node_count(uint64_t n) {
 }
 
 int32_t sezkp_merkle_build(const uint8_t* leaves32, uint64_t n, uint8_t* nodes32, void* stream) {
-  if (n > KABI_MAX_N || (reinterpret_cast<uintptr_t>(nodes32) & 15) ||
-      (n && (reinterpret_cast<uintptr_t>(leaves32) & 15)))
+  if (n > KABI_MAX_N || !nodes32 || (reinterpret_cast<uintptr_t>(nodes32) & 15) ||
+      (n && (!leaves32 || (reinterpret_cast<uintptr_t>(leaves32) & 15))))
     return SEZKP_E_INVALID;
   hipStream_t st = (hipStream_t)stream;
   const MerkleLevels L = merkle_levels(n);
@@ -1650,7 +1652,7 @@ int32_t sezkp_merkle_build(const uint8_t* leaves32, uint64_t n, uint8_t* nodes32
 int32_t sezkp_merkle_paths(const uint8_t* nodes32, uint64_t n, const uint64_t* idx, uint32_t q, uint8_t* out32,
                            void* stream) {
   if (n > KABI_MAX_N || (uint64_t)q * 64 > KABI_MAX_N || (reinterpret_cast<uintptr_t>(nodes32) & 15) ||
-      (reinterpret_cast<uintptr_t>(out32) & 15))
+      (reinterpret_cast<uintptr_t>(out32) & 15) || (q && (!nodes32 || !idx || !out32)))
     return SEZKP_E_INVALID;
   const MerkleLevels L = merkle_levels(n);
   if (launch_merkle_paths((hipStream_t)stream, reinterpret_cast<const uint32_t*>(nodes32), L, idx, q,
@@ -1661,7 +1663,7 @@ int32_t sezkp_merkle_paths(const uint8_t* nodes32, uint64_t n, const uint64_t* i
 
 int32_t sezkp_fri_fold_commit(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64_t* out, uint8_t* root32,
                               void* stream) {
-  if (n_out == 0 || (n_out & (n_out - 1))) return SEZKP_E_INVALID;
+  if (n_out == 0 || (n_out & (n_out - 1)) || n_out > KABI_MAX_N || !in || !out || !root32) return SEZKP_E_INVALID;
   const int L = ilog2(n_out);
   hipStream_t st = (hipStream_t)stream;
   uint32_t* nodes = nullptr;
@@ -1677,7 +1679,7 @@ int32_t sezkp_fri_fold_commit(const uint64_t* in, uint64_t n_out, uint64_t beta,
 }
 
 int32_t sezkp_merkle_root_u64(const uint64_t* vals, uint64_t n, uint8_t* root32, void* stream) {
-  if (n == 0 || (n & (n - 1))) return SEZKP_E_INVALID;
+  if (n == 0 || (n & (n - 1)) || n > KABI_MAX_N || !vals || !root32) return SEZKP_E_INVALID;
   const int L = ilog2(n);
   hipStream_t st = (hipStream_t)stream;
   uint32_t* nodes = nullptr;
@@ -1703,6 +1705,7 @@ struct sezkp_blocks {
   BlockStore s;
 };
 int32_t sezkp_blocks_decode_cbor(const uint8_t* data, size_t len, sezkp_blocks** out, char* err, size_t err_len) {
+  if (!out || (!data && len)) return SEZKP_E_INVALID;
   std::unique_ptr<sezkp_blocks> b(new sezkp_blocks());
   std::string e;
   if (!decode_blocks_cbor(data, len, b->s, e)) {
@@ -1713,6 +1716,7 @@ int32_t sezkp_blocks_decode_cbor(const uint8_t* data, size_t len, sezkp_blocks**
   return SEZKP_OK;
 }
 int32_t sezkp_blocks_decode_jsonl(const uint8_t* data, size_t len, sezkp_blocks** out, char* err, size_t err_len) {
+  if (!out || (!data && len)) return SEZKP_E_INVALID;
   std::unique_ptr<sezkp_blocks> b(new sezkp_blocks());
   std::string e;
   if (!decode_blocks_jsonl(reinterpret_cast<const char*>(data), len, b->s, e)) {

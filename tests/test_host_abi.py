@@ -134,3 +134,20 @@ def test_cli_rejects_jsonl_for_stark_and_mismatched_manifest(tmp_path):
                         "--manifest", os.path.join(GOLDEN, "ref_manifest.cbor"), "--out", str(tmp_path / "p.cbor")],
                        capture_output=True, text=True)
     assert r.returncode != 0 and "root mismatch" in r.stderr
+
+
+def test_kernel_abi_rejects_null_pointers_before_any_launch(product):
+    """Every kernel-level entry point checks its device pointers before it
+    touches HIP, so these return SEZKP_E_INVALID on a machine without a GPU."""
+    lib, E = product.lib, product._lib.SEZKP_E_INVALID
+    buf = C.create_string_buffer(64)
+    assert lib.sezkp_fri_fold(None, 4, 3, None, None) == E
+    assert lib.sezkp_blake3_leaves_u64(None, 8, None, None) == E
+    assert lib.sezkp_blake3_leaves_labeled(None, 8, b"x", 1, None, None) == E
+    assert lib.sezkp_merkle_build(None, 8, None, None) == E
+    assert lib.sezkp_merkle_paths(None, 8, None, 1, None, None) == E
+    assert lib.sezkp_fri_fold_commit(None, 4, 3, None, buf, None) == E
+    assert lib.sezkp_merkle_root_u64(None, 4, buf, None) == E
+    out = C.c_void_p()
+    assert lib.sezkp_blocks_decode_cbor(None, 10, C.byref(out), buf, 64) == E
+    assert lib.sezkp_blocks_decode_jsonl(b"{}", 2, None, buf, 64) == E
