@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <stdexcept>
+#include <system_error>
 #include <thread>
 
 #include "host_crypto.h"
@@ -520,7 +521,13 @@ bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::str
     }
   };
   std::vector<std::thread> th;
-  for (unsigned t = 1; t < T; t++) th.emplace_back(run, t);
+  for (unsigned t = 1; t < T; t++) {
+    try {
+      th.emplace_back(run, t);
+    } catch (const std::system_error&) {  // no thread to be had: decode the range here
+      run(t);
+    }
+  }
   run(0);
   for (auto& x : th) x.join();
   size_t before = 0;
