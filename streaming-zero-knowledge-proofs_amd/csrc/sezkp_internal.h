@@ -113,6 +113,7 @@ struct TraceDev {
   uint32_t* row_blk;          // [n]   (derived)
   uint8_t* row_flags;         // [n]   bit0 first, bit1 last (derived)
   int64_t* head;              // [tau][n] post-move head (derived)
+  int64_t* head_rng;          // [tau][nblk][2] per-block min / max of head (derived by k_expand)
 };
 
 struct Alphas {

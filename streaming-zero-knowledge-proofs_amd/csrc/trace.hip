@@ -57,11 +57,12 @@ __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) 
   }
   // head = block-local inclusive prefix sum of the tape's moves. One wave per
   // tape (no WG barriers): two rows per lane, 32-bit wave scan (|sum| <= 128
-  // rows * 128), 64-bit carry from lane 63.
+  // rows * 128), 64-bit carry from lane 63. The block's min / max head goes to
+  // head_rng, so the dictionary plan need not re-read the head columns.
   for (int tp = wave; tp < T.tau; tp += TR_THREADS / 64) {
     const int8_t* mv = T.mv + (uint64_t)tp * T.n;
     int64_t* hd = T.head + (uint64_t)tp * T.n;
-    int64_t carry = 0;
+    int64_t carry = 0, lo = INT64_MAX, hi = INT64_MIN;
     // even block start (n is even): a lane's row pair is one 2-byte load and
     // one 16-byte store
     const bool paired = (s & 1) == 0;
@@ -83,6 +84,14 @@ __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) 
         if (lane >= o) x += y;
       }
       const int64_t h1 = carry + (int64_t)x;  // through row r + 1
+      if (r < e) {
+        lo = min(lo, h1 - m1);
+        hi = max(hi, h1 - m1);
+      }
+      if (r + 1 < e) {
+        lo = min(lo, h1);
+        hi = max(hi, h1);
+      }
       if (paired && r + 1 < e) {
         *reinterpret_cast<longlong2*>(hd + r) = make_longlong2(h1 - m1, h1);
       } else {
@@ -90,6 +99,15 @@ __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) 
         if (r + 1 < e) hd[r + 1] = h1;
       }
       carry += __shfl(x, 63, 64);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, __shfl_xor(lo, o, 64));
+      hi = max(hi, __shfl_xor(hi, o, 64));
+    }
+    if (lane == 0) {
+      T.head_rng[2 * ((uint64_t)tp * T.nblk + b)] = lo;
+      T.head_rng[2 * ((uint64_t)tp * T.nblk + b) + 1] = hi;
     }
   }
 }
@@ -1001,9 +1019,11 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
 }
 
 constexpr int DICT_WG_ROWS = 64 << DICT_LANE_LOG;                    // 4096 rows per 64-lane WG
-constexpr int DICT_RANGE_ROWS = TR_THREADS * 16;                     // rows per range WG
+constexpr int DICT_RANGE_STEP = TR_THREADS * 16;                     // rows per WG sweep
+constexpr int DICT_RANGE_ROWS = DICT_RANGE_STEP * 8;                  // rows per range WG
 
-// per-(column, 4096 rows) min / max of the raw integers
+// per-(column, 32768 rows) min / max of the raw integers: 8 sweeps of 16 rows
+// per lane (one 16-byte-or-less load each), so the grid stays ~2K workgroups
 __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                            const DictCol* __restrict__ dcols,
                                                            int64_t* __restrict__ part, uint32_t nparts,
@@ -1011,29 +1031,34 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const Col
   __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
   const ColTemplate ct = tmpl[dcols[blockIdx.y].col];
   const int tid = threadIdx.x;
-  const uint64_t r0 = row0 + (uint64_t)blockIdx.x * DICT_RANGE_ROWS + (uint64_t)tid * 16;
   int64_t lo = INT64_MAX, hi = INT64_MIN;
-  if (r0 < row_end) {
-    int64_t k[16];
-    if (ct.kind == 6) {  // head: 64-bit keys
-      load_keys<int64_t, 16>(dict_keys<int64_t>(T, ct) + r0, k);
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        lo = k[i] < lo ? k[i] : lo;
-        hi = k[i] > hi ? k[i] : hi;
-      }
-    } else {  // narrow keys: 32-bit min / max
+  if (ct.kind == 6) {  // head: the per-block ranges of k_expand over the blocks meeting this part
+    const uint64_t p0 = row0 + (uint64_t)blockIdx.x * DICT_RANGE_ROWS;
+    const uint64_t p1 = p0 + DICT_RANGE_ROWS < row_end ? p0 + DICT_RANGE_ROWS : row_end;
+    const int64_t* hr = T.head_rng + 2 * ((uint64_t)ct.tape * T.nblk);
+    for (uint32_t b = T.row_blk[p0] + tid; b <= T.row_blk[p1 - 1]; b += TR_THREADS) {
+      lo = hr[2 * b] < lo ? hr[2 * b] : lo;
+      hi = hr[2 * b + 1] > hi ? hr[2 * b + 1] : hi;
+    }
+  } else {  // narrow keys: 32-bit min / max
+    int32_t l32 = INT32_MAX, h32 = INT32_MIN;
+    for (int sw = 0; sw < DICT_RANGE_ROWS / DICT_RANGE_STEP; sw++) {
+      const uint64_t r0 = row0 + (uint64_t)blockIdx.x * DICT_RANGE_ROWS + (uint64_t)sw * DICT_RANGE_STEP +
+                          (uint64_t)tid * 16;
+      if (r0 >= row_end) break;
+      int64_t k[16];
       switch (ct.kind) {
         case 0: case 3: load_keys<int8_t, 16>(dict_keys<int8_t>(T, ct) + r0, k); break;
         case 4: load_keys<uint8_t, 16>(dict_keys<uint8_t>(T, ct) + r0, k); break;
         default: load_keys<uint16_t, 16>(dict_keys<uint16_t>(T, ct) + r0, k); break;
       }
-      int32_t l32 = (int32_t)k[0], h32 = (int32_t)k[0];
 #pragma unroll
-      for (int i = 1; i < 16; i++) {
+      for (int i = 0; i < 16; i++) {
         l32 = min(l32, (int32_t)k[i]);
         h32 = max(h32, (int32_t)k[i]);
       }
+    }
+    if (l32 <= h32) {
       lo = l32;
       hi = h32;
     }
