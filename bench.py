@@ -244,7 +244,10 @@ def jsonl_threads(nbytes: int) -> int:
     t = 0
     for v in ("SEZKP_HOST_THREADS", "OMP_NUM_THREADS"):
         if not t and os.environ.get(v):
-            t = int(os.environ[v])
+            try:  # the C side reads it with atoi: garbage counts as unset
+                t = max(0, int(os.environ[v]))
+            except ValueError:
+                t = 0
     t = t or (os.cpu_count() or 1)
     return min(max(t, 1), 64, max(1, nbytes >> 22))
 
