@@ -1152,6 +1152,9 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   (void)hipEventElapsedTime(&tot, ev[0], ev[ST_NSTAGE]);
   stage_ms[ST_NSTAGE] = tot;
   have_times = true;
+  // an event pair not recorded on this path fails above; that error must not
+  // surface as the next launch's hipGetLastError()
+  (void)hipGetLastError();
 
   // ---- host-known parts of the body: counts, query headers, FRI roots,
   // positions, final value (prover.rs:242-243), manifest root
