@@ -38,6 +38,16 @@ __device__ __forceinline__ uint64_t pow3(const NttTables& T, uint64_t e) {
   return gl_mul(T.p3_hi[e >> T.S], T.p3_lo[e & ((1ULL << T.S) - 1)]);
 }
 
+// slot of coefficient e (= bitrev of the load position k) in the replicated
+// source: k itself after one n-point DIF INTT, or the sharded INTT's
+// allgathered layout (NttPassArgs::src_logP)
+__device__ __forceinline__ uint64_t src_slot(const NttPassArgs& P, uint64_t k, uint32_t e) {
+  if (!P.src_logP) return k;
+  const int lm = P.log_src - P.src_logP;
+  const uint64_t hi = (uint64_t)e >> P.src_logP;
+  return ((uint64_t)(e & ((1u << P.src_logP) - 1)) << lm) | (lm ? (__brev((uint32_t)hi) >> (32 - lm)) : 0);
+}
+
 // DEEP-quotient coefficient at bit-reversed position p of the N-point DIT
 // input: e = bitrev(p); the q part only where p's low b = log(N/n) bits are 0
 __device__ __forceinline__ uint64_t dp_load(const NttPassArgs& P, const NttTables& T, uint64_t p, int b) {
@@ -46,7 +56,7 @@ __device__ __forceinline__ uint64_t dp_load(const NttPassArgs& P, const NttTable
   if ((p & ((1ULL << b) - 1)) == 0) {
     const uint64_t k = p >> b;
     const uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;  // = e
-    uint64_t qv = gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk));
+    uint64_t qv = gl_mul(gl_mul(P.src[src_slot(P, k, rk)], P.inv_n), pow3(T, rk));
     if (P.coset_e) qv = gl_mul(qv, tw_pow(T, ((uint64_t)rk * P.coset_e) & ((1ULL << T.K) - 1), false));  // (w_N^g)^e
     v = gl_add(v, qv);
   }
@@ -94,7 +104,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(NttPassArgs P) {
     } else if (P.src) {  // LDE replicated load: B[2^skip k + s] = A[k] * n^-1 * (3 w^g)^bitrev(k)
       uint64_t k = pos >> P.skip;
       uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;
-      v = gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk));
+      v = gl_mul(gl_mul(P.src[src_slot(P, k, rk)], P.inv_n), pow3(T, rk));
       if (P.coset_e) v = gl_mul(v, tw_pow(T, ((uint64_t)rk * P.coset_e) & ((1ULL << T.K) - 1), false));
     } else {
       v = P.a[pos];
@@ -421,7 +431,7 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
         for (int r = 0; r < F1; r += (1 << SKIP)) {
           const uint64_t k = (p0 + r) >> P.skip;
           const uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;
-          uint64_t v = gl_mul(gl_mul(P.src[k], P.inv_n), pow3(T, rk));
+          uint64_t v = gl_mul(gl_mul(P.src[src_slot(P, k, rk)], P.inv_n), pow3(T, rk));
           if (P.coset_e) v = gl_mul(v, tw_pow(T, ((uint64_t)rk * P.coset_e) & ((1ULL << T.K) - 1), false));
 #pragma unroll
           for (int s = 0; s < (1 << SKIP); s++) x[r + s] = v;
@@ -745,6 +755,31 @@ __global__ void __launch_bounds__(256) k_dntt_dft(uint64_t* __restrict__ r, uint
   for (int k1 = 0; k1 < P; k1++) r[k1 * Q + q] = o[k1];
 }
 
+// Sharded INTT, first half (block layout in, see bintt_dft_twiddle): the
+// inverse P-point DFT over g (shifts only) and the four-step twiddle
+// w_n^-(j k1), j = d Q + q, generated from the tables per output.
+template <int P>
+__global__ void __launch_bounds__(256) k_bintt_dft_twiddle(uint64_t* __restrict__ r, uint64_t Q, uint64_t j0,
+                                                           int logn, NttTables T) {
+  const uint64_t q = blockIdx.x * 256ull + threadIdx.x;
+  if (q >= Q) return;
+  uint64_t v[P];
+#pragma unroll
+  for (int g = 0; g < P; g++) v[g] = r[g * Q + q];
+  const uint64_t j = j0 + q;
+#pragma unroll
+  for (int k1 = 0; k1 < P; k1++) {
+    uint64_t acc = v[0];
+#pragma unroll
+    for (int g = 1; g < P; g++) {
+      const int jj = (g * k1) % P;
+      acc = gl_add(acc, jj ? tw_small<true>(v[g], jj, P / 2) : v[g]);  // w_P^-jj
+    }
+    if (k1) acc = gl_mul(acc, tw_pow(T, ((j * (uint64_t)k1) << (T.K - logn)) & ((1ULL << T.K) - 1), true));
+    r[k1 * Q + q] = acc;
+  }
+}
+
 // ------------------------------------------- DEEP quotient (base domain)
 // See DeepPoly (sezkp_internal.h). k_inv_base: inv_j = 1 / (w_n^j - z) for
 // the base points j in [row0, row0 + nrows) (16 per lane, one Montgomery
@@ -1001,7 +1036,8 @@ static bool deep_fused_disabled() {  // SEZKP_NO_DEEP_FUSE=1: separate k_deep (A
 }
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
                    const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e, const DeepFuse* deep,
-                   bool* fused, const DeepPoly* dpoly) {
+                   bool* fused, const DeepPoly* dpoly, int src_logP) {
+  if (src_logP < 0 || src_logP > 3 || (src_logP && (!src || log_src < src_logP))) return hipErrorInvalidValue;
   if (fused) *fused = false;
   if (logN == 0) return hipSuccess;
   if (dpoly && (!src || logN > 32 || log_src > logN)) return hipErrorInvalidValue;
@@ -1016,6 +1052,7 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     P.a = a; P.tw = T; P.m = ms[i]; P.sL = sL; P.inverse = inverse ? 1 : 0;
     P.src = (i == 0) ? src : nullptr;
     P.log_src = log_src; P.inv_n = inv_n; P.coset_e = (i == 0) ? coset_e : 0;
+    P.src_logP = (i == 0) ? src_logP : 0;
     P.skip = (i == 0 && src && !dpoly) ? (logN - log_src) : 0;
     if (i == 0 && dpoly) { P.dp_rlo = dpoly->rlo; P.dp_rhi = dpoly->rhi; P.dp_logN = logN; }
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
@@ -1089,6 +1126,20 @@ hipError_t dntt_permute_twiddle(hipStream_t st, const uint64_t* in, uint64_t* ou
                        inverse ? 1 : 0, tw_src ? 1 : 0, scale);
   return hipGetLastError();
 }
+hipError_t bintt_dft_twiddle(hipStream_t st, uint64_t* r, int P, uint64_t Q, uint32_t d, int logn,
+                             const NttTables& T) {
+  if (Q == 0 || logn > T.K) return hipErrorInvalidValue;
+  const dim3 g((unsigned)((Q + 255) / 256));
+  const uint64_t j0 = (uint64_t)d * Q;
+  switch (P) {
+    case 2: hipLaunchKernelGGL(k_bintt_dft_twiddle<2>, g, dim3(256), 0, st, r, Q, j0, logn, T); break;
+    case 4: hipLaunchKernelGGL(k_bintt_dft_twiddle<4>, g, dim3(256), 0, st, r, Q, j0, logn, T); break;
+    case 8: hipLaunchKernelGGL(k_bintt_dft_twiddle<8>, g, dim3(256), 0, st, r, Q, j0, logn, T); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t dntt_dft(hipStream_t st, uint64_t* r, int P, uint64_t Q, bool inverse) {
   const dim3 g((unsigned)((Q + 255) / 256));
 #define SEZKP_DFT(PP)                                                                              \

@@ -914,7 +914,13 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   // f(z) are allgathered in between), then the q values are allgathered for
   // the n-point INTT every rank's coset needs; without the quotient the
   // composition values are allgathered as they are
-  if (sharded && !dq) comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st);
+  // sharded INTT over the ranks (block rows in, all n coefficients out): one
+  // all-to-all, P-point DFTs + twiddle, one all-to-all, a local (n/P)-point
+  // INTT, then the allgather every rank's coset needs anyway. Rank g's rows
+  // are [g n/P, (g+1) n/P) (n >= 4096 P). SEZKP_REPLICATED_INTT=1 gathers the
+  // n values and runs the n-point INTT on every rank instead.
+  const bool dist_intt = sharded && world > 1 && !getenv("SEZKP_REPLICATED_INTT");
+  if (sharded && !dq && !dist_intt) comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st);
   rec(4);
   DeepPoly dpoly{d_dq_rlo, d_dq_rhi};
   if (dq) {
@@ -940,14 +946,25 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
       ok(launch_q_tables(st, d_base, d_lde, d_dq_part, logn, logM, K1, K2, rho, hgl_pow(rho, 4096), d_dq_rlo, d_dq_rhi,
                          row_lo, nrows),
          "q_tables");
-      comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st);
+      if (!dist_intt) comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st);
     } else {
       ok(launch_deep_quotient(st, d_base, d_lde, d_dq_part, logn, logM, z, K1, K2, rho, hgl_pow(rho, 4096), d_dq_rlo,
                               d_dq_rhi, tw),
          "deep_quotient");
     }
   }
-  ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
+  if (dist_intt) {
+    const uint64_t m = n >> logP, Q = m >> logP;
+    if (row_lo != (uint64_t)rank * m || row_hi - row_lo != m) throw Err{SEZKP_E_INVALID, "sharded INTT: row split"};
+    uint64_t* blk = d_base + row_lo;
+    comm->alltoall(blk, d_lde, Q * 8, st);  // d_lde: r[g Q + t] = x[g m + rank Q + t]
+    ok(bintt_dft_twiddle(st, d_lde, world, Q, (uint32_t)rank, logn, tw), "intt_dft");
+    comm->alltoall(d_lde, blk, Q * 8, st);  // blk[j] = y_rank[j], j < m
+    ok(ntt_dif(st, blk, logn - logP, true, tw), "intt_local");  // slot p: n a_(rank + P bitrev(p))
+    comm->allgather(blk, d_base, m * 8, st);
+  } else {
+    ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
+  }
   rec(5);
   // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on
   // 3 w_N^g <w_M> (M = N/P), no communication
@@ -956,10 +973,13 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   const uint64_t coset_e = sharded ? ((uint64_t)rank << (tw.K - logN)) : 0;
   const DeepFuse dfuse{z, logN, logP, (uint32_t)rank};
   bool deep_fused = dq;
+  const int src_logP = dist_intt ? logP : 0;
   if (dq)
-    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, nullptr, nullptr, &dpoly), "lde_ntt");
+    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, nullptr, nullptr, &dpoly, src_logP),
+       "lde_ntt");
   else
-    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused), "lde_ntt");
+    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused, nullptr, src_logP),
+       "lde_ntt");
   rec(6);
   if (!deep_fused) ok(launch_deep(st, lde_out, logN, z, tw, logP, (uint32_t)rank), "deep");
   if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI

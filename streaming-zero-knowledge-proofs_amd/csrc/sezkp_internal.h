@@ -26,6 +26,10 @@ struct NttPassArgs {
   uint64_t inv_n;
   uint64_t coset_e;  // LDE load: extra factor w_{2^K}^(coset_e * bitrev(k)) (sharded coset), 0 = none
   int m, sL, logC, inverse, skip, log_src;
+  // src layout: 0 = the n coefficients bit-reversed (one n-point DIF INTT);
+  // s > 0 = the sharded INTT's allgather: coefficient e at
+  // (e mod 2^s) * (n >> s) + bitrev_{log n - s}(e >> s)
+  int src_logP;
   // fused DEEP on the last forward pass (k_ntt4<..., DEEP = true>)
   uint64_t deep_z;
   int deep_logN, deep_logP;
@@ -71,7 +75,8 @@ hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
 // allows; *fused says whether it did (else the caller runs launch_deep).
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
                    const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e = 0,
-                   const DeepFuse* deep = nullptr, bool* fused = nullptr, const DeepPoly* dpoly = nullptr);
+                   const DeepFuse* deep = nullptr, bool* fused = nullptr, const DeepPoly* dpoly = nullptr,
+                   int src_logP = 0);
 hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale,
                           bool do_scale);
 hipError_t bitrev_inplace(hipStream_t st, uint64_t* a, int logN, uint64_t scale, bool do_scale);  // logN >= 8
@@ -79,6 +84,11 @@ hipError_t bitrev_inplace(hipStream_t st, uint64_t* a, int logN, uint64_t scale,
 hipError_t dntt_permute_twiddle(hipStream_t st, const uint64_t* in, uint64_t* out, int logM, const NttTables& T,
                                 uint64_t e_step, bool inverse, bool tw_src, uint64_t scale);
 hipError_t dntt_dft(hipStream_t st, uint64_t* r, int P, uint64_t Q, bool inverse);
+// sharded INTT (block layout in): after the first all-to-all rank d holds
+// r[g Q + t] = x[g m + d Q + t] (m = n / P, Q = m / P); in place
+// r[k1 Q + t] = w_n^-(j k1) sum_g w_P^-(g k1) r[g Q + t], j = d Q + t
+hipError_t bintt_dft_twiddle(hipStream_t st, uint64_t* r, int P, uint64_t Q, uint32_t d, int logn,
+                             const NttTables& T);
 
 // A binary Merkle tree over 2^logLen leaves whose levels >= lstore are kept
 // in HBM: level l (lstore <= l <= logLen) starts at node

@@ -73,8 +73,9 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
     for rank, digest, repeat_ok, calls in res:
         assert digest == want, f"rank {rank}: {digest}"
         assert repeat_ok
-        # per prove: one all-to-all (LDE), one byte-sum (proof body), allgathers
-        assert calls["alltoall"] == 2 and calls["allreduce"] == 2 and calls["allgather"] > 0
+        # per prove: three all-to-alls (two for the INTT, one for the LDE), one
+        # byte-sum (proof body), allgathers
+        assert calls["alltoall"] == 6 and calls["allreduce"] == 2 and calls["allgather"] > 0
 
 
 def test_sharded_config5_size_p8_matches_openmp_oracle(gpu_ok, product):
@@ -109,6 +110,23 @@ def test_sharded_per_point_deep_matches_oracle(gpu_ok, product, oracle, monkeypa
     for rank, digest, repeat_ok, _ in _run(2, T, b, tau, seed):
         assert digest == want, f"rank {rank}: {digest}"
         assert repeat_ok
+
+
+@pytest.mark.parametrize("no_deep_poly", [False, True])
+def test_sharded_replicated_intt_matches_oracle(gpu_ok, product, oracle, monkeypatch, no_deep_poly):
+    """SEZKP_REPLICATED_INTT=1: the ranks gather all n base values and run the
+    n-point INTT each (the round-1 schedule) instead of the distributed INTT;
+    same bytes, one all-to-all per prove."""
+    monkeypatch.setenv("SEZKP_REPLICATED_INTT", "1")
+    if no_deep_poly:
+        monkeypatch.setenv("SEZKP_NO_DEEP_POLY", "1")
+    T, b, tau, seed = 1 << 14, 512, 3, 11
+    blocks = product.synthetic_blocks(T, b, tau, seed)
+    want = hashlib.sha256(oracle.prove_v1(blocks, blocks.manifest_root())).hexdigest()
+    for rank, digest, repeat_ok, calls in _run(4, T, b, tau, seed):
+        assert digest == want, f"rank {rank}: {digest}"
+        assert repeat_ok
+        assert calls["alltoall"] == 2
 
 
 def test_sharded_context_world1_is_single_gpu(gpu_ok, product, oracle):
