@@ -577,7 +577,8 @@ static bool launch_ntt4(hipStream_t st, const NttPassArgs& P, unsigned tiles) {
       hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, SK>), dim3(tiles), dim3(NTT_THREADS), 0, st, P);           \
   } while (0)
   if (P.m > NTT_MMAX) {  // NARROW + in-tile radix-16 (plan_passes_x16)
-    if (P.sL != 0 || skip || P.src || P.dp_rlo || narrow_disabled()) return false;
+    // plain passes, or the LDE's DEEP-polynomial first pass (all its stages: no skip)
+    if (P.sL != 0 || skip || (P.src && !P.dp_rlo) || narrow_disabled()) return false;
 #define SEZKP_NTT4X(M1, M2) \
   hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, 0, false, true, true>), dim3(tiles), dim3(NTT_THREADS), 0, st, P)
     switch (P.m) {
@@ -1042,7 +1043,9 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
   if (logN == 0) return hipSuccess;
   if (dpoly && (!src || logN > 32 || log_src > logN)) return hipErrorInvalidValue;
   int ms[8], np;
-  const bool x16 = !src && plan_passes_x16(logN, false, ms, &np);  // the LDE's first pass loads src
+  // X16 for plain transforms and for the DEEP-polynomial LDE (its first pass
+  // loads all 2^m points: no replication skip); not for the replicated load
+  const bool x16 = (!src || dpoly) && plan_passes_x16(logN, false, ms, &np);
   if (!x16) plan_passes(logN, src ? 3 : 1, ms, &np);
   // DIT order: smallest strides first; ensure the first pass holds >= 3 stages for the LDE skip
   if (src && ms[0] < logN - log_src) return hipErrorInvalidValue;

@@ -333,6 +333,28 @@ def test_prove_headline_size_matches_openmp_oracle(gpu_ok, product):
     assert got == out.strip()
 
 
+def test_prove_config5_size_one_gpu_matches_openmp_oracle(gpu_ok, product):
+    """Config 5's trace (T = 2^22, N = 2^25) proven on ONE device: the LDE's
+    first pass is an X16 tile (12 stages, DEEP-polynomial load), so the 2^25
+    transform takes 3 passes. Equal to the OpenMP oracle byte for byte."""
+    import sys
+    T, b, tau, seed = 1 << 22, 512, 8, 5
+    code = ("import sys; sys.path[:0]=[%r,%r]\n"
+            "import hashlib, oracle_ctypes as O, sezkp_amd as S\n"
+            "O.use_mt(16)\n"
+            "bl=S.synthetic_blocks(%d,%d,%d,%d); print(hashlib.sha256(O.prove_v1(bl, bl.manifest_root())).hexdigest())\n"
+            % (PKG, os.path.join(ROOT, "oracle"), T, b, tau, seed))
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    blocks = product.synthetic_blocks(T, b, tau, seed)
+    ctx = product.ProverContext(0)
+    ctx.upload(blocks)
+    got = hashlib.sha256(ctx.prove(blocks.manifest_root()).proof_bytes).hexdigest()
+    ctx.close()
+    out, err = child.communicate(timeout=300)
+    assert child.returncode == 0, err[-1500:]
+    assert got == out.strip()
+
+
 def test_reupload_reuses_workspace_bit_exact(gpu_ok, product, oracle):
     """upload() keeps the previous workspace for a trace of the same shape, so
     every buffer holds the old trace's data when the new proof starts: each
