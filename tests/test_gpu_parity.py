@@ -32,7 +32,7 @@ def _host(t) -> np.ndarray:
     return t.cpu().numpy().view(np.uint64)
 
 
-@pytest.mark.parametrize("log_n", list(range(1, 13)) + [14, 16, 17, 18, 19, 20])
+@pytest.mark.parametrize("log_n", list(range(1, 21)))
 def test_ntt_roundtrip_matches_oracle(gpu_ok, product, oracle, log_n):
     """ntt_roundtrip.rs:29-81 + exact forward values vs sezkp-ffts (config 2 at
     2^20). 2^10..2^12 and 2^17..2^20 run the in-tile radix-16 (X16) pass."""
