@@ -49,7 +49,7 @@ def test_ntt_roundtrip_matches_oracle(gpu_ok, product, oracle, log_n):
     np.testing.assert_array_equal(_host(d), x)
 
 
-@pytest.mark.parametrize("log_n", [22, 24, 25, 26])
+@pytest.mark.parametrize("log_n", [21, 22, 23, 24, 25, 26])
 def test_ntt_large_matches_openmp_oracle(gpu_ok, product, oracle, log_n):
     """The headline LDE size (2^24) and config 4's 2^26 on one device: every
     output of sezkp_gl_ntt against the OpenMP oracle (ntt.rs:79-155), and the
