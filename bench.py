@@ -588,7 +588,10 @@ def main():
                 out[key] = {"error": f"watchdog: no result within {args.sharded_timeout:.0f} s"}
                 print(json.dumps(out), flush=True)
             os._exit(3)
-        wd = threading.Timer(args.sharded_timeout, _bail)
+        # the other ranks wait longer: rank 0 enters late (it alone runs the
+        # configs) and must print the main line before any rank's exit makes
+        # the launcher tear the job down
+        wd = threading.Timer(args.sharded_timeout + (0 if rank == 0 else 300.0), _bail)
         wd.daemon = True
         wd.start()
         try:
