@@ -355,6 +355,29 @@ def test_prove_config5_size_one_gpu_matches_openmp_oracle(gpu_ok, product):
     assert got == out.strip()
 
 
+def test_prove_mapped_roots_bit_exact(gpu_ok, product, oracle):
+    """SEZKP_MAPPED_ROOTS=1 (tree kernels store roots into mapped host memory)
+    and the default (roots in device memory, copied at each transcript point)
+    give the oracle's bytes; the switch is read once per process, so the
+    mapped variant runs in a child."""
+    import sys
+    T, b, tau, seed = 1 << 12, 512, 8, 7
+    code = ("import sys; sys.path[:0]=[%r]\n"
+            "import hashlib, sezkp_amd as S\n"
+            "bl=S.synthetic_blocks(%d,%d,%d,%d); c=S.ProverContext(0); c.upload(bl)\n"
+            "print(hashlib.sha256(c.prove(bl.manifest_root()).proof_bytes).hexdigest())\n" % (PKG, T, b, tau, seed))
+    env = dict(os.environ, SEZKP_MAPPED_ROOTS="1")
+    child = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert child.returncode == 0, child.stderr[-1500:]
+    blocks = product.synthetic_blocks(T, b, tau, seed)
+    want = oracle.prove_v1(blocks, blocks.manifest_root())
+    ctx = product.ProverContext(0)
+    ctx.upload(blocks)
+    assert ctx.prove(blocks.manifest_root()).proof_bytes == want
+    ctx.close()
+    assert child.stdout.strip() == hashlib.sha256(want).hexdigest()
+
+
 def test_reupload_reuses_workspace_bit_exact(gpu_ok, product, oracle):
     """upload() keeps the previous workspace for a trace of the same shape, so
     every buffer holds the old trace's data when the new proof starts: each
