@@ -877,11 +877,6 @@ void orc_lde_deep(const uint64_t *base_vals, size_t n, unsigned blow_log2, uint6
 /* ========================================================================
  * prove_v1 — prover.rs:61-462
  * ====================================================================== */
-static int check_shape(const orc_blocks *b, char *err, size_t err_len) {
-    (void)b; (void)err; (void)err_len;
-    return 0;
-}
-
 typedef struct {
     trace_cols tc;
     col_commit *cc;
@@ -896,9 +891,7 @@ typedef struct {
 } prove_state;
 
 static int prove_front(const orc_blocks *b, const uint8_t mroot[32], prove_state *ps, char *err, size_t err_len) {
-    int rc = check_shape(b, err, err_len);
-    if (rc) return rc;
-    rc = build_cols(b, &ps->tc, err, err_len);
+    int rc = build_cols(b, &ps->tc, err, err_len);  /* shape errors are reported here */
     if (rc) return rc;
     trace_cols *tc = &ps->tc;
     size_t n = tc->n;
