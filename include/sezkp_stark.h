@@ -175,8 +175,9 @@ int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, u
  * (16-byte aligned), stream = hipStream_t (NULL = default stream).
  * Asynchronous on `stream`. Digest counts and lengths up to 2^38. */
 /* In-place NTT (dir=+1 forward, -1 inverse incl. n^-1), natural -> natural:
- * ntt.rs:79-155. `scratch` (2^log_n elements) is used below 2^8 points only and may be
- * null from 2^8 up. Null device pointers are rejected (SEZKP_E_INVALID) here and in
+ * ntt.rs:79-155. `scratch` (2^log_n elements, clobbered) is required below 2^8 points and
+ * may be null from 2^8 up; given at 2^19..2^22, the transform runs out of place through it
+ * and needs no bit-reversal pass (distinct from d). Null device pointers are rejected (SEZKP_E_INVALID) here and in
  * every kernel-level entry point below, before anything is launched. */
 int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir, void* stream);
 /* Coset LDE + DEEP (deep_coset_lde_stream, lde.rs:42-97): evals[2^log_n]

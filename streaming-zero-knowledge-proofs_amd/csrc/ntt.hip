@@ -352,6 +352,32 @@ __device__ __forceinline__ void lds_to_narrow(const uint64_t* sh, uint64_t* __re
   }
 }
 
+// nat_out: the tile's point p = tile * 16R + e holds frequency bitrev(p); it
+// goes straight to out[bitrev(p)] (one word per 128-B line per tile; the 16
+// tiles sharing those lines run back to back on one XCD, see nat_tile, so the
+// partial lines merge in its L2 before they are written back)
+template <int R>
+__device__ __forceinline__ void lds_to_natural(const uint64_t* sh, const NttPassArgs& P, uint64_t tile) {
+  constexpr int m = __builtin_ctz(R);
+  const uint64_t p0 = tile * (uint64_t)(NTT_CMAX * R);
+  const int sh_r = 32 - P.nat_logN;
+#pragma unroll
+  for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
+    const int e = j * NTT_THREADS + threadIdx.x;
+    uint64_t v = sh[(e & (R - 1)) * NTT_PADC + (e >> m)];
+    if (P.out_scale != 1) v = gl_mul(v, P.out_scale);
+    P.out[__brev((uint32_t)(p0 + e)) >> sh_r] = v;
+  }
+}
+// dispatch order of a nat_out pass: tiles T and T + j G (G = tiles / 16)
+// write the same output lines; 16 consecutive workgroups of one XCD
+// (workgroup b runs on XCD b mod 8) take one such group
+__device__ __forceinline__ uint64_t nat_tile(uint32_t b, uint32_t tiles) {
+  if (tiles % 128) return b;
+  const uint32_t xcd = b % 8, k = b / 8;
+  return (uint64_t)((k / 16) * 8 + xcd) + (uint64_t)(k % 16) * (tiles / 16);
+}
+
 // X16 (a NARROW pass extended by one radix-16 step inside its tile): a
 // NARROW tile is 16 * R contiguous points, so it also holds every 16-point
 // sub-transform {row + R t : t < 16} of the neighbouring pass with sL = log R.
@@ -396,7 +422,7 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   Tile G;
   G.sL = P.sL;
   G.m = m;
-  G.tile = blockIdx.x;
+  G.tile = (NARROW && P.nat_out) ? nat_tile(blockIdx.x, gridDim.x) : blockIdx.x;
   G.wide = (1ULL << G.sL) >= (uint64_t)NTT_CMAX;
   G.blk_base = 0;
   G.low0 = 0;
@@ -540,8 +566,9 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
         }
       }
       if (!NARROW) {
+        uint64_t* dst = P.out ? P.out : P.a;
 #pragma unroll
-        for (int qq = 0; qq < F1; qq++) P.a[tile_pos(G, q * F1 + qq, c, low)] = y[qq];
+        for (int qq = 0; qq < F1; qq++) dst[tile_pos(G, q * F1 + qq, c, low)] = y[qq];
       }
     }
     if constexpr (NARROW) {
@@ -551,7 +578,8 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
         for (int qq = 0; qq < F1; qq++) sh[(g * F1 + qq) * NTT_PADC + c] = y[qq];
       }
       __syncthreads();
-      lds_to_narrow<R>(sh, P.a, G.tile);
+      if (P.nat_out) lds_to_natural<R>(sh, P, G.tile);
+      else lds_to_narrow<R>(sh, P.a, G.tile);
     }
   }
 }
@@ -1088,6 +1116,44 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     sL += ms[i];
   }
   return hipGetLastError();
+}
+
+// SEZKP_NTT_BITREV_PASS=1: natural-order transforms keep the separate in-place
+// bit reversal (A/B comparison)
+static bool nat_disabled() {
+  static const bool off = getenv("SEZKP_NTT_BITREV_PASS") != nullptr;
+  return off;
+}
+bool ntt_dif_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse, const NttTables& T,
+                     uint64_t scale, hipError_t* err) {
+  *err = hipSuccess;
+  // measured (profiles/r02_ntt_nat_ab.txt): 1-5% faster at 2^19..2^22, slower from 2^24 (where the
+  // scattered lines no longer merge in L2 before write-back: 687 vs 577 us at 2^24)
+  if (!scratch || scratch == a || logN < 19 || logN > 22 || nat_disabled() || ntt4_disabled() || narrow_disabled())
+    return false;
+  int ms[8], np;
+  const bool x16 = plan_passes_x16(logN, true, ms, &np);
+  if (!x16) plan_passes(logN, 1, ms, &np);
+  if (np < 2) return false;
+  int sL = logN;
+  for (int i = 0; i < np; i++) {
+    NttPassArgs P{};
+    P.a = i == 0 ? a : scratch;
+    P.out = i == 0 ? scratch : nullptr;
+    P.tw = T; P.m = ms[i]; sL -= ms[i]; P.sL = sL;
+    P.inverse = inverse ? 1 : 0;
+    P.logC = 4;
+    uint64_t tiles = (1ULL << logN) >> (P.m + 4);
+    if (i == np - 1) {  // the narrow pass: sL = 0, tile of 16 * 2^m' contiguous points
+      P.out = a; P.nat_out = 1; P.nat_logN = logN; P.out_scale = scale;
+      if (P.m > NTT_MMAX) tiles = (1ULL << logN) >> P.m;
+    }
+    const bool ok = inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
+                            : launch_ntt4<true, false>(st, P, (unsigned)tiles);
+    if (!ok) { *err = hipErrorInvalidValue; return true; }
+  }
+  *err = hipGetLastError();
+  return true;
 }
 
 hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int logN, uint64_t scale, bool do_scale) {

@@ -1590,8 +1590,10 @@ int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir
     if (log_n > 28 || (dir != 1 && dir != -1) || !d || (log_n < 8 && !scratch)) return SEZKP_E_INVALID;
     if (log_n == 0) return SEZKP_OK;
     const bool inv = dir < 0;
-    if (ntt_dif(st, d, (int)log_n, inv, T) != hipSuccess) return SEZKP_E_DEVICE;
     const uint64_t scale = inv ? hgl_inv((1ULL << log_n) % GL_P_HOST) : 1;
+    hipError_t e = hipSuccess;  // 2^19..2^22: the last pass stores in natural order (scratch is clobbered)
+    if (ntt_dif_natural(st, d, scratch, (int)log_n, inv, T, scale, &e)) return e == hipSuccess ? SEZKP_OK : SEZKP_E_DEVICE;
+    if (ntt_dif(st, d, (int)log_n, inv, T) != hipSuccess) return SEZKP_E_DEVICE;
     if (log_n >= 8) {
       if (bitrev_inplace(st, d, (int)log_n, scale, inv) != hipSuccess) return SEZKP_E_DEVICE;
     } else {

@@ -39,6 +39,12 @@ struct NttPassArgs {
   const uint64_t* dp_rlo;
   const uint64_t* dp_rhi;
   int dp_logN;
+  // out-of-place DIF store (null = in place); nat_out: the last (narrow) DIF
+  // pass writes position p to out[bitrev_{nat_logN}(p)] * out_scale, i.e. the
+  // transform leaves in natural order without a bit-reversal pass
+  uint64_t* out;
+  int nat_out, nat_logN;
+  uint64_t out_scale;
 };
 // DEEP division y_i / (3 w_N^(g + P i) - z) fused into the LDE's last pass
 struct DeepFuse {
@@ -71,6 +77,11 @@ hipError_t launch_q_tables(hipStream_t st, uint64_t* C, const uint64_t* inv_scra
                            uint64_t row0, uint64_t nrows);
 
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
+// natural order in and out through `scratch` (n words): the first pass reads a
+// and writes scratch, the last scatters scratch back to a in natural order
+// (times scale). False = this size takes ntt_dif + a bit reversal instead.
+bool ntt_dif_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse, const NttTables& T,
+                     uint64_t scale, hipError_t* err);
 // deep != nullptr: fuse the DEEP division into the last pass when its shape
 // allows; *fused says whether it did (else the caller runs launch_deep).
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
