@@ -7,20 +7,22 @@ composition, INTT + coset LDE + DEEP, layer-0 and all FRI layer trees, query
 paths and column openings, bincode proof bytes back on the host) of a
 T = 2^21-row, tau = 8 trace (N = 8T = 2^24 LDE points).
 
-`value`: inputs resident in HBM when the timed region starts (the bench
-contract). Each of `inflight` contexts holds its own uploaded trace and
-re-proves it; contexts keep proofs in flight on one GPU, fed by persistent
-host threads from a shared ticket counter. A step = `inflight` proofs.
-value = N * proofs * ranks / max-over-ranks time. Warmup runs the same
-staggered pipeline, then the pipeline drains, and the timed steps run
-bracketed by barrier + sync.
+`value` is SURVEY 8(d)'s own definition of t: blocks resident in HOST memory
+-> proof bytes on the host (crates/sezkp-stark/src/lib.rs:129-141 takes
+&[BlockSummary]). Each of `inflight` resident contexts proves on its own
+worker; every proof uploads its own trace: the block arrays sit in pinned host
+memory and go over PCIe with hipMemcpyAsync on the context's copy stream into
+its spare trace image (sezkp_ctx_stage) while the context's previous proof
+runs. Contexts are fed by persistent host threads from a shared ticket
+counter. A step = `inflight` proofs; value = N * proofs * ranks / max-over-
+ranks time.
 
-`host_to_proof` is SURVEY 8(d)'s own definition, reported beside `value`:
-blocks resident in HOST memory -> proof bytes on the host
-(crates/sezkp-stark/src/lib.rs:129-141 takes &[BlockSummary]). Every timed
-proof uploads its own trace: the block arrays sit in pinned host memory and go
-over PCIe with hipMemcpyAsync on the context's copy stream into its spare
-trace image (sezkp_ctx_stage) while the context's previous proof runs.
+Timing: warmup proofs run straight into the timed ones in ONE continuous
+pipeline (no drain, the start stagger applied once); the window runs from the
+completion of the last warmup proof to the completion of the last proof and
+counts the steps * inflight proofs that complete inside it. The run is
+bracketed by barrier + device sync. `trace_resident` is the same pipeline with
+every trace already in HBM (the kernel-side throughput).
 
 Multi-GPU (--gpus N, launched by torch.distributed.run): one process per GPU,
 each proving its own traces (independent proofs, weak scaling, no data-path
@@ -28,7 +30,7 @@ collective); the barrier / max-time reduction runs over RCCL. With N > 1 the
 `sharded` object times ONE T = 2^21 proof over all N GPUs (strong scaling).
 
 Objects beside the headline:
-  host_to_proof — the same pipeline, every proof staging its own trace from pinned host memory
+  trace_resident — the same pipeline with the traces resident in HBM (no uploads)
   single_proof  — one proof at a time (latency), with the per-stage split
   roofline      — the dominant kernel, k_layer16 (the BLAKE3 Merkle tree over
                   the 2^24-point LDE): VALU-issue-bound; achieved wave64 VALU
@@ -411,44 +413,52 @@ def main():
     import gc
 
     def timed(pipe, steps, warmup):
-        pipe.run(max(1, warmup) * K)  # warmup: the same staggered pipeline
+        """One continuous pipeline run: `warmup` steps straight into `steps`
+        timed steps (no drain, no second stagger). The timed window runs from
+        the completion of the last warmup proof to the completion of the last
+        proof, and counts the steps * K proofs that complete inside it; the run
+        is bracketed by barrier + device sync on both sides."""
+        w = max(1, warmup) * K
         gc.collect()
         gc.disable()  # no collector pauses in the host threads while proofs are in flight
         barrier()
         c0 = time.process_time()
-        t0, _ = pipe.run(steps * K)
+        pipe.run(w + steps * K)
         barrier()
-        dt = time.perf_counter() - t0
-        cpu = (time.process_time() - c0) / dt
+        ts = sorted(pipe.done_t)
+        t_start, t_end = ts[w - 1], ts[-1]
+        dt = t_end - t_start
+        cpu = (time.process_time() - c0) / (ts[-1] - ts[0] + 1e-9)
         gc.enable()
         if dist:
             t = torch.tensor([dt], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        return dt, t0, cpu
+        return dt, halves(ts[w:], t_start), cpu
 
-    # ---- headline (`value`): traces resident in HBM, each context re-proving its own
-    pipe = Pipeline(ctxs, traces, roots, staged=False, stagger_s=stagger)
-    dt, t0, cpu_frac = timed(pipe, args.steps, args.warmup)
     total = args.steps * K
-    value = N * total * world / dt
+    upload_bytes = traces[0].mv.nbytes * 4 + traces[0].input_mv.nbytes
+    # ---- trace resident in HBM, each context re-proving its own (beside `value`)
+    pipe = Pipeline(ctxs, traces, roots, staged=False, stagger_s=stagger)
+    dt_r, halves_r, cpu_r = timed(pipe, args.steps, args.warmup)
     l0_conc = list(pipe.l0)
-    halves_ = halves(pipe.done_t, t0)
     resident_last = [(t, bytes(v)) for t, v in pipe.last]  # outside the timed region
+    resident = {"value": N * total * world / dt_r, "unit": "field-elements/s", "ms_per_proof": dt_r / total * 1e3,
+                "ms_per_step": dt_r / args.steps * 1e3, "halves_ms_per_proof": halves_r, "host_cpu_per_wall": cpu_r,
+                "note": "the same pipeline with every trace already resident in HBM (no uploads): the kernel-side "
+                        "throughput; not SURVEY 8(d)'s t"}
 
-    # ---- host blocks -> proof bytes, every proof stages its own trace
-    h2p = None
+    # ---- `value`, SURVEY 8(d): host blocks -> proof bytes, every proof stages its own trace
     last = resident_last
     if not args.no_host_to_proof:
         pipe.staged = True
-        dth, t0h, _ = timed(pipe, args.steps, args.warmup)
+        dt, halves_, cpu_frac = timed(pipe, args.steps, args.warmup)
         last = [(t, bytes(v)) for t, v in pipe.last]
-        h2p = {"value": N * total * world / dth, "unit": "field-elements/s", "ms_per_proof": dth / total * 1e3,
-               "ms_per_step": dth / args.steps * 1e3, "halves_ms_per_proof": halves(pipe.done_t, t0h),
-               "upload_bytes_per_proof": traces[0].mv.nbytes * 4 + traces[0].input_mv.nbytes,
-               "note": "SURVEY 8(d) t: blocks in pinned host memory -> proof bytes on the host; every timed proof "
-                       "uploads its own trace (hipMemcpyAsync on the context's copy stream into its spare trace "
-                       "image, overlapping the context's previous proof), same pipeline, same bracket as value"}
+        headline = "host_to_proof"
+    else:
+        dt, halves_, cpu_frac = dt_r, halves_r, cpu_r
+        headline = "trace_resident"
+    value = N * total * world / dt
     holds = list(pipe.cur)  # trace each context holds
     pipe.close()
     # consistency: each context's last timed proof (both pipelines) equals an
@@ -530,13 +540,21 @@ def main():
             "data": f"synthetic: the blocks `sezkp-cli simulate --t {T} --b {args.b} --tau {args.tau}` writes at seeds "
                     f"42..{41 + n_tr} (reference generator + partition, bit-exact restatement)",
             "config": {"workload": f"stark-v1 prove, T=2^{args.log_t} rows (N=2^{args.log_t + 3} LDE domain), "
-                                   f"b={args.b}, tau={args.tau}, trace resident in HBM, proof bytes on the host",
+                                   f"b={args.b}, tau={args.tau}, "
+                                   + ("blocks in pinned host memory -> proof bytes on the host (SURVEY 8(d) t: every "
+                                      "proof uploads its own trace over PCIe, staged while the context's previous "
+                                      "proof runs)" if headline == "host_to_proof" else
+                                      "trace resident in HBM, proof bytes on the host"),
+                       "value_is": headline, "upload_bytes_per_proof": upload_bytes,
                        "T": T, "N": N, "tau": args.tau, "b": args.b, "proof_bytes": proof_len,
                        "proofs_in_flight_per_gpu": K, "distinct_traces": n_tr,
                        "parallelism": f"replicas x{world}, {K} independent proofs in flight per GPU"},
             "halves_ms_per_proof": halves_, "host_cpu_per_wall": cpu_frac,
+            "timing": "one continuous pipeline: warmup proofs run straight into the timed ones; the window runs "
+                      "from the last warmup proof's completion to the last proof's completion (steps x inflight "
+                      "proofs complete inside it), barrier + device sync around the run",
             "proofs_consistent": consistent,
-            "host_to_proof": h2p,
+            "trace_resident": resident,
             "single_proof": {"value": N * nsp / dt1, "unit": "field-elements/s", "ms_per_proof": dt1 / nsp * 1e3,
                              "note": "one proof at a time on one context (rank 0), trace resident: the latency view; "
                                      "stages_ms and roofline come from this pass"},
@@ -617,15 +635,15 @@ def main():
 
 
 def halves(done_t, t0):
-    """Steady-state check: ms per proof between completions over the first and
-    the second half of the timed proofs, and the pipeline-fill latency (first
-    completion after t0). A slow first half would mean the warmup is short."""
+    """Steady-state check: ms per proof over the first and the second half of
+    the timed completions `done_t` (sorted), the window opening at `t0` (the
+    last warmup completion). Equal halves mean the pipeline was already full
+    when the window opened and did not drain inside it."""
     ts = sorted(done_t)
     if len(ts) < 4:
         return None
     h = len(ts) // 2
-    return {"first_half": (ts[h - 1] - ts[0]) / (h - 1) * 1e3, "second_half": (ts[-1] - ts[h - 1]) / (len(ts) - h) * 1e3,
-            "fill_ms": (ts[0] - t0) * 1e3}
+    return {"first_half": (ts[h - 1] - t0) / h * 1e3, "second_half": (ts[-1] - ts[h - 1]) / (len(ts) - h) * 1e3}
 
 
 # k_ntt4's static VALU mix (the plain 256-point pass, tools/isa_hist.py on ntt.hip):

@@ -101,9 +101,14 @@ int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_
  * this context switches to it, its kernels waiting for the copy on the
  * device. Allowed while a proof is in flight on the context (that is the
  * point: the upload of proof i+1 overlaps proof i). The view's arrays must
- * stay valid and unchanged until that prove has started; from pinned or
- * registered memory (sezkp_host_register) the copies are DMA. A trace of
- * another shape: SEZKP_E_INVALID (use sezkp_ctx_upload). */
+ * stay valid and unchanged until the proof that consumes them has completed
+ * (sezkp_ctx_prove / sezkp_ctx_prove_borrow returned, or sezkp_ctx_wait for
+ * sezkp_ctx_prove_async): from pinned or registered memory
+ * (sezkp_host_register) the copies are DMA that may still be reading them
+ * after the prove call that takes the staged trace has returned. The trace a
+ * proof reads is fixed when its prove call is made: a stage() issued right
+ * after sezkp_ctx_prove_async fills the other image and feeds the NEXT proof.
+ * A trace of another shape: SEZKP_E_INVALID (use sezkp_ctx_upload). */
 int32_t sezkp_ctx_stage(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len);
 /* Page-lock (hipHostRegister) / release caller memory, e.g. the SoA arrays a
  * ProvingBackend shim fills from &[BlockSummary], so staging copies are DMA. */
@@ -187,7 +192,8 @@ int32_t sezkp_gl_ntt(uint64_t* d, uint64_t* scratch, uint32_t log_n, int32_t dir
  * prover.rs:119). leaves32 != NULL also writes the N layer-0 leaf digests
  * BLAKE3(out[i] LE) (fri_stream.rs:37-41), 16-byte aligned. `evals` is
  * overwritten. SEZKP_E_INVALID when a denominator vanishes ((z/shift)^N = 1;
- * the prover nudges z off the coset, prover.rs:119-135) or shift = 0. */
+ * the prover nudges z off the coset, prover.rs:119-135), shift = 0, or
+ * N = 1 (log_n + log_blowup = 0). */
 int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_blowup, uint64_t shift, uint64_t z,
                                 uint64_t* out, uint8_t* leaves32, void* stream);
 /* FRI fold (prover.rs:208-230): out[i] = in[i] + beta*in[i+n_out], i < n_out
@@ -225,6 +231,12 @@ int32_t sezkp_merkle_paths(const uint8_t* nodes32, uint64_t n, const uint64_t* i
 /* ------------------------------------------------ host helpers (CPU)
  * Manifest leaf_hash + merkle_root (crates/sezkp-merkle/src/lib.rs:85-157). */
 int32_t sezkp_manifest_root(const sezkp_block_view* blocks, uint8_t out[32]);
+/* The streaming Frontier root (crates/sezkp-merkle/src/lib.rs:167-208) that
+ * commit_block_file / verify_block_file_against_manifest (lib.rs:259-330) use
+ * for .jsonl/.ndjson block files; .json/.cbor files use sezkp_manifest_root.
+ * The two differ at 7, 11, 13, 14, 15, 19, ... blocks (the reference's own
+ * frontier/batch mismatch, kept bit-exact). */
+int32_t sezkp_manifest_frontier_root(const sezkp_block_view* blocks, uint8_t out[32]);
 /* Decode a CBOR Vec<BlockSummary> (io.rs:57-65). The returned handle owns the
  * arrays a view points to; free with sezkp_blocks_free. */
 typedef struct sezkp_blocks sezkp_blocks;

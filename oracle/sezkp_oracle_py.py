@@ -163,6 +163,25 @@ def tree_levels(leaves):  # merkle.rs:46-71
     return levels
 
 
+def frontier_root(leaves):  # sezkp-merkle lib.rs:167-208 (Frontier push_leaf / finalize_root)
+    slots = []  # slots[l]: pending node at level l, or None
+    for h in leaves:
+        lvl = 0
+        while True:
+            if len(slots) <= lvl:
+                slots.append(None)
+            if slots[lvl] is None:
+                slots[lvl] = h
+                break
+            h, slots[lvl] = h2(slots[lvl], h), None
+            lvl += 1
+    acc = None
+    for node in reversed(slots):  # highest level first: parent(higher, lower)
+        if node is not None:
+            acc = node if acc is None else h2(acc, node)
+    return acc if acc is not None else b"\0" * 32
+
+
 def tree_open(levels, idx):  # merkle.rs:80-108
     idx %= len(levels[0])
     sibs = []

@@ -1,7 +1,7 @@
 // cli.cpp — `sezkp-cli` drop-in for the STARK path on MI355X:
 //   prove  --backend stark --blocks B --manifest M --out P [--stream] [--assume-committed]
 //   verify --backend stark --blocks B --manifest M --proof P [--assume-committed]
-//   commit --blocks B --out M
+//   commit --blocks B(.cbor|.json|.jsonl|.ndjson) --out M
 // Semantics follow crates/sezkp-cli/src/main.rs:429-578 (manifest precheck,
 // .json/.cbor block files only for prove/verify, write_proof_auto by extension)
 // and crates/sezkp-merkle/src/lib.rs:259-337 (commit / precheck).
@@ -49,6 +49,10 @@ bool write_file(const std::string& path, const std::vector<uint8_t>& data, std::
   return (bool)f;
 }
 
+bool is_jsonl_like(const std::string& path) {  // sezkp-merkle lib.rs:410-412
+  const std::string e = ext_lower(path);
+  return e == "jsonl" || e == "ndjson";
+}
 bool load_blocks(const std::string& path, BlockStore& bs, std::string& err) {  // io.rs:78-88
   const std::string e = ext_lower(path);
   std::vector<uint8_t> raw;
@@ -96,7 +100,25 @@ struct Args {
   std::string t = "32", b = "4", tau = "2";  // simulate defaults (main.rs:87-100)
 };
 
-int precheck(const Args& a, const BlockStore& bs) {  // verify_block_file_against_manifest
+// The blocks file of `commit` and of the precheck: .jsonl/.ndjson through the
+// line reader (io_jsonl.rs:43-84), .json/.cbor through read_block_summaries_auto
+bool load_blocks_any(const std::string& path, BlockStore& bs, std::string& err) {
+  if (!is_jsonl_like(path)) return load_blocks(path, bs, err);
+  std::vector<uint8_t> raw;
+  if (!read_file(path, raw, err)) return false;
+  return decode_blocks_jsonl((const char*)raw.data(), raw.size(), bs, err);
+}
+// commit_block_file (lib.rs:259-295): the Frontier root for JSON Lines, the
+// batch merkle_root otherwise
+void file_root(const std::string& path, const BlockStore& bs, uint8_t root[32]) {
+  if (is_jsonl_like(path)) manifest_frontier_root(bs.view, root);
+  else manifest_root(bs.view, root);
+}
+
+// verify_block_file_against_manifest (lib.rs:302-337), run on the blocks path
+// before anything else reads it (main.rs:454-457). `bs` keeps the decoded
+// blocks so a .json/.cbor file is read once.
+int precheck(const Args& a, BlockStore& bs) {
   uint8_t mroot[32], got[32];
   uint32_t nl = 0;
   std::string err;
@@ -104,7 +126,11 @@ int precheck(const Args& a, const BlockStore& bs) {  // verify_block_file_agains
     fprintf(stderr, "Error: blocks/manifest mismatch: %s\n", err.c_str());
     return 1;
   }
-  manifest_root(bs.view, got);
+  if (!load_blocks_any(a.blocks, bs, err)) {
+    fprintf(stderr, "Error: blocks/manifest mismatch: read blocks %s: %s\n", a.blocks.c_str(), err.c_str());
+    return 1;
+  }
+  file_root(a.blocks, bs, got);
   if (memcmp(got, mroot, 32) != 0) {
     fprintf(stderr, "Error: blocks/manifest mismatch: root mismatch: manifest=%s, recomputed=%s\n",
             hex(mroot, 32).c_str(), hex(got, 32).c_str());
@@ -118,13 +144,26 @@ int precheck(const Args& a, const BlockStore& bs) {  // verify_block_file_agains
   return 0;
 }
 
+// precheck unless --assume-committed, then the manifest, then the blocks
+// through read_block_summaries_auto (.json/.cbor only: a .jsonl file that
+// passed the precheck is refused here, as main.rs:503-513 does)
+int load_inputs(const Args& a, BlockStore& bs, uint8_t mroot[32]) {
+  std::string err;
+  bool have = false;
+  if (!a.assume) {
+    if (precheck(a, bs)) return 1;
+    have = !is_jsonl_like(a.blocks);
+  }
+  if (!load_manifest(a.manifest, mroot, nullptr, err)) { fprintf(stderr, "Error: reading manifest: %s\n", err.c_str()); return 1; }
+  if (!have && !load_blocks(a.blocks, bs, err)) { fprintf(stderr, "Error: reading blocks: %s\n", err.c_str()); return 1; }
+  return 0;
+}
+
 int cmd_prove(const Args& a) {
   std::string err;
   BlockStore bs;
-  if (!load_blocks(a.blocks, bs, err)) { fprintf(stderr, "Error: reading blocks: %s\n", err.c_str()); return 1; }
-  if (!a.assume && precheck(a, bs)) return 1;
   uint8_t mroot[32];
-  if (!load_manifest(a.manifest, mroot, nullptr, err)) { fprintf(stderr, "Error: reading manifest: %s\n", err.c_str()); return 1; }
+  if (load_inputs(a, bs, mroot)) return 1;
   sezkp_buf art{};
   char msg[512] = {0};
   const int32_t rc = sezkp_stark_v1_prove_artifact_cbor(&bs.view, mroot, a.stream ? SEZKP_FLAG_STREAMING : 0, &art,
@@ -166,10 +205,8 @@ int cmd_prove(const Args& a) {
 int cmd_verify(const Args& a) {
   std::string err;
   BlockStore bs;
-  if (!load_blocks(a.blocks, bs, err)) { fprintf(stderr, "Error: reading blocks: %s\n", err.c_str()); return 1; }
-  if (!a.assume && precheck(a, bs)) return 1;
   uint8_t mroot[32];
-  if (!load_manifest(a.manifest, mroot, nullptr, err)) { fprintf(stderr, "Error: reading manifest: %s\n", err.c_str()); return 1; }
+  if (load_inputs(a, bs, mroot)) return 1;
   std::vector<uint8_t> raw;
   if (!read_file(a.proof, raw, err)) { fprintf(stderr, "Error: reading proof artifact: %s\n", err.c_str()); return 1; }
   if (ext_lower(a.proof) != "cbor") { fprintf(stderr, "Error: only .cbor proof artifacts are supported for verify\n"); return 1; }
@@ -192,9 +229,9 @@ int cmd_verify(const Args& a) {
 int cmd_commit(const Args& a) {
   std::string err;
   BlockStore bs;
-  if (!load_blocks(a.blocks, bs, err)) { fprintf(stderr, "Error: read blocks %s: %s\n", a.blocks.c_str(), err.c_str()); return 1; }
+  if (!load_blocks_any(a.blocks, bs, err)) { fprintf(stderr, "Error: read blocks %s: %s\n", a.blocks.c_str(), err.c_str()); return 1; }
   uint8_t root[32];
-  manifest_root(bs.view, root);
+  file_root(a.blocks, bs, root);
   std::vector<uint8_t> out;
   if (ext_lower(a.out) == "cbor") out = encode_manifest_cbor(root, bs.view.n_blocks);
   else {

@@ -787,4 +787,43 @@ void manifest_root(const sezkp_block_view& v, uint8_t out[32]) {  // lib.rs:140-
   memcpy(out, lv.data(), 32);
 }
 
+// The streaming commitment the reference uses for .jsonl/.ndjson block files
+// (commit_block_file / verify_block_file_against_manifest, lib.rs:259-330):
+// Frontier::push_leaf (lib.rs:173-193) carries a leaf up through the occupied
+// levels like a binary counter; finalize_root (lib.rs:195-207) then folds the
+// leftover levels top-down as parent(higher, lower). That equals the batch root
+// only when every fold pairs equal-height subtrees; at 7, 11, 13, 14, 15, 19 ...
+// leaves it does not, and the reference commits this value, so it
+// is restated as written.
+void manifest_frontier_root(const sezkp_block_view& v, uint8_t out[32]) {
+  uint8_t level[64][32];  // level[l]: the pending 2^l-leaf subtree root (bit l of the count)
+  uint64_t occupied = 0;
+  uint8_t node[64];       // left || right of one parent
+  for (uint32_t k = 0; k < v.n_blocks; k++) {
+    uint8_t h[32];
+    manifest_leaf_hash(v, k, h);
+    int l = 0;
+    while (occupied >> l & 1) {  // a waiting left sibling: merge and carry
+      memcpy(node, level[l], 32);
+      memcpy(node + 32, h, 32);
+      blake3_oneshot(node, 64, h);
+      occupied &= ~(1ull << l);
+      l++;
+    }
+    memcpy(level[l], h, 32);
+    occupied |= 1ull << l;
+  }
+  if (!occupied) { memset(out, 0, 32); return; }
+  int l = 63 - __builtin_clzll(occupied);
+  uint8_t acc[32];
+  memcpy(acc, level[l], 32);
+  while (l-- > 0) {
+    if (!(occupied >> l & 1)) continue;
+    memcpy(node, acc, 32);
+    memcpy(node + 32, level[l], 32);
+    blake3_oneshot(node, 64, acc);
+  }
+  memcpy(out, acc, 32);
+}
+
 }  // namespace sezkp

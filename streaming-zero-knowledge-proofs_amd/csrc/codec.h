@@ -70,5 +70,7 @@ struct BinWriter {
 
 void manifest_leaf_hash(const sezkp_block_view& v, uint32_t k, uint8_t out[32]);
 void manifest_root(const sezkp_block_view& v, uint8_t out[32]);
+// Frontier root of the .jsonl commit path (lib.rs:167-208, 259-330)
+void manifest_frontier_root(const sezkp_block_view& v, uint8_t out[32]);
 
 }  // namespace sezkp

@@ -162,6 +162,14 @@ static bool roots_copied() {
   return on;
 }
 
+static int worker_delay_us() {
+  static const int us = [] {
+    const char* e = getenv("SEZKP_TEST_WORKER_DELAY_US");
+    return e ? atoi(e) : 0;
+  }();
+  return us;
+}
+
 struct sezkp_ctx {
   int device = 0;
   std::unique_ptr<AsyncSlot> async;
@@ -354,6 +362,9 @@ struct sezkp_ctx {
       uint8_t r[32];
       memcpy(r, a.root, 32);
       lk.unlock();
+      // test hook: hold the worker back so that a stage() issued right after
+      // prove_async runs before this proof starts (tests/test_gpu_parity.py)
+      if (const int us = worker_delay_us()) std::this_thread::sleep_for(std::chrono::microseconds(us));
       int32_t rc = SEZKP_OK;
       std::string m;
       size_t len = 0;
@@ -418,8 +429,12 @@ struct sezkp_ctx {
 
 void sezkp_ctx::upload(const sezkp_block_view& v) {
   HIP_OR_THROW(hipSetDevice(device));
+  // a stage() may still be copying into / transposing a slot on the copy
+  // stream: it must finish before its buffers become spares for this upload
+  std::lock_guard<std::mutex> lk(stage_mu);
   HIP_OR_THROW(hipStreamSynchronize(st));
   if (st2 != st) HIP_OR_THROW(hipStreamSynchronize(st2));
+  if (stc) HIP_OR_THROW(hipStreamSynchronize(stc));
   free_all(true);
   tau = v.tau;
   nblk = v.n_blocks;
@@ -838,7 +853,9 @@ void sezkp_ctx::take_staged() {
 
 size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   if (!loaded) throw Err{SEZKP_E_INVALID, "no trace uploaded"};
-  take_staged();
+  // the trace image was fixed by take_staged() in the public entry point that
+  // started this proof (for prove_async: before the worker runs, so a stage()
+  // issued right after prove_async fills the other slot, never this one)
   using clk = std::chrono::steady_clock;
   const auto t_enter = clk::now();
   double t_sync = 0, t_last = 0;
@@ -1385,6 +1402,7 @@ int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_
   try {
     if (!ctx || !manifest_root || !proof_bytes) throw Err{SEZKP_E_INVALID, "null argument"};
     if (ctx->busy()) throw Err{SEZKP_E_INVALID, "a proof is in flight on this context (call sezkp_ctx_wait)"};
+    ctx->take_staged();
     const size_t len = ctx->prove(manifest_root);
     proof_bytes->data = (uint8_t*)malloc(len ? len : 1);
     if (!proof_bytes->data) throw Err{SEZKP_E_NOMEM, "out of host memory"};
@@ -1406,6 +1424,7 @@ int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], 
   try {
     if (!ctx || !manifest_root || !data || !len) throw Err{SEZKP_E_INVALID, "null argument"};
     if (ctx->busy()) throw Err{SEZKP_E_INVALID, "a proof is in flight on this context (call sezkp_ctx_wait)"};
+    ctx->take_staged();
     *len = ctx->prove(manifest_root);
     *data = ctx->h_proof;
     return SEZKP_OK;
@@ -1618,7 +1637,10 @@ int32_t sezkp_gl_coset_lde_deep(uint64_t* evals, uint32_t log_n, uint32_t log_bl
     hipStream_t st = (hipStream_t)stream;
     shift %= GL_P_HOST;
     z %= GL_P_HOST;
-    if (log_blowup > 3 || log_n + log_blowup > 28 || shift == 0 || !evals || !out) return SEZKP_E_INVALID;
+    // N = 1 (log_n + log_blowup = 0) is rejected: the prover never asks for it
+    // (n = 1 still has N = 8) and the NTT/DEEP launches assume N >= 2
+    if (log_blowup > 3 || log_n + log_blowup == 0 || log_n + log_blowup > 28 || shift == 0 || !evals || !out)
+      return SEZKP_E_INVALID;
     if (leaves32 && (reinterpret_cast<uintptr_t>(leaves32) & 15)) return SEZKP_E_INVALID;
     const int logN = (int)(log_n + log_blowup);
     // every denominator shift w^i - z must be nonzero: (z / shift)^N != 1
@@ -1764,6 +1786,11 @@ int32_t sezkp_merkle_root_u64(const uint64_t* vals, uint64_t n, uint8_t* root32,
 int32_t sezkp_manifest_root(const sezkp_block_view* blocks, uint8_t out[32]) {
   if (!blocks || !out) return SEZKP_E_INVALID;
   manifest_root(*blocks, out);
+  return SEZKP_OK;
+}
+int32_t sezkp_manifest_frontier_root(const sezkp_block_view* blocks, uint8_t out[32]) {
+  if (!blocks || !out) return SEZKP_E_INVALID;
+  manifest_frontier_root(*blocks, out);
   return SEZKP_OK;
 }
 

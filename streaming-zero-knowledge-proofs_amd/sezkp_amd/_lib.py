@@ -31,7 +31,7 @@ EXPORTS = [
     "sezkp_blocks_encode_cbor", "sezkp_simulate_trace", "sezkp_simulate_blocks",
     "sezkp_ctx_prove_async", "sezkp_ctx_wait", "sezkp_ctx_stage", "sezkp_host_register", "sezkp_host_unregister",
     "sezkp_fri_fold", "sezkp_blake3_leaves_u64", "sezkp_blake3_leaves_labeled", "sezkp_merkle_node_count",
-    "sezkp_merkle_build", "sezkp_merkle_paths",
+    "sezkp_merkle_build", "sezkp_merkle_paths", "sezkp_manifest_frontier_root",
 ]
 
 
@@ -118,6 +118,7 @@ def _load():
     L.sezkp_fri_fold_commit.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_char_p, C.c_void_p]
     L.sezkp_merkle_root_u64.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p, C.c_void_p]
     L.sezkp_manifest_root.argtypes = [C.POINTER(BlockView), C.c_char_p]
+    L.sezkp_manifest_frontier_root.argtypes = [C.POINTER(BlockView), C.c_char_p]
     L.sezkp_blocks_decode_cbor.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p)] + E
     L.sezkp_blocks_decode_jsonl.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p)] + E
     L.sezkp_blocks_encode_jsonl.argtypes = [C.POINTER(BlockView), C.POINTER(Buf)]

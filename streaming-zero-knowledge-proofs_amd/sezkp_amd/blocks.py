@@ -73,9 +73,23 @@ class BlockSoA:
             pass
 
     def manifest_root(self) -> bytes:
+        """commit_blocks (sezkp-merkle lib.rs:214-222): the batch merkle_root."""
         out = C.create_string_buffer(32)
         lib.sezkp_manifest_root(C.byref(self.view()), out)
         return out.raw
+
+    def manifest_frontier_root(self) -> bytes:
+        """The streaming Frontier root (lib.rs:167-208) that the reference
+        commits and prechecks for .jsonl/.ndjson files (lib.rs:259-330)."""
+        out = C.create_string_buffer(32)
+        lib.sezkp_manifest_frontier_root(C.byref(self.view()), out)
+        return out.raw
+
+    def file_root(self, path: str) -> bytes:
+        """The manifest root the reference computes for a blocks file at `path`:
+        Frontier for .jsonl/.ndjson, batch merkle_root for .json/.cbor."""
+        ext = path.rsplit(".", 1)[-1].lower() if "." in path else ""
+        return self.manifest_frontier_root() if ext in ("jsonl", "ndjson") else self.manifest_root()
 
     @classmethod
     def from_cbor(cls, data: bytes) -> "BlockSoA":

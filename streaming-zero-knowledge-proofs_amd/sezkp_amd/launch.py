@@ -9,7 +9,9 @@ the manifest precheck (main.rs:454-457) unless --assume-committed, then ONE
 proof over all GPUs (`ShardedProverContext`: one process per GPU, RCCL over
 xGMI inside the library), written by rank 0 as the CBOR ProofArtifact
 (io.rs:176-183). Unlike the reference's stark path (io.rs:78-88), .jsonl/.ndjson
-block files are accepted (io_jsonl.rs:43-84), as config 5 requires.
+block files are accepted (io_jsonl.rs:43-84), as config 5 requires; their
+precheck uses the streaming Frontier root as the reference's
+verify_block_file_against_manifest does (sezkp-merkle lib.rs:302-330).
 --gpus 1 runs the single-GPU context. --comm host runs every rank on GPU 0
 with host-staged collectives (tests).
 """
@@ -31,8 +33,9 @@ def _port() -> int:
     return p
 
 
-def _read_manifest_root(path: str) -> bytes:
-    """Manifest file {root: [32 uints], n_leaves} (sezkp-merkle commit output), .cbor or .json."""
+def _read_manifest(path: str):
+    """Manifest file {root: [32 uints], n_leaves} (sezkp-merkle commit output),
+    .cbor or .json -> (root, n_leaves)."""
     import ctypes as C
     from ._lib import check, lib
     raw = open(path, "rb").read()
@@ -41,7 +44,19 @@ def _read_manifest_root(path: str) -> bytes:
     err = C.create_string_buffer(512)
     check(lib.sezkp_manifest_decode(raw, len(raw), int(path.lower().endswith(".json")), root, C.byref(n), err, 512),
           err)
-    return root.raw
+    return root.raw, n.value
+
+
+def _precheck(blocks, path: str, root: bytes, n_leaves: int) -> None:
+    """verify_block_file_against_manifest (sezkp-merkle lib.rs:302-337): the
+    Frontier root for .jsonl/.ndjson files, the batch root otherwise, then the
+    leaf count."""
+    got = blocks.file_root(path)
+    if got != root:
+        raise RuntimeError(f"blocks/manifest mismatch: root mismatch: manifest={root.hex()}, recomputed={got.hex()}")
+    if blocks.n_blocks != n_leaves:
+        raise RuntimeError(f"blocks/manifest mismatch: leaf count mismatch: manifest={n_leaves}, "
+                           f"recomputed={blocks.n_blocks}")
 
 
 def _worker(rank: int, world: int, port: int, args, q) -> None:
@@ -54,9 +69,9 @@ def _worker(rank: int, world: int, port: int, args, q) -> None:
         t0 = time.perf_counter()
         blocks = BlockSoA.from_file(args.blocks)
         t_load = time.perf_counter() - t0
-        root = _read_manifest_root(args.manifest)
-        if not args.assume_committed and blocks.manifest_root() != root:
-            raise RuntimeError("manifest root mismatch: blocks do not match the committed manifest")
+        root, n_leaves = _read_manifest(args.manifest)
+        if not args.assume_committed:
+            _precheck(blocks, args.blocks, root, n_leaves)
         dev = 0 if args.comm == "host" else rank
         ctx = ShardedProverContext(rank, world, device=dev, comm=args.comm)
         ctx.upload(blocks)
@@ -125,10 +140,13 @@ def prove(args) -> int:
         from . import ProverContext
         from .blocks import BlockSoA
         blocks = BlockSoA.from_file(args.blocks)
-        root = _read_manifest_root(args.manifest)
-        if not args.assume_committed and blocks.manifest_root() != root:
-            print("error: manifest root mismatch", file=sys.stderr)
-            return 1
+        root, n_leaves = _read_manifest(args.manifest)
+        if not args.assume_committed:
+            try:
+                _precheck(blocks, args.blocks, root, n_leaves)
+            except RuntimeError as e:
+                print(f"error: {e}", file=sys.stderr)
+                return 1
         ctx = ProverContext(0)
         ctx.upload(blocks)
         art = ctx.prove(root, streaming=args.stream)

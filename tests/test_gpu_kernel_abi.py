@@ -150,3 +150,13 @@ def test_coset_lde_deep_rejects_vanishing_denominator(gpu_ok, product, oracle):
                                                None) == L.SEZKP_E_INVALID
     assert product.lib.sezkp_gl_coset_lde_deep(d_in.data_ptr(), log_n, 3, 0, 1, d_out.data_ptr(), None,
                                                None) == L.SEZKP_E_INVALID
+    # N = 1 (log_n = log_blowup = 0) is rejected before anything is launched;
+    # N = 2 from one point (log_blowup = 1) still works
+    assert product.lib.sezkp_gl_coset_lde_deep(d_in.data_ptr(), 0, 0, 3, 5, d_out.data_ptr(), None,
+                                               None) == L.SEZKP_E_INVALID
+    one = oracle.det_vec(1, 3)
+    d1 = _dev(torch, one)
+    d2 = torch.empty(2, dtype=torch.int64, device="cuda")
+    assert product.lib.sezkp_gl_coset_lde_deep(d1.data_ptr(), 0, 1, 3, 5, d2.data_ptr(), None, None) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d2), oracle.lde_deep_shift(one, 1, 3, 5))

@@ -125,11 +125,14 @@ def test_cli_commit_reproduces_reference_manifest(tmp_path):
 
 
 def test_cli_rejects_jsonl_for_stark_and_mismatched_manifest(tmp_path):
+    import sezkp_amd
     cli = os.path.join(PKG, "bin", "sezkp-cli")
-    r = subprocess.run([cli, "prove", "--backend", "stark", "--blocks", str(tmp_path / "x.jsonl"), "--manifest",
+    jl = tmp_path / "x.jsonl"  # a real JSONL file of the reference's blocks (8 blocks: Frontier == batch root)
+    jl.write_bytes(sezkp_amd.BlockSoA.from_cbor(open(os.path.join(GOLDEN, "ref_blocks.cbor"), "rb").read()).to_jsonl())
+    r = subprocess.run([cli, "prove", "--backend", "stark", "--blocks", str(jl), "--manifest",
                         os.path.join(GOLDEN, "ref_manifest.cbor"), "--out", str(tmp_path / "p.cbor")],
                        capture_output=True, text=True)
-    assert r.returncode != 0 and "unsupported blocks extension" in r.stderr
+    assert r.returncode != 0 and "unsupported blocks extension: jsonl" in r.stderr, r.stderr
     r = subprocess.run([cli, "prove", "--backend", "stark", "--blocks", os.path.join(GOLDEN, "riscv_blocks.cbor"),
                         "--manifest", os.path.join(GOLDEN, "ref_manifest.cbor"), "--out", str(tmp_path / "p.cbor")],
                        capture_output=True, text=True)

@@ -31,8 +31,8 @@ def test_jsonl_matches_cbor_and_serde_layout(product, blocks_path, manifest_path
         for f in _fields(product):
             np.testing.assert_array_equal(getattr(b, f), getattr(b_cbor, f))
         assert b.tau == b_cbor.tau
-    from sezkp_amd.launch import _read_manifest_root
-    assert _read_manifest_root(os.path.join(ROOT, manifest_path)) == b_cbor.manifest_root()
+    from sezkp_amd.launch import _read_manifest
+    assert _read_manifest(os.path.join(ROOT, manifest_path)) == (b_cbor.manifest_root(), b_cbor.n_blocks)
 
 
 def test_jsonl_errors_name_the_line(product):
