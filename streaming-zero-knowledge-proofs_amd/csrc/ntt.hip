@@ -205,10 +205,12 @@ __device__ __forceinline__ uint64_t gl_mul2e(uint64_t x, int e) {
 __device__ __forceinline__ uint64_t gl_mul_pow2(uint64_t x, int e) {
   return e >= 96 ? gl_neg(gl_mul2e(x, e - 96)) : gl_mul2e(x, e);
 }
-// exponent of w_{2h}^j as a power of two: w_16 = 2^156 (w_16^-1 = 2^36)
+// exponent of w_{2h}^j as a power of two: w_32 = 2^78 (w_32^-1 = 2^114), so
+// w_16 = 2^156 (w_16^-1 = 2^36); 2 has order 192 mod p, every w_{2^k} with
+// k <= 6 is a power of two (w_64 = 2^39), the reference's roots included
 template <bool INV>
-__device__ __forceinline__ constexpr int tw_exp(int j, int h) { return ((INV ? 36 : 156) * j * (8 / h)) % 192; }
-// x * w_{2h}^j for 2h <= 16
+__device__ __forceinline__ constexpr int tw_exp(int j, int h) { return ((INV ? 114 : 78) * j * (16 / h)) % 192; }
+// x * w_{2h}^j for 2h <= 32
 template <bool INV>
 __device__ __forceinline__ uint64_t tw_small(uint64_t x, int j, int h) {
   return gl_mul_pow2(x, tw_exp<INV>(j, h));
@@ -369,6 +371,37 @@ __device__ __forceinline__ void lds_to_natural(const uint64_t* sh, const NttPass
     P.out[__brev((uint32_t)(p0 + e)) >> sh_r] = v;
   }
 }
+// nat_tr (the last, narrow DIF pass of a natural-order transform, 2^m-point
+// sub-transforms, m <= 8): after the earlier passes block B (2^m contiguous
+// points) holds the sub-transforms whose outputs land at
+// X[k 2^(N-m) + bitrev_{N-m}(B)], k = bitrev_m(row). Tile T takes the 16
+// blocks B_i = bitrev_{N-m}(16 T + i), i < 16, so for every k its 16 outputs
+// are one contiguous 128-B segment: whole-segment loads (each block is 2^m
+// contiguous points) and whole-segment stores, no bit-reversal pass.
+template <int R>
+__device__ __forceinline__ void gather_to_lds(uint64_t* sh, const uint64_t* __restrict__ a, uint64_t tile, int logN) {
+  constexpr int m = __builtin_ctz(R);
+  const int sb = 32 - (logN - m);
+#pragma unroll
+  for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
+    const int e = j * NTT_THREADS + threadIdx.x, i = e >> m, row = e & (R - 1);
+    const uint64_t B = __brev((uint32_t)(tile * NTT_CMAX + i)) >> sb;
+    sh[row * NTT_PADC + i] = a[(B << m) + row];
+  }
+}
+template <int R>
+__device__ __forceinline__ void lds_to_transposed(const uint64_t* sh, const NttPassArgs& P, uint64_t tile) {
+  constexpr int m = __builtin_ctz(R);
+  const int lo = P.nat_logN - m;
+#pragma unroll
+  for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
+    const int e = j * NTT_THREADS + threadIdx.x, i = e & (NTT_CMAX - 1), k = e >> 4;
+    uint64_t v = sh[(__brev((uint32_t)k) >> (32 - m)) * NTT_PADC + i];
+    if (P.out_scale != 1) v = gl_mul(v, P.out_scale);
+    P.out[((uint64_t)k << lo) + tile * NTT_CMAX + i] = v;
+  }
+}
+
 // dispatch order of a nat_out pass: tiles T and T + j G (G = tiles / 16)
 // write the same output lines; 16 consecutive workgroups of one XCD
 // (workgroup b runs on XCD b mod 8) take one such group
@@ -435,7 +468,12 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   const int c = tid & (NTT_CMAX - 1), g = tid / NTT_CMAX;
   // a plain NARROW load stages the tile through the LDS image first
   const bool staged_load = NARROW && !P.dp_rlo && !P.src;
-  if (staged_load) narrow_to_lds<R>(sh, P.a, G.tile);
+  if constexpr (NARROW && DIF && !X16) {
+    if (P.nat_tr) gather_to_lds<R>(sh, P.a, G.tile, P.nat_logN);
+    else if (staged_load) narrow_to_lds<R>(sh, P.a, G.tile);
+  } else if (staged_load) {
+    narrow_to_lds<R>(sh, P.a, G.tile);
+  }
   __syncthreads();
   if constexpr (X16 && DIF) {  // the previous DIF pass's 4 stages, in the tile
     tile_radix16<R, true, INV>(sh, T);
@@ -578,9 +616,74 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
         for (int qq = 0; qq < F1; qq++) sh[(g * F1 + qq) * NTT_PADC + c] = y[qq];
       }
       __syncthreads();
-      if (P.nat_out) lds_to_natural<R>(sh, P, G.tile);
+      if (!X16 && P.nat_tr) lds_to_transposed<R>(sh, P, G.tile);
+      else if (P.nat_out) lds_to_natural<R>(sh, P, G.tile);
       else lds_to_narrow<R>(sh, P.a, G.tile);
     }
+  }
+}
+
+// Wide DIF pass of m = 9 stages for the natural-order transforms of 2^25 and
+// 2^26 points: their last pass stays at 8 stages (the transposed store of
+// nat_tr needs a 16-block tile), so the other 17 / 18 stages take passes of 9,
+// keeping 3 passes. Tile = 16 columns x 512 rows (70 KB of LDS, 512 threads,
+// two workgroups per CU: 16 waves, as four k_ntt4 workgroups). Four-step
+// 512 = 32 x 16: step 1, thread (c, r) for r < 32, a 16-point DIF over u
+// (x[32 u + r]), then * w_512^(r k_lo); step 2, thread (c, q) for q < 16, a
+// 32-point DIF over r (w_32 = 2^78: shifts). Same row order, pass twiddle and
+// out-of-place store as k_ntt4's wide DIF pass.
+template <bool INV>
+__global__ void __launch_bounds__(512, 2) k_ntt_dif9(NttPassArgs P) {
+  constexpr int M1 = 5, M2 = 4, F1 = 1 << M1, F2 = 1 << M2, m = M1 + M2, R = 1 << m, NT = 512;
+  __shared__ uint64_t sh[R * NTT_PADC];
+  __shared__ uint64_t W[R];
+  const int tid = threadIdx.x;
+  const NttTables& T = P.tw;
+  for (int x = tid; x < R; x += NT) W[x] = tw_pow(T, (uint64_t)x << (T.K - m), INV);
+  Tile G;
+  G.sL = P.sL;
+  G.m = m;
+  G.tile = blockIdx.x;
+  G.wide = true;
+  const uint64_t tiles_per_blk = (1ULL << G.sL) / NTT_CMAX;
+  G.blk_base = (G.tile / tiles_per_blk) * ((uint64_t)R << G.sL);
+  G.low0 = (G.tile % tiles_per_blk) * NTT_CMAX;
+  const int tw_shift = T.K - m - G.sL;
+  const int c = tid & (NTT_CMAX - 1), g = tid / NTT_CMAX;  // g < F1
+  uint64_t low;
+  {  // step 1: thread (c, r), registers u
+    const int r = g;
+    uint64_t x[F2];
+#pragma unroll
+    for (int u = 0; u < F2; u++) x[u] = P.a[tile_pos(G, F1 * u + r, c, low)];
+    fft_dif_regs<M2, INV>(x);
+    __syncthreads();  // W
+#pragma unroll
+    for (int q = 0; q < F2; q++) {
+      const int klo = rev<M2>(q);
+      sh[(q * F1 + r) * NTT_PADC + c] = klo && r ? gl_mul(x[q], W[r * klo]) : x[q];
+    }
+  }
+  __syncthreads();
+  if (g < F2) {  // step 2: thread (c, q), registers r
+    const int q = g;
+    uint64_t y[F1];
+#pragma unroll
+    for (int r = 0; r < F1; r++) y[r] = sh[(q * F1 + r) * NTT_PADC + c];
+    fft_dif_regs<M1, INV>(y);
+    (void)tile_pos(G, q * F1, c, low);
+    if (low != 0) {  // post-twiddle w^(low * (k_lo + F2 k_hi)), k_hi = rev(qq)
+      uint64_t t = tw_pow(T, (low * (uint64_t)rev<M2>(q)) << tw_shift, INV);
+      const uint64_t s1 = tw_pow(T, (low * (uint64_t)F2) << tw_shift, INV);
+#pragma unroll
+      for (int kh = 0; kh < F1; kh++) {
+        y[rev<M1>(kh)] = gl_mul(y[rev<M1>(kh)], t);
+        if (kh + 1 < F1) t = gl_mul(t, s1);
+      }
+    }
+    uint64_t* dst = P.out ? P.out : P.a;
+#pragma unroll
+    for (int qq = 0; qq < F1; qq++) dst[tile_pos(G, q * F1 + qq, c, low)] = y[qq];
   }
 }
 
@@ -1124,9 +1227,52 @@ static bool nat_disabled() {
   static const bool off = getenv("SEZKP_NTT_BITREV_PASS") != nullptr;
   return off;
 }
+// SEZKP_NTT_NAT_TR=0: 2^23..2^26 keep the separate bit reversal (A/B comparison)
+static bool nat_tr_disabled() {
+  static const bool off = getenv("SEZKP_NTT_NAT_TR") && atoi(getenv("SEZKP_NTT_NAT_TR")) == 0;
+  return off;
+}
+// Natural order through the transposed last pass (nat_tr): passes of <= 9
+// stages, then 8 (2^23: 8+7+8, 2^24: 8+8+8, 2^25: 9+8+8, 2^26: 9+9+8). The
+// first pass reads `a` and writes `scratch`, the middle ones run in place on
+// scratch, the last gathers from scratch and writes `a` in natural order.
+static bool ntt_dif_natural_tr(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse,
+                               const NttTables& T, uint64_t scale, hipError_t* err) {
+  if (logN < 23 || logN > 26 || nat_tr_disabled() || ntt4_disabled() || narrow_disabled()) return false;
+  int plan[3];
+  plan[2] = 8;
+  const int rest = logN - 8;              // 15..18
+  plan[0] = (rest + 1) / 2;               // 8, 8, 9, 9
+  plan[1] = rest - plan[0];               // 7, 8, 8, 9
+  int sL = logN;
+  for (int i = 0; i < 3; i++) {
+    NttPassArgs P{};
+    P.a = i == 0 ? a : scratch;
+    P.out = i == 0 ? scratch : nullptr;
+    P.tw = T; P.m = plan[i]; sL -= plan[i]; P.sL = sL;
+    P.inverse = inverse ? 1 : 0;
+    P.logC = 4;
+    const uint64_t tiles = (1ULL << logN) >> (P.m + 4);
+    if (i == 2) {
+      P.a = scratch; P.out = a; P.nat_tr = 1; P.nat_logN = logN; P.out_scale = scale;
+    }
+    if (P.m == 9) {
+      if (inverse) hipLaunchKernelGGL(k_ntt_dif9<true>, dim3((unsigned)tiles), dim3(512), 0, st, P);
+      else hipLaunchKernelGGL(k_ntt_dif9<false>, dim3((unsigned)tiles), dim3(512), 0, st, P);
+      continue;
+    }
+    const bool ok = inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
+                            : launch_ntt4<true, false>(st, P, (unsigned)tiles);
+    if (!ok) { *err = hipErrorInvalidValue; return true; }
+  }
+  *err = hipGetLastError();
+  return true;
+}
+
 bool ntt_dif_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse, const NttTables& T,
                      uint64_t scale, hipError_t* err) {
   *err = hipSuccess;
+  if (scratch && scratch != a && ntt_dif_natural_tr(st, a, scratch, logN, inverse, T, scale, err)) return true;
   // measured (profiles/r02_ntt_nat_ab.txt): 1-5% faster at 2^19..2^22, slower from 2^24 (where the
   // scattered lines no longer merge in L2 before write-back: 687 vs 577 us at 2^24)
   if (!scratch || scratch == a || logN < 19 || logN > 22 || nat_disabled() || ntt4_disabled() || narrow_disabled())

@@ -1528,7 +1528,11 @@ int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, u
       if (e != hipSuccess) throw Err{SEZKP_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
     };
     const uint64_t inv_n = inv ? hgl_inv((1ULL << log_n) % GL_P_HOST) : 1;
-    if (P == 1) {  // no exchange: the twiddle is 1 and the permutation swaps tile pairs in place
+    hipError_t nat_err = hipSuccess;
+    if (P == 1 && ntt_dif_natural(st, local, scratch, logM, inv, ctx->tw, inv_n, &nat_err)) {
+      // no exchange: natural order in and out (2^19..2^26 without a bit-reversal pass)
+      ok(nat_err, "dist_ntt local");
+    } else if (P == 1) {  // no exchange: the twiddle is 1 and the permutation swaps tile pairs in place
       if (!inv) {
         ok(ntt_dif(st, local, logM, false, ctx->tw), "dist_ntt local");
         ok(bitrev_inplace(st, local, logM, 1, false), "dist_ntt bitrev");

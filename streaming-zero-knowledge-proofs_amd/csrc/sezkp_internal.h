@@ -45,6 +45,10 @@ struct NttPassArgs {
   uint64_t* out;
   int nat_out, nat_logN;
   uint64_t out_scale;
+  // nat_tr: the last (narrow, m <= 8) DIF pass gathers the 16 blocks whose
+  // outputs share 128-B lines and stores them transposed into natural order
+  // (ntt.hip gather_to_lds / lds_to_transposed)
+  int nat_tr;
 };
 // DEEP division y_i / (3 w_N^(g + P i) - z) fused into the LDE's last pass
 struct DeepFuse {

@@ -193,7 +193,7 @@ def test_launcher_jsonl_artifact_matches_oracle(gpu_ok, product, oracle, tmp_pat
     bad = cmd[:]
     bad[bad.index(str(tmp_path / "m.cbor"))] = str(tmp_path / "bad.cbor")
     r = subprocess.run(bad, cwd=PKG, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 1 and "manifest root mismatch" in r.stderr
+    assert r.returncode == 1 and "root mismatch" in r.stderr
 
 
 def _trip_worker(rank, world, port, q):
