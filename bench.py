@@ -940,10 +940,14 @@ def measure_sharded(args, world, rank, local, dist, torch):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     stage_sum = {}
+    coll_sum = {}
     for _ in range(args.sharded_steps):
         view = ctx.prove_view(mroot)
         for k, v in ctx.stage_times_ms().items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
+        for c in ctx.comm_stats():
+            a = coll_sum.setdefault(c["name"], {"bytes": c["bytes"], "ms": 0.0})
+            a["ms"] += c["ms"]
     dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -964,7 +968,12 @@ def measure_sharded(args, world, rank, local, dist, torch):
                       "parallelism": f"sharded x{world}: coset-split LDE, 1 RCCL all-to-all, allgathered "
                                      f"Merkle caps, byte-sum proof assembly"},
            "ranks_agree": len(set(ds)) == 1, "matches_single_gpu_proof": ds[0] == single, "proof_bytes": plen,
-           "stages_ms_rank0": {k: v / args.sharded_steps for k, v in stage_sum.items()}}
+           "stages_ms_rank0": {k: v / args.sharded_steps for k, v in stage_sum.items()},
+           "collectives_rank0": {k: {"bytes_sent": v["bytes"], "ms": v["ms"] / args.sharded_steps,
+                                     "GBs": v["bytes"] / (v["ms"] / args.sharded_steps) / 1e6 if v["ms"] > 0 else None}
+                                 for k, v in coll_sum.items()},
+           "collectives_note": "HIP events around each RCCL call on rank 0's prover stream (includes the wait for "
+                               "peers to arrive); bytes_sent = what rank 0 puts on its xGMI links per call"}
     if not ok:
         res["error"] = "sharded proof differs across ranks or from the single-GPU proof"
     return res

@@ -160,6 +160,24 @@ typedef struct sezkp_host_comm {
 } sezkp_host_comm;
 sezkp_ctx* sezkp_ctx_create_sharded_host(int32_t device, int32_t rank, int32_t world, const sezkp_host_comm* comm,
                                          char* err, size_t err_len);
+/* Failure handling of sharded proving: a rank that fails after the first
+ * collective of a prove (a HIP error, a guard trip, a peer that stops
+ * answering) aborts its RCCL communicator (ncclCommAbort) and returns
+ * SEZKP_E_DEVICE; a rank waiting on a stream that holds collectives polls
+ * ncclCommGetAsyncError and gives up after SEZKP_COLL_TIMEOUT_S seconds
+ * (default 60), aborting as well, so every rank returns an error instead of
+ * blocking. The context is then unusable (every later prove fails): destroy
+ * it and create a new communicator.
+ * Per-collective device time of the last sharded prove (HIP events around
+ * each call on the prover stream) and the bytes this rank sent over the links
+ * (allgather (P-1) x its part, all-to-all (P-1) x the per-peer part, allreduce
+ * 2 (P-1)/P x the buffer). Returns the number of entries written. */
+typedef struct sezkp_comm_stat {
+  char name[32];
+  uint64_t bytes;
+  double ms;
+} sezkp_comm_stat;
+int32_t sezkp_ctx_comm_stats(const sezkp_ctx* ctx, sezkp_comm_stat* out, int32_t max);
 
 /* Distributed four-step NTT of n = 2^log_n points over the context's P ranks
  * (BASELINE config 4: 2^26 points across 8 GPUs, the transpose as one RCCL

@@ -9,9 +9,16 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <chrono>
 #include <stdexcept>
+#include <thread>
 
 namespace sezkp {
+
+void Comm::wait(hipStream_t st, double) {
+  const hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) throw std::runtime_error(std::string("stream sync: ") + hipGetErrorString(e));
+}
 
 namespace {
 
@@ -35,16 +42,46 @@ struct RcclComm final : Comm {
   ~RcclComm() override {
     if (c) (void)ncclCommDestroy(c);
   }
+  void wait(hipStream_t st, double timeout_s) override {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (int spin = 0;; spin++) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) throw std::runtime_error(std::string("stream: ") + hipGetErrorString(q));
+      ncclResult_t ae = ncclSuccess;
+      if (c && ncclCommGetAsyncError(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+        throw std::runtime_error(std::string("collective failed: ") + ncclGetErrorString(ae));
+      if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_s)
+        throw std::runtime_error("collective timeout: no progress within " + std::to_string(timeout_s) +
+                                 " s (SEZKP_COLL_TIMEOUT_S); a peer rank failed or stalled");
+      // short proofs finish in a few ms: spin first, then back off
+      if (spin > 200) std::this_thread::sleep_for(std::chrono::microseconds(spin > 2000 ? 1000 : 50));
+    }
+  }
+  void abort() override {
+    if (c) (void)ncclCommAbort(c);
+    c = nullptr;
+  }
+  void live() const {
+    if (!c) throw std::runtime_error("communicator aborted after an earlier failure");
+  }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    live();
     nccl_check(ncclAllGather(send, recv, bytes, ncclUint8, c, st), "ncclAllGather");
   }
   void alltoall(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    live();
     nccl_check(ncclAllToAll(send, recv, bytes, ncclUint8, c, st), "ncclAllToAll");
   }
   void allreduce_sum_u8(void* buf, size_t bytes, hipStream_t st) override {
+    live();
     nccl_check(ncclAllReduce(buf, buf, bytes, ncclUint8, ncclSum, c, st), "ncclAllReduce");
   }
-  void group_start() override { nccl_check(ncclGroupStart(), "ncclGroupStart"); }
+  void group_start() override {
+    live();
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+  }
   void group_end() override { nccl_check(ncclGroupEnd(), "ncclGroupEnd"); }
   std::string name() const override { return "rccl"; }
 };

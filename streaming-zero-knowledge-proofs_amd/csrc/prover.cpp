@@ -276,6 +276,21 @@ struct sezkp_ctx {
   // final D2H wait, proof serialization (after the last sync)
   double host_ms[4]{};
   bool have_times = false;
+  // sharded: a failure after the first collective of a prove aborts the
+  // communicator (peers blocked in an RCCL call then time out instead of
+  // hanging) and leaves the context broken: every later call fails
+  bool broken = false;
+  bool coll_issued = false;
+  // per-collective device time of the last sharded prove (HIP events around
+  // each call on the prover stream) and the bytes this rank sends over links
+  struct CollStat {
+    const char* name;
+    uint64_t bytes;
+    hipEvent_t a, b;
+  };
+  std::vector<CollStat> coll_stats;
+  std::vector<hipEvent_t> coll_ev;
+  size_t coll_used = 0;
 
   static void* take_spare(std::multimap<size_t, void*>& m, size_t bytes) {
     auto it = m.find(bytes);
@@ -402,6 +417,7 @@ struct sezkp_ctx {
     release_spares();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : coll_ev) (void)hipEventDestroy(e);
     if (st2) (void)hipStreamSynchronize(st2);
     if (ev_fold) (void)hipEventDestroy(ev_fold);
     if (ev_tail) (void)hipEventDestroy(ev_tail);
@@ -425,7 +441,26 @@ struct sezkp_ctx {
   void take_staged();
   // proves into the pinned staging buffer; returns its size (bytes at h_proof)
   size_t prove(const uint8_t root[32]);
+  size_t prove_body(const uint8_t root[32]);
 };
+
+// SEZKP_COLL_TIMEOUT_S: how long a sharded rank waits for a stream holding
+// collectives before it aborts the communicator (default 60 s; a T = 2^22
+// proof takes ~10 ms once uploaded)
+static double coll_timeout_s() {
+  static const double t = getenv("SEZKP_COLL_TIMEOUT_S") ? atof(getenv("SEZKP_COLL_TIMEOUT_S")) : 60.0;
+  return t > 0 ? t : 60.0;
+}
+// test hook: SEZKP_DEBUG_FAIL_AT=<rank>:<collective> makes that rank fail
+// right before that collective of every sharded prove (tests/test_gpu_sharded.py)
+static void fail_point(int rank, const char* name) {
+  static const char* spec = getenv("SEZKP_DEBUG_FAIL_AT");
+  if (!spec) return;
+  const char* colon = strchr(spec, ':');
+  if (!colon || atoi(spec) != rank || strcmp(colon + 1, name) != 0) return;
+  throw Err{SEZKP_E_DEVICE, std::string("injected failure before collective ") + name + " on rank " +
+                                std::to_string(rank)};
+}
 
 void sezkp_ctx::upload(const sezkp_block_view& v) {
   HIP_OR_THROW(hipSetDevice(device));
@@ -852,6 +887,27 @@ void sezkp_ctx::take_staged() {
 }
 
 size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
+  if (broken)
+    throw Err{SEZKP_E_DEVICE, "context unusable: an earlier sharded prove failed after its first collective and "
+                              "aborted the communicator (destroy the context and create a new one)"};
+  coll_issued = false;
+  coll_used = 0;
+  coll_stats.clear();
+  try {
+    return prove_body(mroot);
+  } catch (...) {
+    // peers may already be waiting in a collective this rank will never join
+    // (or this rank in one they never join): abort so that every rank's
+    // enqueued collectives stop and every rank returns an error
+    if (sharded() && coll_issued) {
+      comm->abort();
+      broken = true;
+    }
+    throw;
+  }
+}
+
+size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   if (!loaded) throw Err{SEZKP_E_INVALID, "no trace uploaded"};
   // the trace image was fixed by take_staged() in the public entry point that
   // started this proof (for prove_async: before the worker runs, so a stage()
@@ -861,7 +917,15 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   double t_sync = 0, t_last = 0;
   auto sync = [&]() {
     const auto t0 = clk::now();
-    HIP_OR_THROW(hipStreamSynchronize(st));
+    if (sharded() && coll_issued) {
+      try {
+        comm->wait(st, coll_timeout_s());
+      } catch (const std::exception& e) {
+        throw Err{SEZKP_E_DEVICE, std::string("rank ") + std::to_string(rank) + ": " + e.what()};
+      }
+    } else {
+      HIP_OR_THROW(hipStreamSynchronize(st));
+    }
     t_last = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     t_sync += t_last;
   };
@@ -876,6 +940,31 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
 
   const bool sharded = this->sharded();
   const uint64_t S = 1ULL << L16_LOG;
+  // every collective goes through coll(): the failure hook, the events of the
+  // per-collective stats, and the mark that a failure from here on must abort
+  // the communicator. `wire` = bytes this rank sends over the links.
+  auto coll = [&](const char* name, uint64_t wire, auto&& issue) {
+    fail_point(rank, name);
+    while (coll_ev.size() < 2 * (coll_used + 1)) {
+      hipEvent_t e;
+      HIP_OR_THROW(hipEventCreate(&e));
+      coll_ev.push_back(e);
+    }
+    hipEvent_t a = coll_ev[2 * coll_used], b = coll_ev[2 * coll_used + 1];
+    coll_used++;
+    HIP_OR_THROW(hipEventRecord(a, st));
+    coll_issued = true;
+    try {
+      issue();
+    } catch (const Err&) {
+      throw;
+    } catch (const std::exception& e) {
+      throw Err{SEZKP_E_DEVICE, std::string(name) + ": " + e.what()};
+    }
+    HIP_OR_THROW(hipEventRecord(b, st));
+    coll_stats.push_back(CollStat{name, wire, a, b});
+  };
+  const uint64_t P1 = (uint64_t)world - 1;
   rec(0);
   // ---- column commitments (openings.rs:306-398): this rank's chunks, then
   // every rank gathers all chunk roots and builds the outer trees
@@ -898,12 +987,14 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   HIP_OR_THROW(hipStreamWaitEvent(st, ev_cols, 0));
   if (sharded) {
     const size_t bytes = (size_t)(ch_hi - ch_lo) * 32;
-    comm->group_start();
-    for (int c = 0; c < ncols; c++) {
-      uint32_t* lvl0 = d_outer + (size_t)c * outer_stride * 8;
-      comm->allgather(lvl0 + ch_lo * 8, lvl0, bytes, st);
-    }
-    comm->group_end();
+    coll("col_chunk_roots", P1 * bytes * ncols, [&] {
+      comm->group_start();
+      for (int c = 0; c < ncols; c++) {
+        uint32_t* lvl0 = d_outer + (size_t)c * outer_stride * 8;
+        comm->allgather(lvl0 + ch_lo * 8, lvl0, bytes, st);
+      }
+      comm->group_end();
+    });
   }
   rec(2);
   TreeDev outer0{d_outer, d_colroots, logChunks, 0};
@@ -917,7 +1008,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   // check that the failure is collective (tests/test_gpu_sharded.py)
   static const char* trip = getenv("SEZKP_DEBUG_TRIP_GUARD");
   if (trip && atoi(trip) == rank) HIP_OR_THROW(hipMemsetAsync(d_err, 0x7f, 1, st));
-  if (sharded) comm->allgather(d_err, d_err + 8, 4, st);
+  if (sharded) coll("guard_words", P1 * 4, [&] { comm->allgather(d_err, d_err + 8, 4, st); });
   const bool copy_roots = roots_copied();
   if (copy_roots) HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
   HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * ncols, sharded ? d_err + 8 : d_err, 4 * nguard, hipMemcpyDeviceToHost, st));
@@ -976,7 +1067,9 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   // are [g n/P, (g+1) n/P) (n >= 4096 P). SEZKP_REPLICATED_INTT=1 gathers the
   // n values and runs the n-point INTT on every rank instead.
   const bool dist_intt = sharded && world > 1 && !getenv("SEZKP_REPLICATED_INTT");
-  if (sharded && !dq && !dist_intt) comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st);
+  if (sharded && !dq && !dist_intt)
+    coll("base_values", P1 * (row_hi - row_lo) * 8,
+         [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
   rec(4);
   DeepPoly dpoly{d_dq_rlo, d_dq_rhi};
   if (dq) {
@@ -998,11 +1091,13 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     if (sharded) {
       const uint64_t nrows = row_hi - row_lo, per = 4096;
       ok(launch_inv_base(st, d_base, d_lde, d_dq_part, logn, z, tw, row_lo, nrows), "inv_base");
-      comm->allgather(d_dq_part + row_lo / per, d_dq_part, (size_t)(nrows / per) * 8, st);
+      coll("fz_partials", P1 * (nrows / per) * 8,
+           [&] { comm->allgather(d_dq_part + row_lo / per, d_dq_part, (size_t)(nrows / per) * 8, st); });
       ok(launch_q_tables(st, d_base, d_lde, d_dq_part, logn, logM, K1, K2, rho, hgl_pow(rho, 4096), d_dq_rlo, d_dq_rhi,
                          row_lo, nrows),
          "q_tables");
-      if (!dist_intt) comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st);
+      if (!dist_intt)
+        coll("q_values", P1 * nrows * 8, [&] { comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st); });
     } else {
       ok(launch_deep_quotient(st, d_base, d_lde, d_dq_part, logn, logM, z, K1, K2, rho, hgl_pow(rho, 4096), d_dq_rlo,
                               d_dq_rhi, tw),
@@ -1013,11 +1108,12 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     const uint64_t m = n >> logP, Q = m >> logP;
     if (row_lo != (uint64_t)rank * m || row_hi - row_lo != m) throw Err{SEZKP_E_INVALID, "sharded INTT: row split"};
     uint64_t* blk = d_base + row_lo;
-    comm->alltoall(blk, d_lde, Q * 8, st);  // d_lde: r[g Q + t] = x[g m + rank Q + t]
+    // d_lde: r[g Q + t] = x[g m + rank Q + t]
+    coll("intt_alltoall1", P1 * Q * 8, [&] { comm->alltoall(blk, d_lde, Q * 8, st); });
     ok(bintt_dft_twiddle(st, d_lde, world, Q, (uint32_t)rank, logn, tw), "intt_dft");
-    comm->alltoall(d_lde, blk, Q * 8, st);  // blk[j] = y_rank[j], j < m
+    coll("intt_alltoall2", P1 * Q * 8, [&] { comm->alltoall(d_lde, blk, Q * 8, st); });  // blk[j] = y_rank[j]
     ok(ntt_dif(st, blk, logn - logP, true, tw), "intt_local");  // slot p: n a_(rank + P bitrev(p))
-    comm->allgather(blk, d_base, m * 8, st);
+    coll("intt_coeffs", P1 * m * 8, [&] { comm->allgather(blk, d_base, m * 8, st); });
   } else {
     ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
   }
@@ -1040,7 +1136,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   if (!deep_fused) ok(launch_deep(st, lde_out, logN, z, tw, logP, (uint32_t)rank), "deep");
   if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI
     ok(launch_cyc_pack(st, d_cyc, d_xbuf, M, logP), "cyc_pack");
-    comm->alltoall(d_xbuf, d_cyc, (size_t)(M >> logP) * 8, st);
+    coll("lde_alltoall", P1 * (M >> logP) * 8, [&] { comm->alltoall(d_xbuf, d_cyc, (size_t)(M >> logP) * 8, st); });
     ok(launch_cyc_unpack(st, d_cyc, d_lde, M, logP), "cyc_unpack");
   }
   rec(7);
@@ -1051,7 +1147,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     if (sharded) {
       const uint64_t nrun = M >> L16_LOG;
       const uint32_t* lv12 = ltrees[0].nodes + 8 * tree_level_off(ltrees[0].logLen, LSTORE_FRI, L16_LOG);
-      comm->allgather(lv12, rr_gather[0], (size_t)nrun * 32, st);
+      coll("layer0_run_roots", P1 * nrun * 32, [&] { comm->allgather(lv12, rr_gather[0], (size_t)nrun * 32, st); });
       ok(launch_runroots_scatter(st, rr_gather[0], caps[0], nrun, logP), "runroots0");
     }
     for (auto& p : jobs0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_upper");
@@ -1109,14 +1205,18 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   if (!sharded) launch_tail(rep_src);
   ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
   if (sharded) {  // run roots of layers 1..rR + the whole of layer rR
-    comm->group_start();
-    for (int r = 1; r <= rR; r++) {
-      const uint64_t nrun = (N >> r) >> (L16_LOG + logP);
-      const uint32_t* lv12 = ltrees[r].nodes + 8 * tree_level_off(ltrees[r].logLen, LSTORE_FRI, L16_LOG);
-      comm->allgather(lv12, rr_gather[r], (size_t)nrun * 32, st);
-    }
-    comm->allgather(lvals[rR], d_rep, (size_t)S * 8, st);
-    comm->group_end();
+    uint64_t wire = P1 * S * 8;
+    for (int r = 1; r <= rR; r++) wire += P1 * ((N >> r) >> (L16_LOG + logP)) * 32;
+    coll("fri_run_roots", wire, [&] {
+      comm->group_start();
+      for (int r = 1; r <= rR; r++) {
+        const uint64_t nrun = (N >> r) >> (L16_LOG + logP);
+        const uint32_t* lv12 = ltrees[r].nodes + 8 * tree_level_off(ltrees[r].logLen, LSTORE_FRI, L16_LOG);
+        comm->allgather(lv12, rr_gather[r], (size_t)nrun * 32, st);
+      }
+      comm->allgather(lvals[rR], d_rep, (size_t)S * 8, st);
+      comm->group_end();
+    });
     for (int r = 1; r <= rR; r++)
       ok(launch_runroots_scatter(st, rr_gather[r], caps[r], (N >> r) >> (L16_LOG + logP), logP), "runroots");
     rep_src = d_rep;
@@ -1213,7 +1313,8 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
     HIP_OR_THROW(hipEventRecord(ev_tail, st2));
   }
   ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL), "fri_paths");
-  if (sharded) comm->allreduce_sum_u8(PL.base, PL.total, st);
+  if (sharded)
+    coll("proof_allreduce", 2 * P1 * PL.total / (uint64_t)world, [&] { comm->allreduce_sum_u8(PL.base, PL.total, st); });
   rec(ST_PATHS + 1);
   const uint64_t d2h_from = sharded ? 0 : PL.fr_off;
   HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes + d2h_from, (const uint8_t*)PL.base + d2h_from,
@@ -1502,6 +1603,21 @@ int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max)
   return cnt;
 }
 void* sezkp_ctx_stream(const sezkp_ctx* ctx) { return ctx ? (void*)ctx->st : nullptr; }
+int32_t sezkp_ctx_comm_stats(const sezkp_ctx* ctx, sezkp_comm_stat* out, int32_t max) {
+  if (!ctx || !out || max <= 0) return 0;
+  int32_t cnt = 0;
+  for (const auto& c : ctx->coll_stats) {
+    if (cnt >= max) break;
+    sezkp_comm_stat& o = out[cnt++];
+    memset(o.name, 0, sizeof o.name);
+    strncpy(o.name, c.name, sizeof o.name - 1);
+    o.bytes = c.bytes;
+    float ms = 0;
+    o.ms = hipEventElapsedTime(&ms, c.a, c.b) == hipSuccess ? ms : -1.0;
+  }
+  (void)hipGetLastError();
+  return cnt;
+}
 
 // Distributed four-step NTT over the context's ranks (BASELINE
 // config 4). Forward: local M-point NTT (DIF) -> bit-reverse + w_N^(g k2)
@@ -1513,7 +1629,7 @@ int32_t sezkp_ctx_dist_ntt(sezkp_ctx* ctx, uint64_t* local, uint64_t* scratch, u
   try {
     if (!ctx || !local || !scratch) throw Err{SEZKP_E_INVALID, "null argument"};
     if (ctx->busy()) throw Err{SEZKP_E_INVALID, "a proof is in flight on this context (call sezkp_ctx_wait)"};
-
+    if (ctx->broken) throw Err{SEZKP_E_DEVICE, "context unusable after an aborted collective"};
     if (dir != 1 && dir != -1) throw Err{SEZKP_E_INVALID, "dir must be +1 or -1"};
     const int P = ctx->world, logP = ctx->logP;
     if (log_n > 32 || (int)log_n < 8 + logP)

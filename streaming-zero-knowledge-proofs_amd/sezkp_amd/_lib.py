@@ -31,8 +31,12 @@ EXPORTS = [
     "sezkp_blocks_encode_cbor", "sezkp_simulate_trace", "sezkp_simulate_blocks",
     "sezkp_ctx_prove_async", "sezkp_ctx_wait", "sezkp_ctx_stage", "sezkp_host_register", "sezkp_host_unregister",
     "sezkp_fri_fold", "sezkp_blake3_leaves_u64", "sezkp_blake3_leaves_labeled", "sezkp_merkle_node_count",
-    "sezkp_merkle_build", "sezkp_merkle_paths", "sezkp_manifest_frontier_root",
+    "sezkp_merkle_build", "sezkp_merkle_paths", "sezkp_manifest_frontier_root", "sezkp_ctx_comm_stats",
 ]
+
+
+class CommStat(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("bytes", C.c_uint64), ("ms", C.c_double)]
 
 
 class SezkpError(RuntimeError):
@@ -104,6 +108,7 @@ def _load():
                                          C.POINTER(C.c_size_t)] + E
     L.sezkp_ctx_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int32]
     L.sezkp_ctx_stream.restype = C.c_void_p
+    L.sezkp_ctx_comm_stats.argtypes = [C.c_void_p, C.POINTER(CommStat), C.c_int32]
     L.sezkp_ctx_stream.argtypes = [C.c_void_p]
     L.sezkp_gl_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p]
     L.sezkp_gl_coset_lde_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p,

@@ -160,6 +160,19 @@ class ProverContext:
         n = lib.sezkp_ctx_stage_times(self._h, buf, 32)
         return {STAGES[i]: buf[i] for i in range(min(n, len(STAGES)))}
 
+    def comm_stats(self) -> list:
+        """Per-collective stats of the last sharded prove: [{name, bytes, ms,
+        GBs}] (sezkp_ctx_comm_stats; bytes = what this rank sent over links)."""
+        from ._lib import CommStat
+        buf = (CommStat * 64)()
+        n = lib.sezkp_ctx_comm_stats(self._h, buf, 64)
+        out = []
+        for i in range(n):
+            b, ms = int(buf[i].bytes), float(buf[i].ms)
+            out.append({"name": buf[i].name.decode(), "bytes": b, "ms": ms,
+                        "GBs": (b / ms / 1e6) if ms > 0 else None})
+        return out
+
     def dist_ntt(self, local, scratch=None, inverse: bool = False, sync: bool = True):
         """Distributed four-step NTT of n = world * local.numel() points, in
         place on `local` (a device u64/i64 tensor; layouts in sezkp_stark.h,

@@ -39,6 +39,7 @@ def _worker(rank, world, port, T, b, tau, seed, q):
         p1 = ctx.prove(root).proof_bytes
         p2 = ctx.prove(root).proof_bytes
         calls = dict(ctx._coll.calls)
+        calls["stats"] = ctx.comm_stats()
         ctx.close()
         q.put((rank, hashlib.sha256(p1).hexdigest(), p1 == p2, calls))
     except Exception as e:
@@ -76,6 +77,11 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
         # per prove: three all-to-alls (two for the INTT, one for the LDE), one
         # byte-sum (proof body), allgathers
         assert calls["alltoall"] == 6 and calls["allreduce"] == 2 and calls["allgather"] > 0
+        # sezkp_ctx_comm_stats: one entry per collective of the last prove
+        st = {c["name"]: c for c in calls["stats"]}
+        assert {"col_chunk_roots", "guard_words", "intt_alltoall1", "intt_alltoall2", "intt_coeffs",
+                "lde_alltoall", "layer0_run_roots", "fri_run_roots", "proof_allreduce"} <= set(st), sorted(st)
+        assert all(c["bytes"] > 0 and c["ms"] >= 0 for c in calls["stats"])
 
 
 def test_sharded_config5_size_p8_matches_openmp_oracle(gpu_ok, product):
@@ -231,3 +237,84 @@ def test_sharded_guard_trip_fails_every_rank(gpu_ok):
         p.join(timeout=60)
     for rank, msg in res:
         assert "guard tripped on rank 1" in msg, (rank, msg)
+
+
+def _fail_worker(rank, world, port, point, q):
+    """Rank 1 fails right before collective `point` (test hook); gloo's own
+    timeout (20 s) bounds the wait of the rank left inside the collective."""
+    import datetime
+    import time
+    sys.path[:0] = [PKG, ORACLE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SEZKP_DEBUG_FAIL_AT=f"1:{point}")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=20))
+    res = [rank]
+    try:
+        import sezkp_amd
+        blocks = sezkp_amd.synthetic_blocks(1 << 13, 512, 2, 42)
+        ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
+        ctx.upload(blocks)
+        t0 = time.monotonic()
+        try:
+            ctx.prove(blocks.manifest_root())
+            res += ["no error", 0.0]
+        except Exception as e:
+            res += [str(e), time.monotonic() - t0]
+        try:  # the context is unusable afterwards
+            ctx.prove(blocks.manifest_root())
+            res.append("no error")
+        except Exception as e:
+            res.append(str(e))
+        ctx.close()
+    except Exception as e:
+        res += [f"setup: {e}", 0.0, ""]
+    q.put(tuple(res))
+    os._exit(0)  # gloo may hold a timed-out collective: leave without a teardown handshake
+
+
+@pytest.mark.parametrize("point", ["lde_alltoall", "fri_run_roots", "proof_allreduce"])
+def test_sharded_failure_on_one_rank_fails_every_rank(gpu_ok, point):
+    """A rank that fails after the first collective of a prove (injected right
+    before a later collective) must not leave its peers blocked: every rank
+    returns an error within the collective deadline, and both contexts refuse
+    further proofs (the communicator is aborted)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_fail_worker, args=(r, 2, port, point, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert f"injected failure before collective {point} on rank 1" in res[1][1], res[1]
+    assert res[0][1] != "no error" and res[0][2] < 60, res[0]
+    for r in res:
+        assert "context unusable" in r[3], r
+
+
+def test_sharded_rccl_abort_after_failure(gpu_ok, product):
+    """One-rank RCCL communicator (SEZKP_FORCE_SHARDED): a failure injected
+    before the LDE all-to-all aborts the communicator (ncclCommAbort); the
+    error comes back, later proofs are refused, and destroy does not hang. In
+    a child process (the switches are read once per process)."""
+    import subprocess
+    code = ("import sys; sys.path[:0]=[%r]\n"
+            "import sezkp_amd as S\n"
+            "bl=S.synthetic_blocks(1<<12,512,2,3); c=S.ShardedProverContext(0,1,device=0,comm='rccl'); c.upload(bl)\n"
+            "for i in range(2):\n"
+            "    try:\n"
+            "        c.prove(bl.manifest_root()); print('no error')\n"
+            "    except Exception as e:\n"
+            "        print('ERR', e)\n"
+            "c.close(); print('closed')\n" % PKG)
+    env = dict(os.environ, SEZKP_FORCE_SHARDED="1", SEZKP_DEBUG_FAIL_AT="0:lde_alltoall")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-1500:]
+    lines = r.stdout.strip().splitlines()
+    assert "injected failure before collective lde_alltoall on rank 0" in lines[0], lines
+    assert "context unusable" in lines[1], lines
+    assert lines[2] == "closed"
