@@ -410,6 +410,10 @@ __device__ __forceinline__ void tail_sub(const uint64_t* b, uint64_t i0, const T
 __global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
   __shared__ uint64_t buf[1 << (TAIL_MAX)];  // the 2^(Ls+1) <= 4096 source values
   __shared__ uint32_t lds[8][TAIL_THREADS];
+  // these few workgroups share CUs with the forest's (VALU-saturating) waves;
+  // their serial fold chain + tree would otherwise get a 1/7 share of issue
+  // and outlast the forest. Top wave priority for the whole (short) kernel.
+  __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x;
   const int j = blockIdx.x;
   const int L = A.Ls - j;

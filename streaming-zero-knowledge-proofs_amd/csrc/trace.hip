@@ -1252,22 +1252,37 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
                                                         const DictPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ tabs, uint32_t* __restrict__ outer,
                                                         uint64_t outer_stride, uint64_t row0, uint64_t row_end,
-                                                        uint32_t* __restrict__ dlev) {
+                                                        uint32_t* __restrict__ dlev, uint32_t ndict, uint32_t xcd_gx) {
   __shared__ uint32_t lds[8][64];
-  const DictCol dc = dcols[blockIdx.y];
+  // xcd_gx != 0: XCD-interleaved order. Workgroup b runs on XCD b mod 8; XCD
+  // x takes the columns c = x, x + 8, x + 16, ... one after the other (gx =
+  // xcd_gx row blocks each), so the ~512 workgroups one XCD holds at a time
+  // gather from one column's tables (<= 2 MB: they stay in that XCD's 4 MB
+  // L2) instead of eight columns' (16 MB). Columns of one kind are tau
+  // consecutive indices, so every XCD gets about the same mix of table
+  // levels (a contiguous range per XCD measured 347 -> 580 us, round 1: the
+  // XCDs holding the wsym / head columns did 4x the work of the others).
+  uint32_t by = blockIdx.y, bx = blockIdx.x;
+  if (xcd_gx) {
+    const uint32_t b = blockIdx.x, x = b & 7, k = b >> 3;
+    by = x + 8 * (k / xcd_gx);
+    bx = k % xcd_gx;
+    if (by >= ndict) return;
+  }
+  const DictCol dc = dcols[by];
   const ColTemplate* ctp = tmpl + dc.col;
   const ColTemplate ct = *ctp;
-  const DictPlan P = plans[blockIdx.y];
+  const DictPlan P = plans[by];
   const uint32_t* tab = tabs + 8 * dc.tab;
   const int lane = threadIdx.x;
   // high-K columns give each lane more rows (fewer LDS levels per row)
   const int a = dict_extra(P.K);
   const int llog = DICT_LANE_LOG + a;  // rows per lane (log2)
-  const uint64_t wg_row = row0 + ((uint64_t)blockIdx.x << (llog + 6));
+  const uint64_t wg_row = row0 + ((uint64_t)bx << (llog + 6));
   if (wg_row >= row_end) return;  // grid is sized for a = 0
   const uint64_t lrow = wg_row + ((uint64_t)lane << llog);
   const uint64_t nch_all = T.n >> COL_CHUNK_LOG2;
-  uint32_t* dl = dlev + 8 * (uint64_t)blockIdx.y * nch_all * DLEV_NODES;
+  uint32_t* dl = dlev + 8 * (uint64_t)by * nch_all * DLEV_NODES;
   if (lrow < row_end) {
     uint32_t h[8];
     switch (ct.kind) {
@@ -1376,8 +1391,16 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
     }
   }
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
-  hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
-                     outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev);
+  static const bool xcd = !getenv("SEZKP_DICT_XCD") || atoi(getenv("SEZKP_DICT_XCD")) != 0;
+  if (xcd && ndict > 8) {
+    const uint64_t per_xcd = (uint64_t)((ndict + 7) / 8) * gx;  // work items of the busiest XCD
+    hipLaunchKernelGGL(k_col_commit_dict, dim3((unsigned)(8 * per_xcd)), dim3(64), 0, st, T, d_tmpl, d_dcols,
+                       d_plans, d_dtabs, outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev,
+                       (uint32_t)ndict, gx);
+  } else {
+    hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
+                       outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev, (uint32_t)ndict, 0u);
+  }
   return hipGetLastError();
 }
 
