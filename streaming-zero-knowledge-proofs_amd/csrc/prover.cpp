@@ -189,6 +189,8 @@ struct sezkp_ctx {
     uint8_t* raw = nullptr;     // step arrays as the view holds them (row-major), before k_trace_image
     uint64_t* h_tab = nullptr;  // pinned staging of bw | bi | bo
     hipEvent_t ready = nullptr;
+    hipEvent_t consumed = nullptr;  // image_on_main: k_trace_image (main stream) has read `raw`
+    bool raw_pending = false;        // image_on_main: `raw` holds a staged trace not yet transposed
   };
   TraceSlot slot[2];
   int active = 0;
@@ -426,6 +428,8 @@ struct sezkp_ctx {
     if (stc) (void)hipStreamSynchronize(stc);
     for (auto& sl : slot)
       if (sl.ready) (void)hipEventDestroy(sl.ready);
+    for (auto& sl : slot)
+      if (sl.consumed) (void)hipEventDestroy(sl.consumed);
     if (st) (void)hipStreamDestroy(st);
     if (st2 && st2 != st) (void)hipStreamDestroy(st2);
     if (stc) (void)hipStreamDestroy(stc);
@@ -436,7 +440,7 @@ struct sezkp_ctx {
   void stage(const sezkp_block_view& v);
   void alloc_slot(TraceSlot& t);
   // block tables + step arrays of `v` into slot t, async on stream s
-  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s);
+  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, bool image = true);
   void check_shape_same(const sezkp_block_view& v) const;
   void take_staged();
   // proves into the pinned staging buffer; returns its size (bytes at h_proof)
@@ -507,9 +511,10 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   staged = false;
   active = 0;
   {
-    hipEvent_t keep = slot[1].ready;
+    hipEvent_t keep = slot[1].ready, keep_c = slot[1].consumed;
     slot[1] = TraceSlot{};
     slot[1].ready = keep;
+    slot[1].consumed = keep_c;
   }
   alloc_slot(slot[0]);
   uint64_t* d_bs = dalloc<uint64_t>(nblk + 1);
@@ -806,15 +811,32 @@ void sezkp_ctx::alloc_slot(TraceSlot& t) {
   t.raw = dalloc<uint8_t>(4 * cells);  // wsym (2-byte aligned first), mv, has_write
   t.h_tab = halloc<uint64_t>(3 * nt + 1);
   if (!t.ready) HIP_OR_THROW(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
+  if (!t.consumed) {
+    HIP_OR_THROW(hipEventCreateWithFlags(&t.consumed, hipEventDisableTiming));
+    HIP_OR_THROW(hipEventRecord(t.consumed, st));
+  }
+  t.raw_pending = false;
+}
+
+// SEZKP_IMAGE_ON_MAIN=1: a staged trace's transposition (k_trace_image) runs
+// on the main stream when the proof takes the trace, so the copy stream holds
+// only the PCIe copies (no kernel waiting behind them in a hardware queue that
+// other streams share); 0 = the transposition follows the copies on the copy
+// stream (round 2)
+static bool image_on_main() {
+  static const bool on = getenv("SEZKP_IMAGE_ON_MAIN") && atoi(getenv("SEZKP_IMAGE_ON_MAIN")) != 0;
+  return on;
 }
 
 // Per-block tables on the host (window lengths, head offsets: tau * n_blocks
 // values), then every array over PCIe asynchronously on `s` and the row-major
 // step arrays transposed to the tape-major image on the device.
-void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s) {
+void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, bool image) {
   const size_t cells = (size_t)tau * n, nt = (size_t)tau * nblk;
   // the previous copy out of h_tab (an earlier stage into this slot) must be done
   HIP_OR_THROW(hipEventSynchronize(t.ready));
+  // and the raw arrays it filled must have been transposed already
+  if (s != st) HIP_OR_THROW(hipStreamWaitEvent(s, t.consumed, 0));
   for (uint32_t k = 0; k < nblk; k++)
     for (uint32_t r = 0; r < tau; r++) {
       const size_t i = (size_t)k * tau + r, o = (size_t)r * nblk + k;
@@ -835,7 +857,8 @@ void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t
   cp(raw_hw, v.has_write, cells);
   cp(t.imv, v.input_mv, n);
   cp(t.bw, t.h_tab, 3 * nt * 8);
-  HIP_OR_THROW(launch_trace_image(s, raw_mv, raw_hw, raw_ws, n, tau, t.mv, t.wf, t.ws));
+  if (image) HIP_OR_THROW(launch_trace_image(s, raw_mv, raw_hw, raw_ws, n, tau, t.mv, t.wf, t.ws));
+  t.raw_pending = !image;
   HIP_OR_THROW(hipEventRecord(t.ready, s));
 }
 
@@ -861,7 +884,7 @@ void sezkp_ctx::stage(const sezkp_block_view& v) {
   TraceSlot& t = slot[1 - active];
   if (!t.imv) alloc_slot(t);  // first stage on this workspace: the spare image
   staged = false;             // (re)filling the spare slot
-  write_trace(t, v, stc);
+  write_trace(t, v, stc, !image_on_main());
   staged = true;
 }
 
@@ -874,7 +897,7 @@ void sezkp_ctx::take_staged() {
   if (staged) {
     active = 1 - active;
     staged = false;
-    const TraceSlot& t = slot[active];
+    TraceSlot& t = slot[active];
     T.input_mv = t.imv;
     T.mv = t.mv;
     T.wflag = t.wf;
@@ -883,6 +906,13 @@ void sezkp_ctx::take_staged() {
     T.blk_offin = t.bi;
     T.blk_offout = t.bo;
     HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
+    if (t.raw_pending) {  // image_on_main: transpose on the main stream, ahead of the proof
+      const size_t cells = (size_t)tau * n;
+      HIP_OR_THROW(launch_trace_image(st, reinterpret_cast<int8_t*>(t.raw + 2 * cells), t.raw + 3 * cells,
+                                      reinterpret_cast<uint16_t*>(t.raw), n, tau, t.mv, t.wf, t.ws));
+      HIP_OR_THROW(hipEventRecord(t.consumed, st));
+      t.raw_pending = false;
+    }
   }
 }
 

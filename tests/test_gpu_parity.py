@@ -585,12 +585,14 @@ def test_staged_uploads_pipeline_bit_exact(gpu_ok, product, oracle):
         t.unpin()
 
 
-def test_stage_after_prove_async_feeds_the_next_proof(gpu_ok, product, oracle):
+@pytest.mark.parametrize("image_on_main", ["0", "1"])
+def test_stage_after_prove_async_feeds_the_next_proof(gpu_ok, product, oracle, image_on_main):
     """prove_async(i) then stage(i + 1) at once: proof i must read trace i even
     when its worker starts late. SEZKP_TEST_WORKER_DELAY_US holds the worker
     back 50 ms (read once per process, so in a child), so the stage always
     lands before the proof starts; every proof is checked against its own
-    trace's oracle bytes."""
+    trace's oracle bytes. SEZKP_IMAGE_ON_MAIN=1: the staged trace's device
+    transposition runs on the main stream when the proof takes it."""
     import sys
     T, b, tau = 1 << 12, 512, 4
     seeds = (21, 22, 23)
@@ -604,7 +606,7 @@ def test_stage_after_prove_async_feeds_the_next_proof(gpu_ok, product, oracle):
             "c.prove_async(rt[2]); out.append(bytes(c.wait_view()))\n"
             "c.close(); print(' '.join(hashlib.sha256(x).hexdigest() for x in out))\n"
             % (PKG, T, b, tau, seeds))
-    env = dict(os.environ, SEZKP_TEST_WORKER_DELAY_US="50000")
+    env = dict(os.environ, SEZKP_TEST_WORKER_DELAY_US="50000", SEZKP_IMAGE_ON_MAIN=image_on_main)
     child = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
     assert child.returncode == 0, child.stderr[-1500:]
     traces = [product.synthetic_blocks(T, b, tau, s) for s in seeds]
