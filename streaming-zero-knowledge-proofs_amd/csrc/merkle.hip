@@ -330,17 +330,6 @@ __global__ void __launch_bounds__(MK_THREADS) k_layer16(const uint64_t* __restri
   layer16_wg(in, out, logLen, fold, beta, T, blockIdx.x, lds, stop);
 }
 
-// All fold layers of >= 4096 leaves hashed in one launch (their values were
-// produced by the fold chain first): the per-layer trees are independent, so
-// the small layers no longer serialize behind each other's latency.
-__global__ void __launch_bounds__(MK_THREADS) k_forest16(const ForestLayer* __restrict__ layers, int nlayers) {
-  __shared__ uint32_t lds[8][MK_THREADS];
-  int l = 0;
-  while (l + 1 < nlayers && layers[l + 1].wg_start <= blockIdx.x) l++;
-  const ForestLayer F = layers[l];
-  layer16_wg(F.vals, nullptr, F.tree.logLen, 0, 0, F.tree, blockIdx.x - F.wg_start, lds, (int)F.stop);
-}
-
 // FRI fold y'_i = y_i + beta * y_{i+len} (prover.rs:200-239), 4 per lane.
 __global__ void __launch_bounds__(MK_THREADS) k_fold(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
                                                      int logLen, uint64_t beta) {
@@ -453,6 +442,90 @@ __global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
   }
   __syncthreads();
   wg_reduce(lds, nact, lp, 0, T);
+}
+
+// The same small-layer job as k_fri_tail, run by the first workgroups of the
+// forest launch: the fold replay goes through a per-workgroup global scratch
+// (4096 values, L2-resident; workgroup-scope visibility after each barrier)
+// instead of 32 KB of LDS, so these workgroups fit beside the forest's and are
+// dispatched first. As a kernel of its own on the side stream the tail could
+// only start once the forest's ~2K workgroups had all been placed (they fill
+// every CU's VGPRs), and it ended ~60 us after the forest (round 2).
+__device__ __forceinline__ void fri_tail_wg(const TailArgs& A, int j, uint64_t* __restrict__ gbuf,
+                                            uint32_t (*lds)[MK_THREADS]) {
+  __builtin_amdgcn_s_setprio(3);  // a serial chain beside VALU-saturating forest waves
+  const int tid = threadIdx.x;
+  const int L = A.Ls - j;
+  uint64_t* buf = gbuf + ((uint64_t)j << TAIL_MAX);
+  int cur = A.Ls + 1;
+  {  // first fold straight from the source layer
+    const int half = 1 << (cur - 1);
+    for (int i = tid; i < half; i += MK_THREADS) buf[i] = gl_add(A.src[i], gl_mul(A.beta[0], A.src[i + half]));
+    cur--;
+    __syncthreads();
+  }
+  uint64_t* vals = A.vals[0];
+  TreeDev T = A.tree[0];
+#pragma unroll
+  for (int s = 1; s < TAIL_MAX; s++) {
+    if (s <= j) {
+      const int half = 1 << (cur - 1);
+      constexpr int PER = (1 << TAIL_MAX) / 2 / MK_THREADS;
+      uint64_t y[PER];
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const int i = tid + q * MK_THREADS;
+        if (i < half) y[q] = gl_add(buf[i], gl_mul(A.beta[s], buf[i + half]));
+      }
+      __syncthreads();  // every read of this step before any write
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const int i = tid + q * MK_THREADS;
+        if (i < half) buf[i] = y[q];
+      }
+      __syncthreads();
+      cur--;
+    }
+    if (s == j) {
+      vals = A.vals[s];
+      T = A.tree[s];
+    }
+  }
+  const int len = 1 << L;
+  for (int i = tid; i < len; i += MK_THREADS) vals[i] = buf[i];
+  const int lp = L > 8 ? L - 8 : 0;
+  const int nact = len >> lp;
+  if (tid < nact) {
+    uint32_t h[8];
+    const uint64_t i0 = (uint64_t)tid << lp;
+    switch (lp) {
+      case 0: tail_sub<0>(buf, i0, T, h); break;
+      case 1: tail_sub<1>(buf, i0, T, h); break;
+      case 2: tail_sub<2>(buf, i0, T, h); break;
+      default: tail_sub<3>(buf, i0, T, h); break;
+    }
+    lds_put(lds, tid, h);
+  }
+  __syncthreads();
+  wg_reduce(lds, nact, lp, 0, T);
+}
+
+// All fold layers of >= 4096 leaves hashed in one launch (their values were
+// produced by the fold chain first): the per-layer trees are independent, so
+// the small layers no longer serialize behind each other's latency. The first
+// `ntail` workgroups build the layers of <= 2048 leaves (fri_tail_wg).
+__global__ void __launch_bounds__(MK_THREADS) k_forest16(const ForestLayer* __restrict__ layers, int nlayers,
+                                                         TailArgs A, int ntail, uint64_t* __restrict__ tailbuf) {
+  __shared__ uint32_t lds[8][MK_THREADS];
+  if ((int)blockIdx.x < ntail) {
+    fri_tail_wg(A, (int)blockIdx.x, tailbuf, lds);
+    return;
+  }
+  const uint32_t b = blockIdx.x - (uint32_t)ntail;
+  int l = 0;
+  while (l + 1 < nlayers && layers[l + 1].wg_start <= b) l++;
+  const ForestLayer F = layers[l];
+  layer16_wg(F.vals, nullptr, F.tree.logLen, 0, 0, F.tree, b - F.wg_start, lds, (int)F.stop);
 }
 
 // ------------------------------------------------ sharded layout changes
@@ -643,9 +716,14 @@ hipError_t launch_foldm(hipStream_t st, const uint64_t* in, const FoldOuts& outs
   return hipGetLastError();
 }
 
-hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs) {
-  if (nlayers <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_forest16, dim3(total_wgs), dim3(MK_THREADS), 0, st, d_layers, nlayers);
+hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs,
+                           const TailArgs* tail, uint64_t* tailbuf) {
+  if (nlayers <= 0) return tail ? hipErrorInvalidValue : hipSuccess;
+  if (tail && (tail->Ls < 0 || tail->Ls >= TAIL_MAX || !tailbuf)) return hipErrorInvalidValue;
+  const int ntail = tail ? tail->Ls + 1 : 0;
+  const TailArgs none{};
+  hipLaunchKernelGGL(k_forest16, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
+                     tail ? *tail : none, ntail, tailbuf);
   return hipGetLastError();
 }
 

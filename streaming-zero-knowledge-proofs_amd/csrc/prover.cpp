@@ -260,6 +260,7 @@ struct sezkp_ctx {
   int tail_first = 1;                   // first layer of the small-layer tail kernel
   FriLayerDev* d_layers = nullptr;
   ForestLayer* d_forest = nullptr;
+  uint64_t* d_tailbuf = nullptr;   // single device: fold-replay scratch of the small-layer workgroups
   int n_forest = 0;
   uint32_t forest_wgs = 0;
   UpperJob* d_jobs = nullptr;  // upper-level passes: layer 0, then all fold layers
@@ -738,6 +739,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     forest_wgs = wgs;
     d_forest = dalloc<ForestLayer>(fl.size() + 1);
     if (!fl.empty()) up(d_forest, fl.data(), fl.size());
+    d_tailbuf = sharded() ? nullptr : dalloc<uint64_t>((size_t)TAIL_MAX << TAIL_MAX);
   }
   // upper levels (> 12): layer 0's cap, then every other cap / replicated tree
   {
@@ -1199,8 +1201,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   auto beta_of = [&](int r) { return rd64(bb.data() + 8 * r) % GL_P_HOST; };
   // layers of <= 2^11 leaves: one launch on the side stream, overlapping the
   // forest / upper levels (its source is the last fold-chain output)
-  auto launch_tail = [&](const uint64_t* src_vals) {
-    if (tail_first > k) return;
+  auto tail_args = [&](const uint64_t* src_vals) {
     TailArgs ta{};
     ta.src = src_vals;
     ta.Ls = k - tail_first;
@@ -1209,6 +1210,11 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
       ta.vals[j] = lvals[tail_first + j];
       ta.tree[j] = ltrees[tail_first + j];
     }
+    return ta;
+  };
+  auto launch_tail = [&](const uint64_t* src_vals) {
+    if (tail_first > k) return;
+    const TailArgs ta = tail_args(src_vals);
     HIP_OR_THROW(hipEventRecord(ev_fold, st));
     HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
     ok(launch_fri_tail(st2, ta), "fri_tail");
@@ -1232,8 +1238,17 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     }
   }
   const uint64_t* rep_src = rR >= 0 ? lvals[rR] : d_lde;  // full values of the layer above the replicated ones
-  if (!sharded) launch_tail(rep_src);
-  ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
+  // single device: the small layers ride in the forest launch's first
+  // workgroups (SEZKP_TAIL_SEPARATE=1: their own kernel on the side stream)
+  static const bool tail_separate = getenv("SEZKP_TAIL_SEPARATE") != nullptr;
+  const bool tail_merged = !sharded && tail_first <= k && n_forest > 0 && d_tailbuf && !tail_separate;
+  if (tail_merged) {
+    const TailArgs ta = tail_args(rep_src);
+    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf), "fri_forest");
+  } else {
+    if (!sharded) launch_tail(rep_src);
+    ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
+  }
   if (sharded) {  // run roots of layers 1..rR + the whole of layer rR
     uint64_t wire = P1 * S * 8;
     for (int r = 1; r <= rR; r++) wire += P1 * ((N >> r) >> (L16_LOG + logP)) * 32;
@@ -1257,7 +1272,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   }
   if (sharded) launch_tail(rep_src);
   for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
-  if (tail_first <= k) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
+  if (tail_first <= k && !tail_merged) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
   rec(ST_FRI + 1);
   if (copy_roots) HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
   sync();

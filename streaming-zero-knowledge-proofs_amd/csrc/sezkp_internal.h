@@ -317,7 +317,7 @@ struct ForestLayer {
   uint32_t wg_start;  // first WG of this layer in the forest launch
   uint32_t stop;      // level the WG reduces to (see launch_layer16)
 };
-hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs);
+
 // Small FRI layers (logLen <= Ls <= 11) in one launch; layer Ls - j is
 // folded from layer Ls - j + 1 with beta[j]; src = layer Ls + 1.
 constexpr int TAIL_MAX = 12;
@@ -329,6 +329,10 @@ struct TailArgs {
   TreeDev tree[TAIL_MAX];
 };
 hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a);
+// the forest of layer trees >= 4096 leaves; tail != null: its first workgroups
+// also build the small layers (fri_tail_wg), tailbuf = TAIL_MAX x 4096 u64 scratch
+hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs,
+                           const TailArgs* tail = nullptr, uint64_t* tailbuf = nullptr);
 // requests: (layer, index, ordinal in the proof's FRI records) triples
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
                             const ProofLayout& P);

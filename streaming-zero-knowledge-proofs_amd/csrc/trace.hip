@@ -1391,7 +1391,9 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
     }
   }
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
-  static const bool xcd = !getenv("SEZKP_DICT_XCD") || atoi(getenv("SEZKP_DICT_XCD")) != 0;
+  // measured slower (round 3, single-proof k_col_commit_dict 335 -> 355 us,
+  // tools/ab_dict_xcd.sh): off by default, SEZKP_DICT_XCD=1 for A/B
+  static const bool xcd = getenv("SEZKP_DICT_XCD") && atoi(getenv("SEZKP_DICT_XCD")) != 0;
   if (xcd && ndict > 8) {
     const uint64_t per_xcd = (uint64_t)((ndict + 7) / 8) * gx;  // work items of the busiest XCD
     hipLaunchKernelGGL(k_col_commit_dict, dim3((unsigned)(8 * per_xcd)), dim3(64), 0, st, T, d_tmpl, d_dcols,
