@@ -402,6 +402,45 @@ __device__ __forceinline__ void lds_to_transposed(const uint64_t* sh, const NttP
   }
 }
 
+// nat_tr on the DIT side (the first, narrow pass of a natural-order DIT
+// transform): slot p of the DIT input holds x[bitrev_N(p)]. A plain narrow
+// tile (m <= 8) takes the 16 blocks B_i = bitrev_{N-m}(16 T + i): for every
+// in-block slot e their inputs x[bitrev_m(e) 2^(N-m) + 16 T + i] are one
+// contiguous 128-B segment; the blocks go back to their own slots (2^m
+// contiguous points each). An X16 tile (one 2^(m+4)-point sub-transform)
+// reads single points 2^(N-m-4) apart: the 16 tiles whose bitrev(T) are
+// consecutive share those lines, and nat_tile dispatches them back to back
+// on one XCD so the lines are fetched once into its L2.
+template <int R, bool XT>
+__device__ __forceinline__ void gather_dit_to_lds(uint64_t* sh, const uint64_t* __restrict__ x, uint64_t tile,
+                                                  int logN) {
+  constexpr int m = __builtin_ctz(R);
+#pragma unroll
+  for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
+    const int e = j * NTT_THREADS + threadIdx.x;
+    if constexpr (!XT) {
+      const int i = e & (NTT_CMAX - 1), row = e >> 4;
+      sh[row * NTT_PADC + i] =
+          x[((uint64_t)(__brev((uint32_t)row) >> (32 - m)) << (logN - m)) + tile * NTT_CMAX + i];
+    } else {
+      const int lo = logN - m - 4;  // tile index bits
+      const uint64_t hi = __brev((uint32_t)e) >> (32 - m - 4), bt = lo ? __brev((uint32_t)tile) >> (32 - lo) : 0;
+      sh[(e & (R - 1)) * NTT_PADC + (e >> m)] = x[(hi << lo) | bt];
+    }
+  }
+}
+template <int R>
+__device__ __forceinline__ void lds_to_blocks(const uint64_t* sh, uint64_t* __restrict__ a, uint64_t tile, int logN) {
+  constexpr int m = __builtin_ctz(R);
+  const int sb = 32 - (logN - m);
+#pragma unroll
+  for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
+    const int e = j * NTT_THREADS + threadIdx.x, i = e >> m, row = e & (R - 1);
+    const uint64_t B = __brev((uint32_t)(tile * NTT_CMAX + i)) >> sb;
+    a[(B << m) + row] = sh[row * NTT_PADC + i];
+  }
+}
+
 // dispatch order of a nat_out pass: tiles T and T + j G (G = tiles / 16)
 // write the same output lines; 16 consecutive workgroups of one XCD
 // (workgroup b runs on XCD b mod 8) take one such group
@@ -455,7 +494,7 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   Tile G;
   G.sL = P.sL;
   G.m = m;
-  G.tile = (NARROW && P.nat_out) ? nat_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  G.tile = (NARROW && (P.nat_out || (X16 && !DIF && P.nat_tr))) ? nat_tile(blockIdx.x, gridDim.x) : blockIdx.x;
   G.wide = (1ULL << G.sL) >= (uint64_t)NTT_CMAX;
   G.blk_base = 0;
   G.low0 = 0;
@@ -470,6 +509,9 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   const bool staged_load = NARROW && !P.dp_rlo && !P.src;
   if constexpr (NARROW && DIF && !X16) {
     if (P.nat_tr) gather_to_lds<R>(sh, P.a, G.tile, P.nat_logN);
+    else if (staged_load) narrow_to_lds<R>(sh, P.a, G.tile);
+  } else if constexpr (NARROW && !DIF && SKIP == 0) {
+    if (staged_load && P.nat_tr) gather_dit_to_lds<R, X16>(sh, P.a, G.tile, P.nat_logN);
     else if (staged_load) narrow_to_lds<R>(sh, P.a, G.tile);
   } else if (staged_load) {
     narrow_to_lds<R>(sh, P.a, G.tile);
@@ -506,9 +548,18 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
       } else {
 #pragma unroll
         for (int r = 0; r < F1; r++) x[r] = P.a[tile_pos(G, F1 * u + r, c, low)];
+        // out_scale > 1 (the last pass of an inverse natural-order transform):
+        // n^-1 rides on the pre-twiddle chain (one product per thread), the
+        // rare low = 0 column is scaled point by point
+        const bool scale = P.out_scale > 1;
+        if (scale && low == 0) {
+#pragma unroll
+          for (int r = 0; r < F1; r++) x[r] = gl_mul(x[r], P.out_scale);
+        }
         if (low != 0) {  // pre-twiddle w^(low * (j1 + F2 j2)), j2 = rev(r)
           const int j1 = rev<M2>(u);
           uint64_t t = tw_pow(T, (low * (uint64_t)j1) << tw_shift, INV);
+          if (scale) t = gl_mul(t, P.out_scale);
           const uint64_t s1 = tw_pow(T, (low * (uint64_t)F2) << tw_shift, INV);
 #pragma unroll
           for (int q = 0; q < F1; q++) {  // x[rev(q)] *= t s1^q, the chain applied as it goes
@@ -548,8 +599,9 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
           P.a[tile_pos(G, k2 + F1 * k1, c, low)] = gl_mul(sh[(k1 * F1 + k2) * NTT_PADC + c], inv);
         });
       } else if (!NARROW) {
+        uint64_t* dst = P.out ? P.out : P.a;
 #pragma unroll
-        for (int k1 = 0; k1 < F2; k1++) P.a[tile_pos(G, k2 + F1 * k1, c, low)] = y[k1];
+        for (int k1 = 0; k1 < F2; k1++) dst[tile_pos(G, k2 + F1 * k1, c, low)] = y[k1];
       }
     }
     if constexpr (NARROW) {  // rows k2 + F1 k1 back through the image, lane-consecutive stores
@@ -563,7 +615,8 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
         tile_radix16<R, false, INV>(sh, T);
         __syncthreads();
       }
-      lds_to_narrow<R>(sh, P.a, G.tile);
+      if (!X16 && P.nat_tr) lds_to_blocks<R>(sh, P.out ? P.out : P.a, G.tile, P.nat_logN);
+      else lds_to_narrow<R>(sh, P.out ? P.out : P.a, G.tile);
     }
   } else {
     uint64_t x[F2];
@@ -1269,9 +1322,44 @@ static bool ntt_dif_natural_tr(hipStream_t st, uint64_t* a, uint64_t* scratch, i
   return true;
 }
 
+// Natural order as a DIT whose first (narrow) pass gathers its input in
+// bit-reversed order (gather_dit_to_lds): the plain plans of 2^21..2^24 and
+// the X16 plans of 2^19, 2^20 and 2^25..2^28, no bit-reversal pass. The first
+// pass reads `a` and writes `scratch`, the middle ones run in place on
+// scratch, the last one writes `a` (n^-1 on its pre-twiddle chain).
+// SEZKP_NTT_NAT_DIT=0: keep the DIF forms below (A/B).
+static bool nat_dit_disabled() {
+  static const bool off = getenv("SEZKP_NTT_NAT_DIT") && atoi(getenv("SEZKP_NTT_NAT_DIT")) == 0;
+  return off;
+}
+static bool ntt_dit_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse,
+                            const NttTables& T, uint64_t scale, hipError_t* err) {
+  if (logN < 19 || logN > 28 || nat_dit_disabled() || ntt4_disabled() || narrow_disabled()) return false;
+  int ms[8], np;
+  const bool x16 = plan_passes_x16(logN, false, ms, &np);
+  if (!x16) plan_passes(logN, 1, ms, &np);
+  if (np < 2 || (!x16 && ms[0] > NTT_MMAX)) return false;
+  int sL = 0;
+  for (int i = 0; i < np; i++) {
+    NttPassArgs P{};
+    P.tw = T; P.m = ms[i]; P.sL = sL; P.inverse = inverse ? 1 : 0; P.logC = 4;
+    P.a = i == 0 ? a : scratch;
+    P.out = i == 0 ? scratch : (i == np - 1 ? a : nullptr);
+    if (i == 0) { P.nat_tr = 1; P.nat_logN = logN; }
+    if (i == np - 1) P.out_scale = scale;
+    const unsigned tiles = (unsigned)(P.m > NTT_MMAX ? (1ULL << logN) >> P.m : (1ULL << logN) >> (P.m + 4));
+    const bool ok = inverse ? launch_ntt4<false, true>(st, P, tiles) : launch_ntt4<false, false>(st, P, tiles);
+    if (!ok) { *err = hipErrorInvalidValue; return true; }
+    sL += ms[i];
+  }
+  *err = hipGetLastError();
+  return true;
+}
+
 bool ntt_dif_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse, const NttTables& T,
                      uint64_t scale, hipError_t* err) {
   *err = hipSuccess;
+  if (scratch && scratch != a && ntt_dit_natural(st, a, scratch, logN, inverse, T, scale, err)) return true;
   if (scratch && scratch != a && ntt_dif_natural_tr(st, a, scratch, logN, inverse, T, scale, err)) return true;
   // measured (profiles/r02_ntt_nat_ab.txt): 1-5% faster at 2^19..2^22, slower from 2^24 (where the
   // scattered lines no longer merge in L2 before write-back: 687 vs 577 us at 2^24)

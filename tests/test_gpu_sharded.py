@@ -269,6 +269,8 @@ def _fail_worker(rank, world, port, point, q):
     except Exception as e:
         res += [f"setup: {e}", 0.0, ""]
     q.put(tuple(res))
+    q.close()
+    q.join_thread()  # the result must reach the parent before the hard exit below
     os._exit(0)  # gloo may hold a timed-out collective: leave without a teardown handshake
 
 
@@ -285,7 +287,7 @@ def test_sharded_failure_on_one_rank_fails_every_rank(gpu_ok, point):
     ps = [ctx.Process(target=_fail_worker, args=(r, 2, port, point, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = sorted(q.get(timeout=240) for _ in ps)
+    res = sorted(q.get(timeout=150) for _ in ps)
     for p in ps:
         p.join(timeout=30)
         if p.is_alive():
@@ -314,7 +316,8 @@ def test_sharded_rccl_abort_after_failure(gpu_ok, product):
     env = dict(os.environ, SEZKP_FORCE_SHARDED="1", SEZKP_DEBUG_FAIL_AT="0:lde_alltoall")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr[-1500:]
-    lines = r.stdout.strip().splitlines()
+    # RCCL prints a banner on stdout: keep the script's own lines
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith(("ERR", "no error", "closed"))]
     assert "injected failure before collective lde_alltoall on rank 0" in lines[0], lines
     assert "context unusable" in lines[1], lines
     assert lines[2] == "closed"
