@@ -1334,11 +1334,17 @@ static bool nat_dit_disabled() {
 }
 static bool ntt_dit_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse,
                             const NttTables& T, uint64_t scale, hipError_t* err) {
-  if (logN < 19 || logN > 28 || nat_dit_disabled() || ntt4_disabled() || narrow_disabled()) return false;
+  // measured (round 3, profiles/r03/ntt_nat_ab2.txt, fwd + inv round trips):
+  // 2^21 96.6 vs 129.0 us (DIF natural store), 2^22 164.9 vs 178.6, 2^23 275.9
+  // vs 283.2, 2^24 498.5 vs 508.7 (584.8 with the bit-reversal pass); the
+  // X16 plans' point gather loses (2^25 1267 vs 1053, 2^26 2493 vs 2109), so
+  // those sizes keep the DIF forms
+  if (logN < 21 || logN > 24 || nat_dit_disabled() || ntt4_disabled() || narrow_disabled()) return false;
   int ms[8], np;
-  const bool x16 = plan_passes_x16(logN, false, ms, &np);
-  if (!x16) plan_passes(logN, 1, ms, &np);
-  if (np < 2 || (!x16 && ms[0] > NTT_MMAX)) return false;
+  if (plan_passes_x16(logN, false, ms, &np)) return false;
+  plan_passes(logN, 1, ms, &np);
+  const bool x16 = false;
+  if (np < 2 || ms[0] > NTT_MMAX) return false;
   int sL = 0;
   for (int i = 0; i < np; i++) {
     NttPassArgs P{};

@@ -686,6 +686,19 @@ __device__ __forceinline__ void load_keys(const Key* __restrict__ p, int64_t (&k
         k[q * PER + i] = (int64_t)(Key)raw;
       }
     }
+  } else if constexpr ((BYTES == 8 || BYTES == 4) && sizeof(Key) < 8) {
+    // one 8- or 4-byte load per table node instead of CNT narrow loads: the
+    // lanes of a wave sit 2^(6+a) rows apart, so every load instruction
+    // touches 64 cache lines and the commit was bound by load issue
+    // (mv: 8 byte loads per node, wsym: 4 short loads)
+    uint64_t w;
+    if constexpr (BYTES == 8) w = *reinterpret_cast<const uint64_t*>(p);
+    else w = *reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+    for (int i = 0; i < CNT; i++) {
+      const int bit = i * 8 * (int)sizeof(Key);
+      k[i] = (int64_t)(Key)((w >> bit) & ((1ull << (8 * sizeof(Key))) - 1ull));
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < CNT; i++) k[i] = (int64_t)p[i];
