@@ -403,30 +403,22 @@ __device__ __forceinline__ void lds_to_transposed(const uint64_t* sh, const NttP
 }
 
 // nat_tr on the DIT side (the first, narrow pass of a natural-order DIT
-// transform): slot p of the DIT input holds x[bitrev_N(p)]. A plain narrow
-// tile (m <= 8) takes the 16 blocks B_i = bitrev_{N-m}(16 T + i): for every
-// in-block slot e their inputs x[bitrev_m(e) 2^(N-m) + 16 T + i] are one
-// contiguous 128-B segment; the blocks go back to their own slots (2^m
-// contiguous points each). An X16 tile (one 2^(m+4)-point sub-transform)
-// reads single points 2^(N-m-4) apart: the 16 tiles whose bitrev(T) are
-// consecutive share those lines, and nat_tile dispatches them back to back
-// on one XCD so the lines are fetched once into its L2.
-template <int R, bool XT>
+// transform, m <= 8): slot p of the DIT input holds x[bitrev_N(p)]. Tile T
+// takes the 16 blocks B_i = bitrev_{N-m}(16 T + i): for every in-block slot e
+// their inputs x[bitrev_m(e) 2^(N-m) + 16 T + i] are one contiguous 128-B
+// segment; the blocks go back to their own slots (2^m contiguous points
+// each). (An X16 tile, one 2^(m+4)-point sub-transform, would read single
+// points 2^(N-m-4) apart and rely on L2 sharing between 16 tiles: measured
+// 2^25 1267 vs 1053 us and 2^26 2493 vs 2109 us per round trip against the DIF
+// transposed store, so it is not built.)
+template <int R>
 __device__ __forceinline__ void gather_dit_to_lds(uint64_t* sh, const uint64_t* __restrict__ x, uint64_t tile,
                                                   int logN) {
   constexpr int m = __builtin_ctz(R);
 #pragma unroll
   for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
-    const int e = j * NTT_THREADS + threadIdx.x;
-    if constexpr (!XT) {
-      const int i = e & (NTT_CMAX - 1), row = e >> 4;
-      sh[row * NTT_PADC + i] =
-          x[((uint64_t)(__brev((uint32_t)row) >> (32 - m)) << (logN - m)) + tile * NTT_CMAX + i];
-    } else {
-      const int lo = logN - m - 4;  // tile index bits
-      const uint64_t hi = __brev((uint32_t)e) >> (32 - m - 4), bt = lo ? __brev((uint32_t)tile) >> (32 - lo) : 0;
-      sh[(e & (R - 1)) * NTT_PADC + (e >> m)] = x[(hi << lo) | bt];
-    }
+    const int e = j * NTT_THREADS + threadIdx.x, i = e & (NTT_CMAX - 1), row = e >> 4;
+    sh[row * NTT_PADC + i] = x[((uint64_t)(__brev((uint32_t)row) >> (32 - m)) << (logN - m)) + tile * NTT_CMAX + i];
   }
 }
 template <int R>
@@ -494,7 +486,7 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   Tile G;
   G.sL = P.sL;
   G.m = m;
-  G.tile = (NARROW && (P.nat_out || (X16 && !DIF && P.nat_tr))) ? nat_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  G.tile = (NARROW && P.nat_out) ? nat_tile(blockIdx.x, gridDim.x) : blockIdx.x;
   G.wide = (1ULL << G.sL) >= (uint64_t)NTT_CMAX;
   G.blk_base = 0;
   G.low0 = 0;
@@ -510,8 +502,8 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
   if constexpr (NARROW && DIF && !X16) {
     if (P.nat_tr) gather_to_lds<R>(sh, P.a, G.tile, P.nat_logN);
     else if (staged_load) narrow_to_lds<R>(sh, P.a, G.tile);
-  } else if constexpr (NARROW && !DIF && SKIP == 0) {
-    if (staged_load && P.nat_tr) gather_dit_to_lds<R, X16>(sh, P.a, G.tile, P.nat_logN);
+  } else if constexpr (NARROW && !DIF && SKIP == 0 && !X16) {
+    if (staged_load && P.nat_tr) gather_dit_to_lds<R>(sh, P.a, G.tile, P.nat_logN);
     else if (staged_load) narrow_to_lds<R>(sh, P.a, G.tile);
   } else if (staged_load) {
     narrow_to_lds<R>(sh, P.a, G.tile);
@@ -1323,8 +1315,8 @@ static bool ntt_dif_natural_tr(hipStream_t st, uint64_t* a, uint64_t* scratch, i
 }
 
 // Natural order as a DIT whose first (narrow) pass gathers its input in
-// bit-reversed order (gather_dit_to_lds): the plain plans of 2^21..2^24 and
-// the X16 plans of 2^19, 2^20 and 2^25..2^28, no bit-reversal pass. The first
+// bit-reversed order (gather_dit_to_lds): the plain plans of 2^21..2^24, no
+// bit-reversal pass. The first
 // pass reads `a` and writes `scratch`, the middle ones run in place on
 // scratch, the last one writes `a` (n^-1 on its pre-twiddle chain).
 // SEZKP_NTT_NAT_DIT=0: keep the DIF forms below (A/B).
@@ -1343,7 +1335,6 @@ static bool ntt_dit_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int 
   int ms[8], np;
   if (plan_passes_x16(logN, false, ms, &np)) return false;
   plan_passes(logN, 1, ms, &np);
-  const bool x16 = false;
   if (np < 2 || ms[0] > NTT_MMAX) return false;
   int sL = 0;
   for (int i = 0; i < np; i++) {
