@@ -710,25 +710,38 @@ __global__ void __launch_bounds__(512, 2) k_ntt_dif9(NttPassArgs P) {
     }
   }
   __syncthreads();
-  if (g < F2) {  // step 2: thread (c, q), registers r
-    const int q = g;
-    uint64_t y[F1];
+  {  // step 2: the 32-point DIF over r of column q as two threads (c, q, h):
+     // its first radix-2 stage (pairs r, r + 16; twiddle w_32^r, a shift) is
+     // split by output half, h = 0 the sums, h = 1 the differences, then each
+     // thread runs a 16-point DIF. Slot s of thread h is slot s + 16 h of
+     // the 32-point output, i.e. k_hi = 2 rev4(s) + h. All 512 threads busy.
+    const int q = g & (F2 - 1), h = g >> M2;
+    uint64_t y[16];
 #pragma unroll
-    for (int r = 0; r < F1; r++) y[r] = sh[(q * F1 + r) * NTT_PADC + c];
-    fft_dif_regs<M1, INV>(y);
+    for (int r = 0; r < 16; r++) {
+      const uint64_t a = sh[(q * F1 + r) * NTT_PADC + c], b = sh[(q * F1 + r + 16) * NTT_PADC + c];
+      if (h == 0) {
+        y[r] = gl_add(a, b);
+      } else {
+        const int e = r ? tw_exp<INV>(r, 16) : 0;
+        const bool neg = e >= 96;
+        y[r] = gl_mul2e(neg ? gl_sub(b, a) : gl_sub(a, b), neg ? e - 96 : e);
+      }
+    }
+    fft_dif_regs<4, INV>(y);
     (void)tile_pos(G, q * F1, c, low);
-    if (low != 0) {  // post-twiddle w^(low * (k_lo + F2 k_hi)), k_hi = rev(qq)
-      uint64_t t = tw_pow(T, (low * (uint64_t)rev<M2>(q)) << tw_shift, INV);
-      const uint64_t s1 = tw_pow(T, (low * (uint64_t)F2) << tw_shift, INV);
+    if (low != 0) {  // post-twiddle w^(low * (k_lo + F2 k_hi)), k_hi = 2 k' + h, slot rev4(k')
+      uint64_t t = tw_pow(T, (low * ((uint64_t)rev<M2>(q) + (uint64_t)F2 * h)) << tw_shift, INV);
+      const uint64_t s2 = tw_pow(T, (low * (uint64_t)(2 * F2)) << tw_shift, INV);
 #pragma unroll
-      for (int kh = 0; kh < F1; kh++) {
-        y[rev<M1>(kh)] = gl_mul(y[rev<M1>(kh)], t);
-        if (kh + 1 < F1) t = gl_mul(t, s1);
+      for (int kp = 0; kp < 16; kp++) {
+        y[rev<4>(kp)] = gl_mul(y[rev<4>(kp)], t);
+        if (kp + 1 < 16) t = gl_mul(t, s2);
       }
     }
     uint64_t* dst = P.out ? P.out : P.a;
 #pragma unroll
-    for (int qq = 0; qq < F1; qq++) dst[tile_pos(G, q * F1 + qq, c, low)] = y[qq];
+    for (int s = 0; s < 16; s++) dst[tile_pos(G, q * F1 + 16 * h + s, c, low)] = y[s];
   }
 }
 
