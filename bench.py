@@ -365,7 +365,7 @@ def main():
                     help="watchdog: print the main line and exit (status 3) if an extra measurement stalls")
     ap.add_argument("--dntt-log-n", type=int, default=26,
                     help="distributed four-step NTT sub-measurement size (BASELINE config 4: 2^26); 0 = skip")
-    ap.add_argument("--dntt-steps", type=int, default=5)
+    ap.add_argument("--dntt-steps", type=int, default=20)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -912,7 +912,8 @@ def measure_dist_ntt(args, world, rank, local, dist, torch):
     per = dt / (2 * args.dntt_steps)
     alg = 16 * M / per / 1e9  # read + write each local element once, per GPU
     shape = (f"four-step: local 2^{log_n - (world.bit_length() - 1)} NTT, twiddle, 1 RCCL all-to-all, "
-             f"{world}-point DFTs" if world > 1 else "one rank: local NTT + in-place bit reversal, no exchange")
+             f"{world}-point DFTs" if world > 1 else
+             "one rank: natural-order local NTT (DIF passes with the transposed last pass), no exchange")
     return {"workload": f"2^{log_n}-point Goldilocks NTT over {world} GPU(s), forward + inverse ({shape})",
             "value": n / per, "unit": "field-elements/s", "ms_per_transform": per * 1e3, "steps": args.dntt_steps,
             "scaling": "strong", "roundtrip_ok": ok, "alg_GBs_per_gpu": alg, "frac_hbm_alg": alg / HBM_PEAK_GBS}
