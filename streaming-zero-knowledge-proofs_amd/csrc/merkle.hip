@@ -597,6 +597,23 @@ __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict_
     o[2] = (uint32_t)L;
     o[3] = 0;
   }
+  // stored siblings above the group: lane (j, w) takes word w of level
+  // glog + 8 i + j. All loads issued up front, so their latency overlaps the
+  // group's hashing instead of one dependent load/store round per level.
+  constexpr int PATH_ROUNDS = (64 - LSTORE_FRI + 7) / 8;
+  uint32_t sw[PATH_ROUNDS];
+#pragma unroll
+  for (int i = 0; i < PATH_ROUNDS; i++) {
+    const int lvl = glog + 8 * i + (lane >> 3);
+    if (lvl >= L) break;
+    if (lvl < C.lstore) {  // inside this rank's run subtree (local tree)
+      const uint64_t sib = (li >> lvl) ^ 1;
+      sw[i] = T.nodes[8 * (tree_level_off(T.logLen, T.lstore, lvl) + sib) + (lane & 7)];
+    } else {               // cap levels (global indices)
+      const uint64_t sib = (idx >> lvl) ^ 1;
+      sw[i] = C.nodes[8 * (tree_level_off(C.logLen, C.lstore, lvl) + sib) + (lane & 7)];
+    }
+  }
   if (lane < (int)g) {
     uint32_t h[8];
     b3_leaf_u64(Ly.vals[base + lane], h);
@@ -620,16 +637,11 @@ __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict_
     __syncthreads();
     cnt = half;
   }
-  for (int lvl = glog; lvl < L; lvl++) {
-    uint32_t s;
-    if (lvl < C.lstore) {  // inside this rank's run subtree (local tree)
-      const uint64_t sib = (li >> lvl) ^ 1;
-      s = T.nodes[8 * (tree_level_off(T.logLen, T.lstore, lvl) + sib) + (lane & 7)];
-    } else {               // cap levels (global indices)
-      const uint64_t sib = (idx >> lvl) ^ 1;
-      s = C.nodes[8 * (tree_level_off(C.logLen, C.lstore, lvl) + sib) + (lane & 7)];
-    }
-    if (lane < 8) o[4 + 8 * lvl + lane] = s;
+#pragma unroll
+  for (int i = 0; i < PATH_ROUNDS; i++) {
+    const int lvl = glog + 8 * i + (lane >> 3);
+    if (lvl >= L) break;
+    o[4 + 8 * lvl + (lane & 7)] = sw[i];
   }
 }
 

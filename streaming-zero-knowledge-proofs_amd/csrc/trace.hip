@@ -868,6 +868,14 @@ __device__ __forceinline__ void dict_node_at(const TraceDev& T, const ColTemplat
 #undef SEZKP_DN
 }
 
+// path_in_chunk siblings at levels glog..9 of a dictionary column, stored by
+// the commitment: thread (level, word), one round of loads
+__device__ __forceinline__ void copy_dlev_siblings(const uint32_t* __restrict__ lev, uint64_t in, int glog,
+                                                   uint32_t* __restrict__ o) {
+  const int lvl = glog + (threadIdx.x >> 3), w = threadIdx.x & 7;
+  if (lvl < COL_CHUNK_LOG2) o[18 + 8 * lvl + w] = lev[8 * (dlev_base(lvl) + ((in >> lvl) ^ 1)) + w];
+}
+
 // One 256-lane WG per request (column, row). Record words: [0,1] value,
 // [2..9] chunk_root, [10..89] path_in (<= 10), [90..345] path_to_chunk (<= 32).
 //  - piecewise columns: sibling at level l = hash of an aligned 2^l-row range
@@ -917,6 +925,13 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
     o[1] = (uint32_t)(v >> 32);
   }
   const uint32_t* ob = outer + (uint64_t)c * outer_stride * 8;
+  {  // path_to_chunk from the stored outer tree (all levels kept): thread
+     // (level, word), one round of independent loads instead of a dependent
+     // load / store per level on 8 lanes
+    uint32_t* op = o + 20 + 8 * logcl;
+    const int lvl = tid >> 3, w = tid & 7;
+    if (lvl < logChunks) op[8 * lvl + w] = ob[8 * (tree_level_off(logChunks, 0, lvl) + ((ch >> lvl) ^ 1)) + w];
+  }
   const bool pw = kind_piecewise(ct.kind) && ct.tab != NO_TAB;
   const bool dict = dsel != NO_DICT && logcl == COL_CHUNK_LOG2;
   const int K = dict ? plans[dsel].K : -1;
@@ -974,10 +989,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
       cnt = half;
     }
     const uint32_t* lev = dlev + 8 * ((uint64_t)dsel * (T.n >> COL_CHUNK_LOG2) + ch) * DLEV_NODES;
-    for (int lvl = glog; lvl < COL_CHUNK_LOG2; lvl++) {
-      const uint64_t sib = (in >> lvl) ^ 1;
-      if (tid < 8) o[18 + 8 * lvl + tid] = lev[8 * (dlev_base(lvl) + sib) + tid];
-    }
+    copy_dlev_siblings(lev, in, glog, o);
     if (tid < 8) o[8 + tid] = ob[8 * ch + tid];
   } else {
     // rebuild the chunk (or, for a K = -1 dictionary column, its 64-row group)
@@ -1014,20 +1026,11 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
     }
     if (dict) {
       const uint32_t* lev = dlev + 8 * ((uint64_t)dsel * (T.n >> COL_CHUNK_LOG2) + ch) * DLEV_NODES;
-      for (int lvl = glog; lvl < COL_CHUNK_LOG2; lvl++) {
-        const uint64_t sib = (in >> lvl) ^ 1;
-        if (tid < 8) o[18 + 8 * lvl + tid] = lev[8 * (dlev_base(lvl) + sib) + tid];
-      }
+      copy_dlev_siblings(lev, in, glog, o);
       if (tid < 8) o[8 + tid] = ob[8 * ch + tid];  // chunk root = outer leaf
     } else {
       if (tid < 8) o[8 + tid] = lds[tid][0];
     }
-  }
-  // path_to_chunk from the stored outer tree (all levels kept)
-  uint32_t* op = o + 20 + 8 * logcl;
-  for (int lvl = 0; lvl < logChunks; lvl++) {
-    const uint64_t sib = (ch >> lvl) ^ 1;
-    if (tid < 8) op[8 * lvl + tid] = ob[8 * (tree_level_off(logChunks, 0, lvl) + sib) + tid];
   }
 }
 
