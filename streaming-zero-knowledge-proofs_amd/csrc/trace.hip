@@ -705,19 +705,63 @@ __device__ __forceinline__ void load_keys(const Key* __restrict__ p, int64_t (&k
   }
 }
 
-// Node providers for lane_tree: node j of the lane's 2^D nodes.
+// Node providers for lane_tree: node j of the lane's 2^D nodes. The gathered
+// providers also split get() into raw(j) (the node's key bytes, one load)
+// and node(raw) (table index, node load) for lane_tree_pf.
 template <typename Key, int K>
 struct DictNodes {
   const Key* p;           // first row of the lane
   const uint32_t* tab;    // T_K
   int64_t mn;
   uint32_t R;
+  static constexpr int CNT = 1 << K;
+  static constexpr int BYTES = CNT * (int)sizeof(Key);
+  static constexpr int NW = BYTES >= 4 ? BYTES / 4 : 1;
+  struct Raw {
+    uint32_t w[NW];
+  };
   __device__ __forceinline__ void get(int j, uint32_t (&h)[8]) const {
     int64_t k[1 << K];
     load_keys<Key, (1 << K)>(p + ((uint64_t)j << K), k);
     uint32_t idx = 0;
 #pragma unroll
     for (int i = (1 << K) - 1; i >= 0; i--) idx = idx * R + (uint32_t)(k[i] - mn);
+    node_load(tab + 8 * (uint64_t)idx, h);
+  }
+  __device__ __forceinline__ Raw raw(int j) const {
+    Raw r;
+    const Key* q = p + ((uint64_t)j << K);
+    if constexpr (BYTES >= 16) {
+#pragma unroll
+      for (int i = 0; i < BYTES / 16; i++) {
+        const uint4 v = reinterpret_cast<const uint4*>(q)[i];
+        r.w[4 * i] = v.x; r.w[4 * i + 1] = v.y; r.w[4 * i + 2] = v.z; r.w[4 * i + 3] = v.w;
+      }
+    } else if constexpr (BYTES == 8) {
+      const uint2 v = *reinterpret_cast<const uint2*>(q);
+      r.w[0] = v.x; r.w[1] = v.y;
+    } else if constexpr (BYTES == 4) {
+      r.w[0] = *reinterpret_cast<const uint32_t*>(q);
+    } else if constexpr (BYTES == 2) {
+      r.w[0] = *reinterpret_cast<const uint16_t*>(q);
+    } else {
+      r.w[0] = *reinterpret_cast<const uint8_t*>(q);
+    }
+    return r;
+  }
+  __device__ __forceinline__ void node(const Raw& r, int, uint32_t (&h)[8]) const {
+    uint32_t idx = 0;
+#pragma unroll
+    for (int i = CNT - 1; i >= 0; i--) {
+      int64_t k;
+      if constexpr (sizeof(Key) == 8) {
+        k = (int64_t)((uint64_t)r.w[2 * i] | ((uint64_t)r.w[2 * i + 1] << 32));
+      } else {
+        const int bit = i * 8 * (int)sizeof(Key);
+        k = (int64_t)(Key)((r.w[bit / 32] >> (bit % 32)) & ((1u << (8 * sizeof(Key))) - 1u));
+      }
+      idx = idx * R + (uint32_t)(k - mn);
+    }
     node_load(tab + 8 * (uint64_t)idx, h);
   }
 };
@@ -746,6 +790,30 @@ struct DeltaNodes {
       b3_parent(a, b, h);
     }
   }
+  // lane_tree_pf split: flags, moves and the first head of the group (the
+  // other three heads are read only in the rare block-start case)
+  struct Raw {
+    uint32_t f, m;
+    int64_t h0;
+  };
+  __device__ __forceinline__ Raw raw(int j) const {
+    const uint64_t g = (uint64_t)j << 2;
+    return Raw{*reinterpret_cast<const uint32_t*>(fp + g), *reinterpret_cast<const uint32_t*>(mp + g), hp[g]};
+  }
+  __device__ __forceinline__ void node(const Raw& r, int j, uint32_t (&h)[8]) const {
+    const int64_t c0 = r.h0 - mn;
+    if (!(r.f & 0x01010100u)) {
+      const int64_t d1 = (int64_t)(int8_t)(r.m >> 8) - dmin, d2 = (int64_t)(int8_t)(r.m >> 16) - dmin,
+                    d3 = (int64_t)(int8_t)(r.m >> 24) - dmin;
+      node_load(td + 8 * (uint64_t)(c0 + (int64_t)R * (d1 + (int64_t)dR * (d2 + (int64_t)dR * d3))), h);
+    } else {
+      const uint64_t g = (uint64_t)j << 2;
+      uint32_t a[8], b[8];
+      node_load(t1 + 8 * (uint64_t)(c0 + (int64_t)R * (hp[g + 1] - mn)), a);
+      node_load(t1 + 8 * (uint64_t)((hp[g + 2] - mn) + (int64_t)R * (hp[g + 3] - mn)), b);
+      b3_parent(a, b, h);
+    }
+  }
 };
 template <typename Key>
 struct RawLeaves {
@@ -765,6 +833,44 @@ __device__ __forceinline__ void lane_tree(const Prov& P, uint32_t (&h)[8]) {
   for (int j = 0; j < (1 << D); j++) {
     uint32_t x[8];
     P.get(j, x);
+    bool done = false;
+#pragma unroll
+    for (int l = 0; l < D; l++) {
+      if (!done) {
+        if ((j >> l) & 1) {
+          b3_parent(s[l], x, x);
+        } else {
+#pragma unroll
+          for (int w = 0; w < 8; w++) s[l][w] = x[w];
+          done = true;
+        }
+      }
+    }
+    if (!done) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) h[w] = x[w];
+    }
+  }
+}
+// lane_tree with the gathers software-pipelined: while node j is merged, the
+// table node of j + 1 and the key bytes of j + 2 are in flight, so a lane's
+// dependent key -> index -> node chain is paid once per lane, not per node
+// (the rolled loop of lane_tree issues each node's loads only after the
+// previous node's compressions)
+template <int D, class Prov>
+__device__ __forceinline__ void lane_tree_pf(const Prov& P, uint32_t (&h)[8]) {
+  constexpr int N = 1 << D;
+  uint32_t s[D > 0 ? D : 1][8];
+  uint32_t nx[8];
+  typename Prov::Raw k1 = P.raw(0);
+  P.node(k1, 0, nx);
+  if (N > 1) k1 = P.raw(1);
+  for (int j = 0; j < N; j++) {
+    uint32_t x[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) x[w] = nx[w];
+    if (j + 1 < N) P.node(k1, j + 1, nx);
+    if (j + 2 < N) k1 = P.raw(j + 2);
     bool done = false;
 #pragma unroll
     for (int l = 0; l < D; l++) {
@@ -1246,16 +1352,21 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __
   }
 }
 
-template <typename Key>
+template <bool PF, int D, class Prov>
+__device__ __forceinline__ void lane_tree_sel(const Prov& P, uint32_t (&h)[8]) {
+  if constexpr (PF) lane_tree_pf<D>(P, h);
+  else lane_tree<D>(P, h);
+}
+template <typename Key, bool PF>
 __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const uint32_t* tab,
                                           const ColTemplate* ct, uint32_t (&h)[8]) {
   // a lane covers 2^(6 + dict_extra(K)) rows: 2^(6+a-K) table nodes
   switch (P.K) {
-    case 0: lane_tree<6>(DictNodes<Key, 0>{p, tab, P.min, P.R}, h); break;
-    case 1: lane_tree<5>(DictNodes<Key, 1>{p, tab + 8 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 2: lane_tree<5>(DictNodes<Key, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 3: lane_tree<5>(DictNodes<Key, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 4: lane_tree<4>(DictNodes<Key, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 0: lane_tree_sel<PF, 6>(DictNodes<Key, 0>{p, tab, P.min, P.R}, h); break;
+    case 1: lane_tree_sel<PF, 5>(DictNodes<Key, 1>{p, tab + 8 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 2: lane_tree_sel<PF, 5>(DictNodes<Key, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 3: lane_tree_sel<PF, 5>(DictNodes<Key, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 4: lane_tree_sel<PF, 4>(DictNodes<Key, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
     default: lane_tree<6>(RawLeaves<Key>{p, ct}, h); break;
   }
 }
@@ -1263,6 +1374,7 @@ __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const
 // 64-lane WG = 4096 rows of one dictionary column (4 chunks): each lane folds
 // 64 rows to a level-6 node, 4 LDS levels give the 4 chunk roots, written as
 // leaves of the column's outer tree. Requires n >= 1024 (n % 64 == 0).
+template <bool PF>
 __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                         const DictCol* __restrict__ dcols,
                                                         const DictPlan* __restrict__ plans,
@@ -1302,17 +1414,17 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
   if (lrow < row_end) {
     uint32_t h[8];
     switch (ct.kind) {
-      case 0: case 3: dict_lane<int8_t>(dict_keys<int8_t>(T, ct) + lrow, P, tab, ctp, h); break;
-      case 4: dict_lane<uint8_t>(dict_keys<uint8_t>(T, ct) + lrow, P, tab, ctp, h); break;
-      case 5: dict_lane<uint16_t>(dict_keys<uint16_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      case 0: case 3: dict_lane<int8_t, PF>(dict_keys<int8_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      case 4: dict_lane<uint8_t, PF>(dict_keys<uint8_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      case 5: dict_lane<uint16_t, PF>(dict_keys<uint16_t>(T, ct) + lrow, P, tab, ctp, h); break;
       default:
         if (P.delta) {
           const uint64_t o = (uint64_t)ct.tape * T.n + lrow;
-          lane_tree<5>(DeltaNodes{T.head + o, T.mv + o, T.row_flags + lrow, tab + 8 * (uint64_t)DICT_CAP,
+          lane_tree_sel<PF, 5>(DeltaNodes{T.head + o, T.mv + o, T.row_flags + lrow, tab + 8 * (uint64_t)DICT_CAP,
                                   tab + 16 * (uint64_t)DICT_CAP, P.min, P.dmin, P.R, P.dR},
                        h);
         } else {
-          dict_lane<int64_t>(dict_keys<int64_t>(T, ct) + lrow, P, tab, ctp, h);
+          dict_lane<int64_t, PF>(dict_keys<int64_t>(T, ct) + lrow, P, tab, ctp, h);
         }
         break;
     }
@@ -1410,13 +1522,16 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
   // measured slower (round 3, single-proof k_col_commit_dict 335 -> 355 us,
   // tools/ab_dict_xcd.sh): off by default, SEZKP_DICT_XCD=1 for A/B
   static const bool xcd = getenv("SEZKP_DICT_XCD") && atoi(getenv("SEZKP_DICT_XCD")) != 0;
+  // SEZKP_DICT_PF=0: the rolled lane_tree without gather prefetch (A/B)
+  static const bool pf = !(getenv("SEZKP_DICT_PF") && atoi(getenv("SEZKP_DICT_PF")) == 0);
+  const auto kern = pf ? k_col_commit_dict<true> : k_col_commit_dict<false>;
   if (xcd && ndict > 8) {
     const uint64_t per_xcd = (uint64_t)((ndict + 7) / 8) * gx;  // work items of the busiest XCD
-    hipLaunchKernelGGL(k_col_commit_dict, dim3((unsigned)(8 * per_xcd)), dim3(64), 0, st, T, d_tmpl, d_dcols,
+    hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per_xcd)), dim3(64), 0, st, T, d_tmpl, d_dcols,
                        d_plans, d_dtabs, outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev,
                        (uint32_t)ndict, gx);
   } else {
-    hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
+    hipLaunchKernelGGL(kern, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
                        outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev, (uint32_t)ndict, 0u);
   }
   return hipGetLastError();
