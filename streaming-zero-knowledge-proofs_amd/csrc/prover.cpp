@@ -947,6 +947,13 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   using clk = std::chrono::steady_clock;
   const auto t_enter = clk::now();
   double t_sync = 0, t_last = 0;
+  // SEZKP_HOST_TRACE=1: host-side marks (us from entry) printed per proof, to
+  // split the Fiat-Shamir round trips into wake-up, host work and launch
+  static const bool htrace = getenv("SEZKP_HOST_TRACE") != nullptr;
+  std::vector<std::pair<const char*, double>> hmarks;
+  auto mark = [&](const char* what) {
+    if (htrace) hmarks.push_back({what, std::chrono::duration<double, std::micro>(clk::now() - t_enter).count()});
+  };
   auto sync = [&]() {
     const auto t0 = clk::now();
     if (sharded() && coll_issued) {
@@ -956,6 +963,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
         throw Err{SEZKP_E_DEVICE, std::string("rank ") + std::to_string(rank) + ": " + e.what()};
       }
     } else {
+      // (polling hipStreamQuery instead measured 10-20 us slower per proof)
       HIP_OR_THROW(hipStreamSynchronize(st));
     }
     t_last = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
@@ -1045,6 +1053,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   if (copy_roots) HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
   HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * ncols, sharded ? d_err + 8 : d_err, 4 * nguard, hipMemcpyDeviceToHost, st));
   sync();
+  mark("sync1");
   const uint32_t* colroots_h = copy_roots ? h_small : d_colroots;  // mapped: the kernels' own stores
   for (int r = 0; r < nguard; r++)
     if (h_small[8 * ncols + r])
@@ -1062,6 +1071,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   tr.absorb_u64("n_cols", (uint64_t)ncols);
   for (int c = 0; c < ncols; c++) tr.absorb("col_root", colroots.data() + 32 * c, 32);
   // alphas (params.rs:82-92) with the reuse of prover.rs:86-98
+  mark("tr_roots");
   auto ab = tr.challenge("alphas", 64);
   uint64_t a[8];
   for (int i = 0; i < 8; i++) a[i] = rd64(ab.data() + 8 * i) % GL_P_HOST;
@@ -1083,10 +1093,12 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   }
 
   // ---- composition (this rank's rows), DEEP quotient, INTT
+  mark("z_done");
   ok(launch_compose(st, T, A, mask, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
   // single device: DEEP as the LDE of H = q + c S (DeepPoly); the base
   // evaluations become q(w^j) before the INTT. Not when z^n = 1 (z on the
   // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
+  mark("compose_issued");
   const uint64_t zn = hgl_pow(z, n);
   const bool dq = logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY");
   // sharded: each rank turns its own rows into q(w^j) (the partial sums of
@@ -1190,6 +1202,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   rec(ST_L0UP + 1);
   if (copy_roots) HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
   sync();
+  mark("sync2");
   const uint32_t* roots_h = copy_roots ? h_small : d_roots;
   std::vector<uint8_t> roots((size_t)(k + 1) * 32);
   memcpy(roots.data(), roots_h, 32);
@@ -1222,6 +1235,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   };
   static const int fold_max = getenv("SEZKP_FOLD_MAX") ? std::max(2, std::min(FOLD_MAX, atoi(getenv("SEZKP_FOLD_MAX"))))
                                                       : FOLD_MAX;
+  mark("folds");
   for (int r = 0; r < rR;) {  // fold chain, up to fold_max layers per pass
     const int F = std::min(fold_max, rR - r);
     if (F >= 2) {
@@ -1276,16 +1290,19 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   rec(ST_FRI + 1);
   if (copy_roots) HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
   sync();
+  mark("sync3");
   memcpy(roots.data(), roots_h, (size_t)(k + 1) * 32);
   for (int r = 1; r <= k; r++) tr.absorb("fri_layer_root", roots.data() + 32 * r, 32);
 
   // ---- queries (prover.rs:248, 297)
+  mark("tr_fri");
   auto qb = tr.challenge("row_queries", 8 * NUM_QUERIES);
   uint64_t rows[NUM_QUERIES], frows[NUM_QUERIES];
   for (int i = 0; i < NUM_QUERIES; i++) rows[i] = rd64(qb.data() + 8 * i) % n;
   auto fb = tr.challenge("row_queries", 8 * NUM_QUERIES);
   for (int i = 0; i < NUM_QUERIES; i++) frows[i] = rd64(fb.data() + 8 * i) % N;
 
+  mark("queries");
   // FRI path requests (layer, index, ordinal) for the records this rank owns:
   // run layers by run owner, replicated layers on rank 0
   std::vector<uint64_t> pos((size_t)NUM_QUERIES * (k + 1));
@@ -1343,30 +1360,42 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     push_open(2, row);  // is_last
     push_open(0, row);  // input_mv
   }
+  mark("req_copy");
   HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (3 * max_fri_req + OPEN_REQ_WORDS * no) * 4, hipMemcpyHostToDevice, st));
   if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
   // openings first: their section of the proof (~70% of it) goes back over
   // PCIe on the side stream while the FRI path kernel runs
+  mark("col_open");
   ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, d_req + 3 * max_fri_req, (int)no, PL, d_tabs,
                      d_dlev, d_dplans, d_dtabs, d_dcols),
      "col_open");
   rec(ST_OPEN + 1);
+  mark("col_open_issued");
   if (!sharded) {
     HIP_OR_THROW(hipEventRecord(ev_fold, st));
     HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
     HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.fr_off, hipMemcpyDeviceToHost, st2));
     HIP_OR_THROW(hipEventRecord(ev_tail, st2));
   }
+  mark("open_d2h_issued");
   ok(launch_fri_paths(st, d_layers, d_req, (int)nf, PL), "fri_paths");
+  mark("fri_paths_issued");
   if (sharded)
     coll("proof_allreduce", 2 * P1 * PL.total / (uint64_t)world, [&] { comm->allreduce_sum_u8(PL.base, PL.total, st); });
   rec(ST_PATHS + 1);
   const uint64_t d2h_from = sharded ? 0 : PL.fr_off;
   HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes + d2h_from, (const uint8_t*)PL.base + d2h_from,
                               PL.total - d2h_from, hipMemcpyDeviceToHost, st));
+  mark("proof_d2h_issued");
   HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), lvals[k], 8, hipMemcpyDeviceToHost, st));
   if (!sharded) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
+  mark("issued");
   sync();
+  mark("sync4");
+  if (htrace) {
+    for (auto& m : hmarks) fprintf(stderr, "%s %.1f ", m.first, m.second);
+    fprintf(stderr, "\n");
+  }
   for (int s = 0; s < ST_NSTAGE; s++) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, ev[s], ev[s + 1]) == hipSuccess) stage_ms[s] = ms;
