@@ -333,6 +333,14 @@ def high_entropy_blocks(T: int, b: int, tau: int, seed: int):
     return partition(im, mv, hw, ws, b)
 
 
+# SEZKP_BENCH_HOST_COMM=1: rehearse the N > 1 paths on ONE GPU (every rank on
+# device 0, gloo instead of RCCL, the sharded contexts' exchanges staged
+# through host memory): the code paths of `--gpus N`, not its numbers
+REHEARSE = os.environ.get("SEZKP_BENCH_HOST_COMM") == "1"
+RED_DEV = "cpu" if REHEARSE else "cuda"  # device of the timing reductions
+COMM = "host" if REHEARSE else "rccl"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -375,15 +383,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(0 if REHEARSE else local)
+        dist.init_process_group("gloo" if REHEARSE else "nccl")
     else:
         torch.cuda.set_device(0)
 
     from sezkp_amd import ProverContext, reference_blocks
     T = 1 << args.log_t
     N = 8 * T
-    dev = local if world > 1 else 0
+    dev = local if world > 1 and not REHEARSE else 0
     K = max(1, args.inflight)
     # trace pool: context i cycles through traces i, i+K, ...; each is exactly
     # what `sezkp-cli simulate` writes at its seed (42 = the reference's own),
@@ -431,7 +439,7 @@ def main():
         cpu = (time.process_time() - c0) / (ts[-1] - ts[0] + 1e-9)
         gc.enable()
         if dist:
-            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            t = torch.tensor([dt], dtype=torch.float64, device=RED_DEV)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         return dt, halves(ts[w:], t_start), cpu
@@ -548,7 +556,9 @@ def main():
                        "value_is": headline, "upload_bytes_per_proof": upload_bytes,
                        "T": T, "N": N, "tau": args.tau, "b": args.b, "proof_bytes": proof_len,
                        "proofs_in_flight_per_gpu": K, "distinct_traces": n_tr,
-                       "parallelism": f"replicas x{world}, {K} independent proofs in flight per GPU"},
+                       "parallelism": f"replicas x{world}, {K} independent proofs in flight per GPU"
+                                      + (" (REHEARSAL: every rank on GPU 0, gloo + host-staged exchanges; not a "
+                                         "multi-GPU measurement)" if REHEARSE and world > 1 else "")},
             "halves_ms_per_proof": halves_, "host_cpu_per_wall": cpu_frac,
             "timing": "one continuous pipeline: warmup proofs run straight into the timed ones; the window runs "
                       "from the last warmup proof's completion to the last proof's completion (steps x inflight "
@@ -624,10 +634,10 @@ def main():
         guarded("configs", lambda: measure_configs(args, torch))
     if args.dntt_log_n:
         # BASELINE config 4 (at N = 8): 2^26-point four-step NTT over all ranks
-        guarded("dist_ntt", lambda: measure_dist_ntt(args, world, rank, local, dist, torch))
+        guarded("dist_ntt", lambda: measure_dist_ntt(args, world, rank, dev, dist, torch))
     if world > 1 and not args.no_sharded:
         # ONE T = 2^21 proof over all ranks (strong scaling)
-        guarded("sharded", lambda: measure_sharded(args, world, rank, local, dist, torch))
+        guarded("sharded", lambda: measure_sharded(args, world, rank, dev, dist, torch))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
@@ -875,7 +885,7 @@ def measure_dist_ntt(args, world, rank, local, dist, torch):
     (strong scaling: fixed n), forward + inverse per step on the context
     stream; one RCCL all-to-all per transform. Round trip checked."""
     from sezkp_amd import ProverContext, ShardedProverContext
-    ctx = ShardedProverContext(rank, world, device=local, comm="rccl") if world > 1 else ProverContext(0)
+    ctx = ShardedProverContext(rank, world, device=local, comm=COMM) if world > 1 else ProverContext(0)
     log_n = args.dntt_log_n
     M = (1 << log_n) // world
     g = torch.Generator(device="cuda")
@@ -901,7 +911,7 @@ def measure_dist_ntt(args, world, rank, local, dist, torch):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=RED_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         oks = [None] * world
@@ -933,7 +943,7 @@ def measure_sharded(args, world, rank, local, dist, torch):
         c1.upload(blocks)
         single = hashlib.sha256(bytes(c1.prove_view(mroot))).hexdigest()
         c1.close()
-    ctx = ShardedProverContext(rank, world, device=local, comm="rccl")
+    ctx = ShardedProverContext(rank, world, device=local, comm=COMM)
     ctx.upload(blocks)
     del blocks
     ctx.prove(mroot)  # warmup
@@ -952,7 +962,7 @@ def measure_sharded(args, world, rank, local, dist, torch):
     dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    t = torch.tensor([dt], dtype=torch.float64, device=RED_DEV)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     digest = hashlib.sha256(view).hexdigest()
