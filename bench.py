@@ -921,7 +921,8 @@ def measure_dist_ntt(args, world, rank, local, dist, torch):
     n = 1 << log_n
     per = dt / (2 * args.dntt_steps)
     alg = 16 * M / per / 1e9  # read + write each local element once, per GPU
-    shape = (f"four-step: local 2^{log_n - (world.bit_length() - 1)} NTT, twiddle, 1 RCCL all-to-all, "
+    xchg = "1 host-staged (gloo) all-to-all, REHEARSAL on one GPU" if REHEARSE else "1 RCCL all-to-all"
+    shape = (f"four-step: local 2^{log_n - (world.bit_length() - 1)} NTT, twiddle, {xchg}, "
              f"{world}-point DFTs" if world > 1 else
              "one rank: natural-order local NTT (DIF passes with the transposed last pass), no exchange")
     return {"workload": f"2^{log_n}-point Goldilocks NTT over {world} GPU(s), forward + inverse ({shape})",
@@ -976,8 +977,9 @@ def measure_sharded(args, world, rank, local, dist, torch):
            "ms_per_proof": dt / args.sharded_steps * 1e3, "steps": args.sharded_steps, "scaling": "strong",
            "config": {"workload": f"ONE stark-v1 proof over {world} GPUs, T=2^{T.bit_length() - 1} rows "
                                   f"(N=2^{N.bit_length() - 1}), b={args.b}, tau={args.tau}, trace resident",
-                      "parallelism": f"sharded x{world}: coset-split LDE, 1 RCCL all-to-all, allgathered "
-                                     f"Merkle caps, byte-sum proof assembly"},
+                      "parallelism": f"sharded x{world}: coset-split LDE, 1 {'host-staged' if REHEARSE else 'RCCL'} "
+                                     f"all-to-all, allgathered Merkle caps, byte-sum proof assembly"
+                                     + (" (REHEARSAL: all ranks on GPU 0)" if REHEARSE else "")},
            "ranks_agree": len(set(ds)) == 1, "matches_single_gpu_proof": ds[0] == single, "proof_bytes": plen,
            "stages_ms_rank0": {k: v / args.sharded_steps for k, v in stage_sum.items()},
            "collectives_rank0": {k: {"bytes_sent": v["bytes"], "ms": v["ms"] / args.sharded_steps,
