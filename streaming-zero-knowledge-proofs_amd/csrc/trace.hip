@@ -44,6 +44,115 @@ __global__ void __launch_bounds__(TR_THREADS) k_trace_image(const int8_t* __rest
   }
 }
 
+// tau = 8 (the headline shape): a lane takes 8 consecutive steps, loads their
+// 64 + 64 + 128 raw bytes as 16-byte vectors, transposes the 8 x 8 byte /
+// u16 matrices in registers (three XOR-swap stages, 64-bit words) and stores
+// 8 bytes / 16 bytes per tape: the same image as k_trace_image with wide
+// coalesced accesses instead of byte loads and stores.
+__device__ __forceinline__ void swap_bits(uint64_t& a, uint64_t& b, int sh, uint64_t m) {
+  const uint64_t t = ((a >> sh) ^ b) & m;
+  a ^= t << sh;
+  b ^= t;
+}
+__device__ __forceinline__ void transpose8x8_u8(uint64_t (&r)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) swap_bits(r[i], r[i + 4], 32, 0x00000000FFFFFFFFull);
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if ((i & 2) == 0) swap_bits(r[i], r[i + 2], 16, 0x0000FFFF0000FFFFull);
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) swap_bits(r[i], r[i + 1], 8, 0x00FF00FF00FF00FFull);
+}
+// rows of 8 u16 as (lo = elements 0..3, hi = 4..7)
+__device__ __forceinline__ void transpose8x8_u16(uint64_t (&lo)[8], uint64_t (&hi)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t t = hi[i];
+    hi[i] = lo[i + 4];
+    lo[i + 4] = t;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if ((i & 2) == 0) {
+      swap_bits(lo[i], lo[i + 2], 32, 0x00000000FFFFFFFFull);
+      swap_bits(hi[i], hi[i + 2], 32, 0x00000000FFFFFFFFull);
+    }
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    swap_bits(lo[i], lo[i + 1], 16, 0x0000FFFF0000FFFFull);
+    swap_bits(hi[i], hi[i + 1], 16, 0x0000FFFF0000FFFFull);
+  }
+}
+// bytes -> 0 / 1 (any nonzero byte is a write)
+__device__ __forceinline__ uint64_t bytes_nonzero(uint64_t x) {
+  x |= x >> 4;
+  x |= x >> 2;
+  x |= x >> 1;
+  return x & 0x0101010101010101ull;
+}
+// 4 bytes of 0 / 1 (low half of b) -> 4 u16 masks of 0 / 0xFFFF
+__device__ __forceinline__ uint64_t spread_mask16(uint32_t b) {
+  const uint64_t s = (uint64_t)(b & 0xFF) | ((uint64_t)(b & 0xFF00) << 8) | ((uint64_t)(b & 0xFF0000) << 16) |
+                     ((uint64_t)(b & 0xFF000000u) << 24);
+  return (s << 16) - s;
+}
+__global__ void __launch_bounds__(TR_THREADS) k_trace_image8(const int8_t* __restrict__ raw_mv,
+                                                           const uint8_t* __restrict__ raw_hw,
+                                                           const uint16_t* __restrict__ raw_ws, uint64_t n,
+                                                           int8_t* __restrict__ mv, uint8_t* __restrict__ wf,
+                                                           uint16_t* __restrict__ ws) {
+  const uint64_t s0 = ((uint64_t)blockIdx.x * TR_THREADS + threadIdx.x) * 8;
+  if (s0 >= n) return;
+  if (s0 + 8 > n) {  // ragged tail: element by element
+    for (uint64_t s = s0; s < n; s++)
+      for (int r = 0; r < 8; r++) {
+        const bool w = raw_hw[s * 8 + r] != 0;
+        mv[(uint64_t)r * n + s] = raw_mv[s * 8 + r];
+        wf[(uint64_t)r * n + s] = w ? 1 : 0;
+        ws[(uint64_t)r * n + s] = w ? raw_ws[s * 8 + r] : 0;
+      }
+    return;
+  }
+  uint64_t m[8], h[8], wl[8], wh[8];
+  {
+    const uint4* pm = reinterpret_cast<const uint4*>(raw_mv + s0 * 8);
+    const uint4* ph = reinterpret_cast<const uint4*>(raw_hw + s0 * 8);
+    const uint4* pw = reinterpret_cast<const uint4*>(raw_ws + s0 * 8);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 a = pm[q], b = ph[q];
+      m[2 * q] = (uint64_t)a.x | ((uint64_t)a.y << 32);
+      m[2 * q + 1] = (uint64_t)a.z | ((uint64_t)a.w << 32);
+      h[2 * q] = (uint64_t)b.x | ((uint64_t)b.y << 32);
+      h[2 * q + 1] = (uint64_t)b.z | ((uint64_t)b.w << 32);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint4 c = pw[q];
+      wl[q] = (uint64_t)c.x | ((uint64_t)c.y << 32);
+      wh[q] = (uint64_t)c.z | ((uint64_t)c.w << 32);
+    }
+  }
+  // mask the symbols of steps that write nothing (row = step here)
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    h[i] = bytes_nonzero(h[i]);
+    wl[i] &= spread_mask16((uint32_t)h[i]);
+    wh[i] &= spread_mask16((uint32_t)(h[i] >> 32));
+  }
+  transpose8x8_u8(m);
+  transpose8x8_u8(h);
+  transpose8x8_u16(wl, wh);
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const uint64_t o = (uint64_t)r * n + s0;
+    *reinterpret_cast<uint64_t*>(mv + o) = m[r];
+    *reinterpret_cast<uint64_t*>(wf + o) = h[r];
+    *reinterpret_cast<uint4*>(ws + o) =
+        make_uint4((uint32_t)wl[r], (uint32_t)(wl[r] >> 32), (uint32_t)wh[r], (uint32_t)(wh[r] >> 32));
+  }
+}
+
 // ------------------------------------------------------------ expansion
 // One workgroup per block: row -> block id, first/last flags, and the
 // post-move head prefix sums per tape (head starts at 0 in every block).
@@ -1474,6 +1583,15 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
 hipError_t launch_trace_image(hipStream_t st, const int8_t* raw_mv, const uint8_t* raw_hw, const uint16_t* raw_ws,
                               uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws) {
   if (n == 0 || tau <= 0) return hipSuccess;
+  // SEZKP_TRACE_IMAGE_BYTES=1: the byte-wise kernel for tau = 8 too (A/B)
+  static const bool bytes = getenv("SEZKP_TRACE_IMAGE_BYTES") && atoi(getenv("SEZKP_TRACE_IMAGE_BYTES")) != 0;
+  if (tau == 8 && !bytes) {
+    const uint64_t g8 = ((n + 7) / 8 + TR_THREADS - 1) / TR_THREADS;
+    if (g8 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_trace_image8, dim3((unsigned)g8), dim3(TR_THREADS), 0, st, raw_mv, raw_hw, raw_ws, n, mv, wf,
+                       ws);
+    return hipGetLastError();
+  }
   const uint64_t g = (n + TR_THREADS - 1) / TR_THREADS;
   if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_trace_image, dim3((unsigned)g), dim3(TR_THREADS), 0, st, raw_mv, raw_hw, raw_ws, n, tau, mv,
