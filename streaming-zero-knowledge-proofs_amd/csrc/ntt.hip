@@ -677,10 +677,17 @@ __global__ void __launch_bounds__(NTT_THREADS, 4) k_ntt4(NttPassArgs P) {
 // (x[32 u + r]), then * w_512^(r k_lo); step 2, thread (c, q) for q < 16, a
 // 32-point DIF over r (w_32 = 2^78: shifts). Same row order, pass twiddle and
 // out-of-place store as k_ntt4's wide DIF pass.
+// LDS slot of (q, r, c): 16 u64 (32 banks) of padding after every q-block. A
+// q-block is 32 rows = 64 * NTT_PADC dwords, so without it the four q of a
+// step-2 wave hit the same 32 banks (a 2x serialised read).
+template <int F1>
+__device__ __forceinline__ int dif9_slot(int q, int r, int c) {
+  return (q * F1 + r) * NTT_PADC + c + (q << 4);
+}
 template <bool INV>
 __global__ void __launch_bounds__(512, 2) k_ntt_dif9(NttPassArgs P) {
   constexpr int M1 = 5, M2 = 4, F1 = 1 << M1, F2 = 1 << M2, m = M1 + M2, R = 1 << m, NT = 512;
-  __shared__ uint64_t sh[R * NTT_PADC];
+  __shared__ uint64_t sh[R * NTT_PADC + 16 * (1 << M2)];
   __shared__ uint64_t W[R];
   const int tid = threadIdx.x;
   const NttTables& T = P.tw;
@@ -706,7 +713,7 @@ __global__ void __launch_bounds__(512, 2) k_ntt_dif9(NttPassArgs P) {
 #pragma unroll
     for (int q = 0; q < F2; q++) {
       const int klo = rev<M2>(q);
-      sh[(q * F1 + r) * NTT_PADC + c] = klo && r ? gl_mul(x[q], W[r * klo]) : x[q];
+      sh[dif9_slot<F1>(q, r, c)] = klo && r ? gl_mul(x[q], W[r * klo]) : x[q];
     }
   }
   __syncthreads();
@@ -719,7 +726,7 @@ __global__ void __launch_bounds__(512, 2) k_ntt_dif9(NttPassArgs P) {
     uint64_t y[16];
 #pragma unroll
     for (int r = 0; r < 16; r++) {
-      const uint64_t a = sh[(q * F1 + r) * NTT_PADC + c], b = sh[(q * F1 + r + 16) * NTT_PADC + c];
+      const uint64_t a = sh[dif9_slot<F1>(q, r, c)], b = sh[dif9_slot<F1>(q, r + 16, c)];
       if (h == 0) {
         y[r] = gl_add(a, b);
       } else {
