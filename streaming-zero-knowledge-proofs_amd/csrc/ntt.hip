@@ -395,10 +395,14 @@ __device__ __forceinline__ void lds_to_transposed(const uint64_t* sh, const NttP
   const int lo = P.nat_logN - m;
 #pragma unroll
   for (int j = 0; j < NTT_CMAX * R / NTT_THREADS; j++) {
-    const int e = j * NTT_THREADS + threadIdx.x, i = e & (NTT_CMAX - 1), k = e >> 4;
-    uint64_t v = sh[(__brev((uint32_t)k) >> (32 - m)) * NTT_PADC + i];
+    // lanes walk consecutive LDS rows (conflict-free reads; consecutive k =
+    // rows R/4 apart put a wave's four k on the same banks); each k's 16
+    // outputs stay one 128-B segment
+    const int e = j * NTT_THREADS + threadIdx.x, i = e & (NTT_CMAX - 1), row = e >> 4;
+    const uint64_t k = __brev((uint32_t)row) >> (32 - m);
+    uint64_t v = sh[row * NTT_PADC + i];
     if (P.out_scale != 1) v = gl_mul(v, P.out_scale);
-    P.out[((uint64_t)k << lo) + tile * NTT_CMAX + i] = v;
+    P.out[(k << lo) + tile * NTT_CMAX + i] = v;
   }
 }
 
