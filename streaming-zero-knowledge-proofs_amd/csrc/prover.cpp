@@ -537,7 +537,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   T.blk_offout = t0.bo;
   T.row_blk = dalloc<uint32_t>(n);
   T.row_flags = dalloc<uint8_t>(n);
-  T.head = dalloc<int64_t>((size_t)tau * n + 1);
+  T.head = dalloc<int32_t>((size_t)tau * n + 2);
   T.head_rng = dalloc<int64_t>(2 * (size_t)tau * nblk + 2);
 
   // ---- column templates + outer trees (all levels kept)

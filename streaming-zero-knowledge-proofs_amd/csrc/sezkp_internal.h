@@ -137,7 +137,7 @@ struct TraceDev {
   const uint64_t* blk_offout; // [tau][nblk]
   uint32_t* row_blk;          // [n]   (derived)
   uint8_t* row_flags;         // [n]   bit0 first, bit1 last (derived)
-  int64_t* head;              // [tau][n] post-move head (derived)
+  int32_t* head;              // [tau][n] post-move head (derived; block-local, |head| <= block length < 2^29)
   int64_t* head_rng;          // [tau][nblk][2] per-block min / max of head (derived by k_expand)
 };
 

@@ -170,10 +170,10 @@ __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) 
   // head_rng, so the dictionary plan need not re-read the head columns.
   for (int tp = wave; tp < T.tau; tp += TR_THREADS / 64) {
     const int8_t* mv = T.mv + (uint64_t)tp * T.n;
-    int64_t* hd = T.head + (uint64_t)tp * T.n;
+    int32_t* hd = T.head + (uint64_t)tp * T.n;
     int64_t carry = 0, lo = INT64_MAX, hi = INT64_MIN;
     // even block start (n is even): a lane's row pair is one 2-byte load and
-    // one 16-byte store
+    // one 8-byte store
     const bool paired = (s & 1) == 0;
     for (uint64_t r0 = s; r0 < e; r0 += 128) {
       const uint64_t r = r0 + 2 * (uint64_t)lane;
@@ -202,10 +202,10 @@ __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) 
         hi = max(hi, h1);
       }
       if (paired && r + 1 < e) {
-        *reinterpret_cast<longlong2*>(hd + r) = make_longlong2(h1 - m1, h1);
+        *reinterpret_cast<int2*>(hd + r) = make_int2((int32_t)(h1 - m1), (int32_t)h1);
       } else {
-        if (r < e) hd[r] = h1 - m1;
-        if (r + 1 < e) hd[r + 1] = h1;
+        if (r < e) hd[r] = (int32_t)(h1 - m1);
+        if (r + 1 < e) hd[r + 1] = (int32_t)h1;
       }
       carry += __shfl(x, 63, 64);
     }
@@ -274,9 +274,8 @@ __device__ __forceinline__ void col_values4(const TraceDev& T, const ColTemplate
       return;
     }
     case 6: {
-      const longlong2* p = reinterpret_cast<const longlong2*>(T.head + o);
-      longlong2 a = p[0], b = p[1];
-      v[0] = gl_from_i64(a.x); v[1] = gl_from_i64(a.y); v[2] = gl_from_i64(b.x); v[3] = gl_from_i64(b.y);
+      const int4 a = *reinterpret_cast<const int4*>(T.head + o);
+      v[0] = gl_from_i64(a.x); v[1] = gl_from_i64(a.y); v[2] = gl_from_i64(a.z); v[3] = gl_from_i64(a.w);
       return;
     }
     default: {
@@ -687,7 +686,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, Alphas 
     int64_t head[RW + 1];
 #pragma unroll
     for (int j = 0; j < RW; j += 2) {
-      const longlong2 h2 = *reinterpret_cast<const longlong2*>(T.head + o + i + j);
+      const int2 h2 = *reinterpret_cast<const int2*>(T.head + o + i + j);
       head[j] = h2.x;
       head[j + 1] = h2.y;
     }
@@ -757,7 +756,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, Alphas 
 template <typename Key>
 __device__ __forceinline__ const Key* dict_keys(const TraceDev& T, const ColTemplate& ct) {
   const uint64_t o = (uint64_t)ct.tape * T.n;
-  if constexpr (sizeof(Key) == 8) return reinterpret_cast<const Key*>(T.head + o);
+  if constexpr (sizeof(Key) == 4) return reinterpret_cast<const Key*>(T.head + o);
   else if constexpr (sizeof(Key) == 2) return reinterpret_cast<const Key*>(T.wsym + o);
   else {
     if (ct.kind == 0) return reinterpret_cast<const Key*>(T.input_mv);
@@ -791,6 +790,7 @@ __device__ __forceinline__ void load_keys(const Key* __restrict__ p, int64_t (&k
         const int bit = i * 8 * (int)sizeof(Key);
         uint64_t raw;
         if constexpr (sizeof(Key) == 8) raw = (uint64_t)ww[bit / 32] | ((uint64_t)ww[bit / 32 + 1] << 32);
+        else if constexpr (sizeof(Key) == 4) raw = ww[bit / 32];
         else raw = (ww[bit / 32] >> (bit % 32)) & ((1u << (8 * sizeof(Key))) - 1u);
         k[q * PER + i] = (int64_t)(Key)raw;
       }
@@ -865,6 +865,8 @@ struct DictNodes {
       int64_t k;
       if constexpr (sizeof(Key) == 8) {
         k = (int64_t)((uint64_t)r.w[2 * i] | ((uint64_t)r.w[2 * i + 1] << 32));
+      } else if constexpr (sizeof(Key) == 4) {
+        k = (int64_t)(int32_t)r.w[i];
       } else {
         const int bit = i * 8 * (int)sizeof(Key);
         k = (int64_t)(Key)((r.w[bit / 32] >> (bit % 32)) & ((1u << (8 * sizeof(Key))) - 1u));
@@ -876,7 +878,7 @@ struct DictNodes {
 };
 // head delta plan: node j = the 4-row group at row 4j of the lane
 struct DeltaNodes {
-  const int64_t* hp;      // head, first row of the lane
+  const int32_t* hp;      // head, first row of the lane
   const int8_t* mp;       // mv of the same tape
   const uint8_t* fp;      // row_flags (bit 0 = block start)
   const uint32_t* t1;     // T_1
@@ -1078,7 +1080,7 @@ __device__ __forceinline__ void dict_node_at(const TraceDev& T, const ColTemplat
     case 0: case 3: SEZKP_DN(int8_t) break;
     case 4: SEZKP_DN(uint8_t) break;
     case 5: SEZKP_DN(uint16_t) break;
-    default: SEZKP_DN(int64_t) break;
+    default: SEZKP_DN(int32_t) break;
   }
 #undef SEZKP_DN
 }
@@ -1533,7 +1535,7 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
                                   tab + 16 * (uint64_t)DICT_CAP, P.min, P.dmin, P.R, P.dR},
                        h);
         } else {
-          dict_lane<int64_t, PF>(dict_keys<int64_t>(T, ct) + lrow, P, tab, ctp, h);
+          dict_lane<int32_t, PF>(dict_keys<int32_t>(T, ct) + lrow, P, tab, ctp, h);
         }
         break;
     }
