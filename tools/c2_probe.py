@@ -11,7 +11,13 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "streaming-zero-knowledge-proofs_amd"))
 import torch  # noqa: E402  (one HIP runtime: torch first)
 
-from sezkp_amd._lib import lib  # noqa: E402
+if os.environ.get("SEZKP_PROBE_LIB"):  # A/B: another build of the library (same C ABI)
+    import ctypes
+    lib = ctypes.CDLL(os.environ["SEZKP_PROBE_LIB"])
+    lib.sezkp_gl_ntt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]
+    lib.sezkp_gl_ntt.restype = ctypes.c_int32
+else:
+    from sezkp_amd._lib import lib  # noqa: E402
 
 
 def main():
