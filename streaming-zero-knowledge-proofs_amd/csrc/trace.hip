@@ -1341,9 +1341,15 @@ __device__ __forceinline__ void reduce_parts(const int64_t* pp, uint32_t nparts,
   __syncthreads();
 }
 
+// SEZKP_DICT_MISS_PEN=<q8> (A/B): gather-miss price of the table planner
+constexpr uint64_t DICT_PEN_ENTRIES = 32768;
+static uint32_t dict_miss_pen() {
+  static const uint32_t v = getenv("SEZKP_DICT_MISS_PEN") ? (uint32_t)atoi(getenv("SEZKP_DICT_MISS_PEN")) : 0;
+  return v;
+}
 __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restrict__ part, uint32_t nparts,
                                                           uint64_t n, const DictCol* __restrict__ dcols,
-                                                          DictPlan* __restrict__ plans) {
+                                                          DictPlan* __restrict__ plans, uint32_t pen_q8) {
   __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
   const int tid = threadIdx.x;
   int64_t lo, hi, mlo = 0, mhi = -1;
@@ -1361,7 +1367,9 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restr
     for (int k = 0; k < DICT_LEVELS && (1ULL << k) <= n && sz <= DICT_CAP; k++) {
       P.pw[k] = (uint32_t)sz;
       tabcost += sz;
-      const uint64_t cost = tabcost + (n >> k);
+      // pen_q8 / 256: extra cost of a gather from a table of > DICT_PEN_ENTRIES
+      // entries (1 MB: it misses the reading XCD's L2) relative to a hash
+      const uint64_t cost = tabcost + (((n >> k) * (256 + (sz > DICT_PEN_ENTRIES ? pen_q8 : 0))) >> 8);
       if (cost < best) { best = cost; P.K = k; }
       sz = sz * sz;
     }
@@ -1626,7 +1634,8 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
                      row0, row0 + nrows);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_dcols, d_plans);
+  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_dcols, d_plans,
+                     dict_miss_pen());
   if ((e = hipGetLastError()) != hipSuccess) return e;
   for (int l = 0; l < DICT_LEVELS; l++) {
     // one flat launch per level (and per DICT_FLAT_MAX columns): all WGs
