@@ -467,6 +467,16 @@ static void fail_point(int rank, const char* name) {
                                 std::to_string(rank)};
 }
 
+// The query requests (a few KB per proof) live in mapped host memory that the
+// path / opening kernels read directly, so no small H2D copy queues behind a
+// staged trace upload on the copy engine (round 3, tools/ab_req_mapped.sh:
+// host -> proof 7.91 -> 7.97e9 mean of three alternating runs, spread 2.5% ->
+// 0.3%). SEZKP_REQ_MAPPED=0: the H2D copy into device memory (A/B).
+static bool req_mapped() {
+  static const bool on = !(getenv("SEZKP_REQ_MAPPED") && atoi(getenv("SEZKP_REQ_MAPPED")) == 0);
+  return on;
+}
+
 void sezkp_ctx::upload(const sezkp_block_view& v) {
   HIP_OR_THROW(hipSetDevice(device));
   // a stage() may still be copying into / transposing a slot on the copy
@@ -763,8 +773,13 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   }
   max_fri_req = (size_t)NUM_QUERIES * 2 * k;
   max_open_req = (size_t)NUM_QUERIES * (3 + 9 * tau);
-  d_req = dalloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
-  h_req = halloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
+  if (req_mapped()) {  // the path / opening kernels read the requests over PCIe: no H2D copy
+    h_req = hmapped<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
+    d_req = h_req;
+  } else {
+    d_req = dalloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
+    h_req = halloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
+  }
   // ---- proof layout (proof.rs:80-98, bincode fixint LE)
   {
     BinWriter w;
@@ -1361,7 +1376,8 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     push_open(0, row);  // input_mv
   }
   mark("req_copy");
-  HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (3 * max_fri_req + OPEN_REQ_WORDS * no) * 4, hipMemcpyHostToDevice, st));
+  if (d_req != h_req)
+    HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (3 * max_fri_req + OPEN_REQ_WORDS * no) * 4, hipMemcpyHostToDevice, st));
   if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
   // openings first: their section of the proof (~70% of it) goes back over
   // PCIe on the side stream while the FRI path kernel runs
