@@ -1200,11 +1200,31 @@ static bool plan_passes_x16(int logN, bool dif, int* ms, int* np) {
   return false;
 }
 
+// A 2^21-point DIF (the prover's INTT at T = 2^21) as a 9-stage wide pass
+// (k_ntt_dif9) + the 12-stage X16 narrow pass: 2 HBM round trips instead of
+// 3 passes of 7 (round 3, tools/ab_intt_dif9.sh: intt stage 97 -> 91 us per
+// proof, in flight +0.7-1.1%). SEZKP_NTT_DIF9X16=0: the three passes (A/B).
+static bool dif9x16_enabled() {
+  static const bool on = !(getenv("SEZKP_NTT_DIF9X16") && atoi(getenv("SEZKP_NTT_DIF9X16")) == 0);
+  return on;
+}
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T) {
   if (logN == 0) return hipSuccess;
   int ms[8], np;
   const bool x16 = plan_passes_x16(logN, true, ms, &np);
   if (!x16) plan_passes(logN, 1, ms, &np);
+  if (logN == 21 && dif9x16_enabled() && !ntt4_disabled() && !narrow_disabled()) {
+    NttPassArgs P{};
+    P.a = a; P.tw = T; P.m = 9; P.sL = 12; P.inverse = inverse ? 1 : 0; P.logC = 4;
+    const unsigned tiles = (unsigned)((1ULL << logN) >> (9 + 4));
+    if (inverse) hipLaunchKernelGGL(k_ntt_dif9<true>, dim3(tiles), dim3(512), 0, st, P);
+    else hipLaunchKernelGGL(k_ntt_dif9<false>, dim3(tiles), dim3(512), 0, st, P);
+    P.m = 12; P.sL = 0;
+    const bool ok = inverse ? launch_ntt4<true, true>(st, P, (unsigned)((1ULL << logN) >> 12))
+                            : launch_ntt4<true, false>(st, P, (unsigned)((1ULL << logN) >> 12));
+    if (!ok) return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   int sL = logN;
   for (int i = 0; i < np; i++) {
     NttPassArgs P{};

@@ -863,8 +863,18 @@ void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t
       t.h_tab[nt + o] = v.off_in[i];
       t.h_tab[2 * nt + o] = v.off_out[i];
     }
+  // each array in copies of <= 4 MB, so a proof's D2H copy queued on the same
+  // copy engine waits for one chunk, not for the rest of a 67 MB upload
+  // (round 3, tools/ab_upload_chunk.sh: host -> proof 7.89 -> 7.94e9, within
+  // the run-to-run spread). SEZKP_UPLOAD_CHUNK_MB=<m>: m MB, 0 = one copy.
+  static const size_t chunk =
+      (getenv("SEZKP_UPLOAD_CHUNK_MB") ? (size_t)atol(getenv("SEZKP_UPLOAD_CHUNK_MB")) : (size_t)4) << 20;
   auto cp = [&](void* dst, const void* src, size_t bytes) {
-    if (bytes) HIP_OR_THROW(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    for (size_t o = 0; o < bytes;) {
+      const size_t b = chunk ? std::min(chunk, bytes - o) : bytes - o;
+      HIP_OR_THROW(hipMemcpyAsync((uint8_t*)dst + o, (const uint8_t*)src + o, b, hipMemcpyHostToDevice, s));
+      o += b;
+    }
   };
   uint16_t* raw_ws = reinterpret_cast<uint16_t*>(t.raw);
   int8_t* raw_mv = reinterpret_cast<int8_t*>(t.raw + 2 * cells);
