@@ -1364,16 +1364,25 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restr
   if (R <= DICT_CAP) {
     P.R = (uint32_t)R;
     uint64_t best = 2 * n, tabcost = 0, sz = R;  // K = -1: n leaves + n parents
-    for (int k = 0; k < DICT_LEVELS && (1ULL << k) <= n && sz <= DICT_CAP; k++) {
-      P.pw[k] = (uint32_t)sz;
-      tabcost += sz;
-      // pen_q8 / 256: extra cost of a gather from a table of > DICT_PEN_ENTRIES
-      // entries (1 MB: it misses the reading XCD's L2) relative to a hash
-      const uint64_t cost = tabcost + (((n >> k) * (256 + (sz > DICT_PEN_ENTRIES ? pen_q8 : 0))) >> 8);
-      if (cost < best) { best = cost; P.K = k; }
-      sz = sz * sz;
+    bool open = true;
+    // unrolled: constant pw[] indices keep P in registers (a runtime index put
+    // it in scratch memory, and the kernel took ~23 us for 33 tiny workgroups)
+#pragma unroll
+    for (int k = 0; k < DICT_LEVELS; k++) {
+      open = open && (1ULL << k) <= n && sz <= DICT_CAP;
+      if (open) {
+        P.pw[k] = (uint32_t)sz;
+        tabcost += sz;
+        // pen_q8 / 256: extra cost of a gather from a table of > DICT_PEN_ENTRIES
+        // entries (1 MB: it misses the reading XCD's L2) relative to a hash
+        const uint64_t cost = tabcost + (((n >> k) * (256 + (sz > DICT_PEN_ENTRIES ? pen_q8 : 0))) >> 8);
+        if (cost < best) { best = cost; P.K = k; }
+        sz = sz * sz;
+      }
     }
-    for (int k = P.K + 1; k < DICT_LEVELS; k++) P.pw[k] = 0;
+#pragma unroll
+    for (int k = 0; k < DICT_LEVELS; k++)
+      if (k > P.K) P.pw[k] = 0;
     // head delta plan (see DictPlan): 4-row groups from (head, 3 moves)
     const uint64_t dR = mhi >= mlo ? (uint64_t)mhi - (uint64_t)mlo + 1 : 0;
     if (mvc != NO_DICT && P.K <= 1 && n >= 4 && dR && R * R <= DICT_CAP && dR <= 256 &&
