@@ -817,12 +817,12 @@ def measure_configs(args, torch):
         g.manual_seed(5)
         x = torch.randint(0, 0xFFFFFFFF00000001 >> 1, (m,), dtype=torch.int64, device="cuda", generator=g)
         d, s = x.clone(), torch.empty_like(x)
-        for _ in range(3):
+        for _ in range(10 if lg < 26 else 5):
             lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, 1, None)
             lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, -1, None)
         torch.cuda.synchronize()
         ok = bool(torch.equal(d, x))
-        reps = 20
+        reps = 50 if lg < 26 else 20
         e0.record()
         for _ in range(reps):
             lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, 1, None)

@@ -467,6 +467,15 @@ static void fail_point(int rank, const char* name) {
                                 std::to_string(rank)};
 }
 
+// SEZKP_SIDE_AT=0|1|2 (A/B): where the side-stream columns (tables, dense,
+// piecewise) start: 0 right after expand, beside the whole dictionary chain;
+// 1 after the dictionary plan; 2 after the table levels, beside the commit
+// kernel only (measured: the commit kernel then starves k_col_tables,
+// 37 -> 337 us, and the stage is 35 us longer)
+static int side_at() {
+  static const int v = getenv("SEZKP_SIDE_AT") ? atoi(getenv("SEZKP_SIDE_AT")) : 0;
+  return v;
+}
 // The query requests (a few KB per proof) live in mapped host memory that the
 // path / opening kernels read directly, so no small H2D copy queues behind a
 // staged trace upload on the copy engine (round 3, tools/ab_req_mapped.sh:
@@ -1039,16 +1048,28 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   const uint64_t row_hi = n >= 1024 ? ch_hi << COL_CHUNK_LOG2 : n;
   // piecewise / table / dense columns on the side stream, concurrent with the
   // (VALU-bound) dictionary columns; disjoint outer-tree leaves
-  HIP_OR_THROW(hipEventRecord(ev_expand, st));
-  HIP_OR_THROW(hipStreamWaitEvent(st2, ev_expand, 0));
-  ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
-  ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
-  ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
-                          outer_stride, d_err), "col_commit_pw");
-  HIP_OR_THROW(hipEventRecord(ev_cols, st2));
-  ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
-                        row_hi - row_lo, d_dlev),
-     "col_commit_dict");
+  auto side_columns = [&](hipEvent_t after) {
+    HIP_OR_THROW(hipStreamWaitEvent(st2, after, 0));
+    ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
+    ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
+    ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
+                            outer_stride, d_err), "col_commit_pw");
+    HIP_OR_THROW(hipEventRecord(ev_cols, st2));
+  };
+  if (side_at() > 0) {
+    // the latency-bound head of the dictionary chain (ranges, plan; with 2 the
+    // table levels too) alone on the chip, the side-stream columns after it
+    ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
+                          row_hi - row_lo, d_dlev, ev_expand, side_at()),
+       "col_commit_dict");
+    side_columns(ev_expand);
+  } else {
+    HIP_OR_THROW(hipEventRecord(ev_expand, st));
+    side_columns(ev_expand);
+    ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
+                          row_hi - row_lo, d_dlev),
+       "col_commit_dict");
+  }
   HIP_OR_THROW(hipStreamWaitEvent(st, ev_cols, 0));
   if (sharded) {
     const size_t bytes = (size_t)(ch_hi - ch_lo) * 32;

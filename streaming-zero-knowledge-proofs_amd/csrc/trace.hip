@@ -1634,8 +1634,14 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
 }
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev) {
-  if (ndict == 0) return hipSuccess;
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev,
+                              hipEvent_t ev_side, int side_at) {
+  // ev_side (optional) is recorded after the plan (side_at = 1) or after the
+  // table levels (side_at = 2): the caller starts its side-stream work there
+  if (ndict == 0) {
+    if (ev_side) return hipEventRecord(ev_side, st);
+    return hipSuccess;
+  }
   if (T.n < (1ULL << COL_CHUNK_LOG2)) return hipErrorInvalidValue;
   if (row0 + nrows > T.n || (nrows != T.n && (row0 % DICT_WG_ROWS || nrows % DICT_WG_ROWS))) return hipErrorInvalidValue;
   const uint32_t nparts = (uint32_t)((nrows + DICT_RANGE_ROWS - 1) / DICT_RANGE_ROWS);
@@ -1646,6 +1652,7 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
   hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_dcols, d_plans,
                      dict_miss_pen());
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (ev_side && side_at == 1 && (e = hipEventRecord(ev_side, st)) != hipSuccess) return e;
   for (int l = 0; l < DICT_LEVELS; l++) {
     // one flat launch per level (and per DICT_FLAT_MAX columns): all WGs
     // share every column's entries
@@ -1656,6 +1663,7 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
   }
+  if (ev_side && side_at == 2 && (e = hipEventRecord(ev_side, st)) != hipSuccess) return e;
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
   // measured slower (round 3, single-proof k_col_commit_dict 335 -> 355 us,
   // tools/ab_dict_xcd.sh): off by default, SEZKP_DICT_XCD=1 for A/B
