@@ -514,14 +514,17 @@ __device__ __forceinline__ void fri_tail_wg(const TailArgs& A, int j, uint64_t* 
 // produced by the fold chain first): the per-layer trees are independent, so
 // the small layers no longer serialize behind each other's latency. The first
 // `ntail` workgroups build the layers of <= 2048 leaves (fri_tail_wg).
+// A launch may cover a sub-range of the layers: `layers` then points at its
+// first one and wg_base is that layer's wg_start (wg_start values are global).
 __global__ void __launch_bounds__(MK_THREADS) k_forest16(const ForestLayer* __restrict__ layers, int nlayers,
-                                                         TailArgs A, int ntail, uint64_t* __restrict__ tailbuf) {
+                                                         TailArgs A, int ntail, uint64_t* __restrict__ tailbuf,
+                                                         uint32_t wg_base) {
   __shared__ uint32_t lds[8][MK_THREADS];
   if ((int)blockIdx.x < ntail) {
     fri_tail_wg(A, (int)blockIdx.x, tailbuf, lds);
     return;
   }
-  const uint32_t b = blockIdx.x - (uint32_t)ntail;
+  const uint32_t b = blockIdx.x - (uint32_t)ntail + wg_base;
   int l = 0;
   while (l + 1 < nlayers && layers[l + 1].wg_start <= b) l++;
   const ForestLayer F = layers[l];
@@ -729,13 +732,13 @@ hipError_t launch_foldm(hipStream_t st, const uint64_t* in, const FoldOuts& outs
 }
 
 hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs,
-                           const TailArgs* tail, uint64_t* tailbuf) {
+                           const TailArgs* tail, uint64_t* tailbuf, uint32_t wg_base) {
   if (nlayers <= 0) return tail ? hipErrorInvalidValue : hipSuccess;
   if (tail && (tail->Ls < 0 || tail->Ls >= TAIL_MAX || !tailbuf)) return hipErrorInvalidValue;
   const int ntail = tail ? tail->Ls + 1 : 0;
   const TailArgs none{};
   hipLaunchKernelGGL(k_forest16, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
-                     tail ? *tail : none, ntail, tailbuf);
+                     tail ? *tail : none, ntail, tailbuf, wg_base);
   return hipGetLastError();
 }
 

@@ -262,6 +262,7 @@ struct sezkp_ctx {
   ForestLayer* d_forest = nullptr;
   uint64_t* d_tailbuf = nullptr;   // single device: fold-replay scratch of the small-layer workgroups
   int n_forest = 0;
+  std::vector<uint32_t> forest_wg_start;  // host copy of d_forest[i].wg_start
   uint32_t forest_wgs = 0;
   UpperJob* d_jobs = nullptr;  // upper-level passes: layer 0, then all fold layers
   std::vector<std::pair<size_t, int>> jobs0, jobsF;
@@ -467,6 +468,15 @@ static void fail_point(int rank, const char* name) {
                                 std::to_string(rank)};
 }
 
+// SEZKP_FOREST_EARLY=1 (A/B): the FRI forest's first-fold-pass layers
+// hashed on the side stream beside the later fold passes instead of one
+// forest launch after the whole chain (measured round 3, tools/
+// ab_forest_early.sh: fri_fold_trees 0.709 -> 0.725 ms, the forest's
+// workgroups starve the later folds; off)
+static bool forest_early() {
+  static const bool on = getenv("SEZKP_FOREST_EARLY") && atoi(getenv("SEZKP_FOREST_EARLY")) != 0;
+  return on;
+}
 // SEZKP_SIDE_AT=0|1|2 (A/B): where the side-stream columns (tables, dense,
 // piecewise) start: 0 right after expand, beside the whole dictionary chain;
 // 1 after the dictionary plan; 2 after the table levels, beside the commit
@@ -756,6 +766,8 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     }
     n_forest = (int)fl.size();
     forest_wgs = wgs;
+    forest_wg_start.clear();
+    for (auto& f : fl) forest_wg_start.push_back(f.wg_start);
     d_forest = dalloc<ForestLayer>(fl.size() + 1);
     if (!fl.empty()) up(d_forest, fl.data(), fl.size());
     d_tailbuf = sharded() ? nullptr : dalloc<uint64_t>((size_t)TAIL_MAX << TAIL_MAX);
@@ -1282,6 +1294,12 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   static const int fold_max = getenv("SEZKP_FOLD_MAX") ? std::max(2, std::min(FOLD_MAX, atoi(getenv("SEZKP_FOLD_MAX"))))
                                                       : FOLD_MAX;
   mark("folds");
+  static const bool tail_separate = getenv("SEZKP_TAIL_SEPARATE") != nullptr;
+  const bool tail_merged = !sharded && tail_first <= k && n_forest > 0 && d_tailbuf && !tail_separate;
+  // SEZKP_FOREST_EARLY=1: the layers of the first fold pass (15/16 of the
+  // forest's work) are hashed on the side stream as soon as that pass is
+  // done, beside the later fold passes; the rest (and the tail) follows them
+  int forest_split = 0;  // layers 1..forest_split go to the early launch
   for (int r = 0; r < rR;) {  // fold chain, up to fold_max layers per pass
     const int F = std::min(fold_max, rR - r);
     if (F >= 2) {
@@ -1296,15 +1314,23 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
       ok(launch_fold(st, lvals[r], lvals[r + 1], ltrees[r + 1].logLen, beta_of(r)), "fri_fold");
       r += 1;
     }
+    if (forest_split == 0 && r < rR && tail_merged && forest_early()) {
+      forest_split = r;
+      HIP_OR_THROW(hipEventRecord(ev_fold, st));
+      HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+      ok(launch_forest16(st2, d_forest, r, forest_wg_start[r], nullptr, nullptr, 0), "fri_forest_early");
+      HIP_OR_THROW(hipEventRecord(ev_tail, st2));
+    }
   }
   const uint64_t* rep_src = rR >= 0 ? lvals[rR] : d_lde;  // full values of the layer above the replicated ones
   // single device: the small layers ride in the forest launch's first
   // workgroups (SEZKP_TAIL_SEPARATE=1: their own kernel on the side stream)
-  static const bool tail_separate = getenv("SEZKP_TAIL_SEPARATE") != nullptr;
-  const bool tail_merged = !sharded && tail_first <= k && n_forest > 0 && d_tailbuf && !tail_separate;
   if (tail_merged) {
     const TailArgs ta = tail_args(rep_src);
-    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf), "fri_forest");
+    const uint32_t base = forest_split ? forest_wg_start[forest_split] : 0;
+    ok(launch_forest16(st, d_forest + forest_split, n_forest - forest_split, forest_wgs - base, &ta, d_tailbuf, base),
+       "fri_forest");
+    if (forest_split) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
   } else {
     if (!sharded) launch_tail(rep_src);
     ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");

@@ -333,7 +333,7 @@ hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a);
 // the forest of layer trees >= 4096 leaves; tail != null: its first workgroups
 // also build the small layers (fri_tail_wg), tailbuf = TAIL_MAX x 4096 u64 scratch
 hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs,
-                           const TailArgs* tail = nullptr, uint64_t* tailbuf = nullptr);
+                           const TailArgs* tail = nullptr, uint64_t* tailbuf = nullptr, uint32_t wg_base = 0);
 // requests: (layer, index, ordinal in the proof's FRI records) triples
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
                             const ProofLayout& P);
