@@ -477,6 +477,13 @@ static bool forest_early() {
   static const bool on = getenv("SEZKP_FOREST_EARLY") && atoi(getenv("SEZKP_FOREST_EARLY")) != 0;
   return on;
 }
+// SEZKP_TABLES_EARLY=1 (A/B): k_col_tables beside expand (measured round 3,
+// tools/ab_tables_early.sh: expand 37.7 -> 54.1 us, expand + col_commit
+// 0.481 -> 0.511 ms; off)
+static bool tables_early_on() {
+  static const bool on = getenv("SEZKP_TABLES_EARLY") && atoi(getenv("SEZKP_TABLES_EARLY")) != 0;
+  return on;
+}
 // SEZKP_SIDE_AT=0|1|2 (A/B): where the side-stream columns (tables, dense,
 // piecewise) start: 0 right after expand, beside the whole dictionary chain;
 // 1 after the dictionary plan; 2 after the table levels, beside the commit
@@ -1054,6 +1061,15 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   rec(0);
   // ---- column commitments (openings.rs:306-398): this rank's chunks, then
   // every rank gathers all chunk roots and builds the outer trees
+  // SEZKP_TABLES_EARLY=1: the piecewise columns' U tables (they need only
+  // the block tables) on the side stream beside expand instead of beside the
+  // dictionary chain's head
+  const bool tables_early = tables_early_on() && side_at() == 0;
+  if (tables_early) {
+    HIP_OR_THROW(hipEventRecord(ev_fold, st));
+    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+    ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
+  }
   ok(launch_expand(st, T, blk_lo, blk_cnt), "expand");
   rec(1);
   const uint64_t row_lo = n >= 1024 ? ch_lo << COL_CHUNK_LOG2 : 0;
@@ -1062,7 +1078,8 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   // (VALU-bound) dictionary columns; disjoint outer-tree leaves
   auto side_columns = [&](hipEvent_t after) {
     HIP_OR_THROW(hipStreamWaitEvent(st2, after, 0));
-    ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
+    if (!tables_early)
+      ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
     ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
     ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
                             outer_stride, d_err), "col_commit_pw");
