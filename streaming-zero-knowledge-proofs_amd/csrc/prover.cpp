@@ -1568,8 +1568,22 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     for (auto& e : c->ev) HIP_OR_THROW(hipEventCreate(&e));
     // SEZKP_ONE_STREAM=1: the side-stream work runs on the main stream (one
     // hardware queue per context when many contexts share the GPU)
-    if (getenv("SEZKP_ONE_STREAM")) c->st2 = c->st;
-    else HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+    // SEZKP_SIDE_CU_EVERY=<k> (A/B): the side stream may use only every k-th
+    // CU (hipExtStreamCreateWithCUMask), so its latency-bound kernels cannot
+    // take the whole chip from the main stream's chain
+    const int cu_every = getenv("SEZKP_SIDE_CU_EVERY") ? atoi(getenv("SEZKP_SIDE_CU_EVERY")) : 0;
+    if (getenv("SEZKP_ONE_STREAM")) {
+      c->st2 = c->st;
+    } else if (cu_every > 1) {
+      hipDeviceProp_t prop;
+      HIP_OR_THROW(hipGetDeviceProperties(&prop, device));
+      const int ncu = prop.multiProcessorCount;
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+      for (int cu = 0; cu < ncu; cu += cu_every) mask[(size_t)cu / 32] |= 1u << (cu % 32);
+      HIP_OR_THROW(hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)mask.size(), mask.data()));
+    } else {
+      HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+    }
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));
