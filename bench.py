@@ -392,6 +392,7 @@ def main():
     T = 1 << args.log_t
     N = 8 * T
     dev = local if world > 1 and not REHEARSE else 0
+    numa = bind_gpu_local_cpus(torch, dev)
     K = max(1, args.inflight)
     # trace pool: context i cycles through traces i, i+K, ...; each is exactly
     # what `sezkp-cli simulate` writes at its seed (42 = the reference's own),
@@ -593,6 +594,8 @@ def main():
         c.close()
     del ctxs, ctx
     if rank == 0:
+        if numa is not None:
+            out["numa"] = numa
         out["worst_case"] = worst
         out["host_rows"] = host_rows
         if not args.no_cpu_baseline and world == 1:
@@ -642,6 +645,34 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def bind_gpu_local_cpus(torch, dev):
+    """Run this process (its proof threads, the pinned trace buffers they
+    first touch, the DMA reads of the uploads) on the CPUs of the GPU's own
+    NUMA node (sysfs local_cpulist of its PCI device), capped to the CPUs it
+    may already use; SEZKP_BENCH_NUMA=0 leaves placement to the scheduler.
+    Measured round 3 (tools/ab_numa.sh, profiles/r03/ab/ab_numa.txt, three
+    alternating pairs on one box): host -> proof 7.75 / 8.03 / 7.68 ->
+    8.02 / 7.97 / 7.91e9, trace resident even. Returns what was done."""
+    if os.environ.get("SEZKP_BENCH_NUMA", "1") == "0":
+        return None
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/local_cpulist") as f:
+            spec = f.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        if not cpus:
+            return {"pci": bdf, "error": "no allowed CPU on the GPU's node"}
+        os.sched_setaffinity(0, cpus)
+        return {"pci": bdf, "cpus": len(cpus)}
+    except Exception as e:  # reported, never fatal
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def halves(done_t, t0):
