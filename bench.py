@@ -652,9 +652,13 @@ def bind_gpu_local_cpus(torch, dev):
     first touch, the DMA reads of the uploads) on the CPUs of the GPU's own
     NUMA node (sysfs local_cpulist of its PCI device), capped to the CPUs it
     may already use; SEZKP_BENCH_NUMA=0 leaves placement to the scheduler.
-    Measured round 3 (tools/ab_numa.sh, profiles/r03/ab/ab_numa.txt, three
-    alternating pairs on one box): host -> proof 7.75 / 8.03 / 7.68 ->
-    8.02 / 7.97 / 7.91e9, trace resident even. Returns what was done."""
+    The PCI address comes from the HIP device properties, so the runtime is
+    up by now: every thread the process already has (/proc/self/task: the
+    HIP runtime's own threads too) is bound, not only the calling one, and
+    threads created later inherit the mask. Measured round 3
+    (tools/ab_numa.sh, profiles/r03/ab/ab_numa.txt, three alternating pairs
+    on one box, binding the calling thread only): host -> proof 7.75 / 8.03 /
+    7.68 -> 8.02 / 7.97 / 7.91e9, trace resident even. Returns what was done."""
     if os.environ.get("SEZKP_BENCH_NUMA", "1") == "0":
         return None
     try:
@@ -669,8 +673,15 @@ def bind_gpu_local_cpus(torch, dev):
         cpus &= os.sched_getaffinity(0)
         if not cpus:
             return {"pci": bdf, "error": "no allowed CPU on the GPU's node"}
-        os.sched_setaffinity(0, cpus)
-        return {"pci": bdf, "cpus": len(cpus)}
+        bound = 0
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                os.sched_setaffinity(int(tid), cpus)
+                bound += 1
+            except OSError:  # a thread that exited meanwhile
+                pass
+        return {"pci": bdf, "cpus": len(cpus), "threads_bound": bound,
+                "note": "every existing thread of the process (incl. the HIP runtime's) bound; later ones inherit"}
     except Exception as e:  # reported, never fatal
         return {"error": f"{type(e).__name__}: {e}"}
 

@@ -348,3 +348,185 @@ def prove_v1(blocks, manifest_root: bytes) -> bytes:
             ln //= 2
     out += U(layers[k][0]) + bytes(manifest_root)
     return out
+
+
+# ---------------------------------------------------------------- v1 verifier
+class _Rd:
+    """bincode 1.3 fixint LE reader over a ProofV1 (proof.rs:80-98)."""
+
+    def __init__(self, b: bytes):
+        self.b, self.p = bytes(b), 0
+
+    def take(self, n):
+        if self.p + n > len(self.b):
+            raise ValueError("truncated proof bytes")
+        s = self.b[self.p:self.p + n]
+        self.p += n
+        return s
+
+    def u64(self):
+        return struct.unpack("<Q", self.take(8))[0]
+
+    def vec32(self):
+        return [self.take(32) for _ in range(self.u64())]
+
+
+def _opening(rd):  # proof.rs:44-66
+    return {"value_le": rd.take(8), "index": rd.u64(), "chunk_index": rd.u64(), "index_in_chunk": rd.u64(),
+            "chunk_root": rd.take(32), "path_in_chunk": rd.vec32(), "path_to_chunk": rd.vec32()}
+
+
+def parse_proof_v1(b: bytes) -> dict:
+    rd = _Rd(b)
+    pf = {"domain_n": rd.u64(), "tau": rd.u64(), "col_roots": []}
+    for _ in range(rd.u64()):
+        lab = rd.take(rd.u64()).decode()
+        pf["col_roots"].append((lab, rd.take(32)))
+    pf["queries"] = []
+    for _ in range(rd.u64()):
+        q = {"row": rd.u64(), "per_tape": []}
+        for _ in range(rd.u64()):
+            q["per_tape"].append({k: _opening(rd) for k in ("mv", "next_mv", "write_flag", "write_sym", "head",
+                                                              "next_head", "win_len", "in_off", "out_off")})
+        for k in ("is_first", "is_last", "input_mv"):
+            q[k] = _opening(rd)
+        pf["queries"].append(q)
+    pf["fri_roots"] = rd.vec32()
+    pf["fri_queries"] = []
+    for _ in range(rd.u64()):
+        pos = [rd.u64() for _ in range(rd.u64())]
+        pairs = [(rd.take(8), rd.vec32(), rd.take(8), rd.vec32()) for _ in range(rd.u64())]
+        pf["fri_queries"].append({"positions": pos, "pairs": pairs})
+    pf["fri_final_value_le"] = rd.take(8)
+    pf["manifest_root"] = rd.take(32)
+    return pf
+
+
+def merkle_verify(root, leaf_h, idx, sibs):  # merkle.rs:111-126 (MerkleTree::verify)
+    cur = leaf_h
+    for s in sibs:
+        cur = h2(cur, s) if idx & 1 == 0 else h2(s, cur)
+        idx >>= 1
+    return cur == root
+
+
+def _leaf_lab_raw(value_le: bytes, label: str):  # merkle.rs:132-147 over the opened bytes as given
+    lb = label.encode()
+    return blake3(b"col_leaf" + struct.pack("<I", len(lb)) + lb + bytes(value_le))
+
+
+def verify_v1(proof_bytes: bytes, tau_blocks=None):
+    """verify_v1 (crates/sezkp-stark/src/v1/verify.rs:60-196) with fri_verify
+    (fri.rs:130-222) and verify_chunked_open (merkle.rs:243-280). Returns None
+    when the proof is accepted, else the reference's error text. `tau_blocks`:
+    the block windows' tau (verify.rs:73-81), or None for no blocks."""
+    fe = lambda le: int.from_bytes(le, "little") % P
+    try:
+        pf = parse_proof_v1(proof_bytes)
+    except ValueError as e:
+        return str(e)
+    if pf["domain_n"] % 8:
+        return "FRI domain_n not multiple of blowup"
+    n = pf["domain_n"] // 8
+    if n == 0 or n & (n - 1):
+        return "trace length n must be a power of two"
+    tau = pf["tau"]
+    if tau_blocks is not None and tau_blocks != tau:
+        return f"tau mismatch vs. block windows: got {tau}, expected {tau_blocks}"
+    tr = Transcript("sezkp-stark/v1")
+    tr.absorb("manifest_root", pf["manifest_root"])
+    tr.absorb_u64("n", n)
+    tr.absorb_u64("tau", tau)
+    tr.absorb_u64("n_cols", len(pf["col_roots"]))
+    for _lab, r in pf["col_roots"]:
+        tr.absorb("col_root", r)
+    ab = tr.challenge("alphas", 64)
+    a = [int.from_bytes(ab[8 * i:8 * i + 8], "little") % P for i in range(8)]
+    tr.absorb("masks", b"masks")  # derive_mask_coeffs (masking.rs:56-79): alignment only
+    tr.absorb_u64("n_masks", 1)
+    tr.absorb_u64("deg", 4)
+    for _ in range(4):
+        tr.challenge("mask_coeff", 8)
+    tr.challenge("ood_point", 8)
+    roots = pf["fri_roots"]
+    nl = len(roots)
+    tr_rows = Transcript.__new__(Transcript)
+    tr_rows.stream = tr.stream
+    if nl > 0:
+        tr_rows.absorb("fri_layer_root", roots[0])
+        tr_rows.challenge("fri_betas", 8 * max(nl - 1, 0))
+        for r in range(1, nl):
+            tr_rows.absorb("fri_layer_root", roots[r])
+    qb = tr_rows.challenge("row_queries", 8 * 30)
+    expected = [int.from_bytes(qb[8 * i:8 * i + 8], "little") % max(n, 1) for i in range(30)]
+    if len(expected) != len(pf["queries"]):
+        return f"AIR query count mismatch (expected {len(expected)}, got {len(pf['queries'])})"
+    for i, q in enumerate(pf["queries"]):
+        if q["row"] != expected[i]:
+            return f"AIR query row mismatch at position {i}: got {q['row']}, expected {expected[i]}"
+    root_map = dict(pf["col_roots"])
+
+    def vopen(label, o):
+        if label not in root_map:
+            return f"missing col root for {label}"
+        lh = _leaf_lab_raw(o["value_le"], label)
+        if not (merkle_verify(o["chunk_root"], lh, o["index_in_chunk"], o["path_in_chunk"])
+                and merkle_verify(root_map[label], o["chunk_root"], o["chunk_index"], o["path_to_chunk"])):
+            return f"chunked merkle path failed for column {label} @ {o['index']}"
+        return None
+
+    names = [("mv", "mv"), ("mv", "next_mv"), ("wflag", "write_flag"), ("wsym", "write_sym"), ("head", "head"),
+             ("head", "next_head"), ("winlen", "win_len"), ("in_off", "in_off"), ("out_off", "out_off")]
+    for q in pf["queries"]:
+        for lab in ("input_mv", "is_first", "is_last"):
+            e = vopen(lab, q[lab])
+            if e:
+                return e
+        for r, t in enumerate(q["per_tape"]):
+            for kind, key in names:
+                e = vopen(f"{kind}_{r}", t[key])
+                if e:
+                    return e
+        # compose_row_from_openings + compose_boundary_from_openings (air.rs:209-238)
+        isf, isl = fe(q["is_first"]["value_le"]), fe(q["is_last"]["value_le"])
+        acc = 0
+        for t in q["per_tape"]:
+            mv, flg, hd, hn, nmv = (fe(t[k]["value_le"]) for k in ("mv", "write_flag", "head", "next_head", "next_mv"))
+            acc += a[0] * flg * (flg - 1) + a[1] * mv * (mv - 1) * (mv + 1) + a[2] * (1 - isl) * (hn - hd - nmv)
+            acc += a[2] * isf * (hd - mv - fe(t["in_off"]["value_le"])) + a[2] * isl * (hd - fe(t["out_off"]["value_le"]))
+        if acc % P:
+            return f"AIR composition non-zero at row {q['row']}"
+    # fri_verify (fri.rs:130-222), on the transcript after the OOD draw
+    if nl == 0:
+        return "no FRI roots"
+    tr.absorb("fri_layer_root", roots[0])
+    bb = tr.challenge("fri_betas", 8 * (nl - 1))
+    betas = [int.from_bytes(bb[8 * i:8 * i + 8], "little") % P for i in range(nl - 1)]
+    final = pf["fri_final_value_le"]
+    if roots[nl - 1] != blake3(bytes(final)):
+        return "final FRI value mismatch with last root"
+    for fq in pf["fri_queries"]:
+        pos, pairs = fq["positions"], fq["pairs"]
+        if len(pos) != nl:
+            return "positions length mismatch"
+        if len(pairs) != nl - 1:
+            return "pairs length mismatch"
+        idx, ln = pos[0], 1 << (nl - 1)
+        for l in range(nl - 1):
+            half = ln // 2
+            j = idx ^ half
+            vi_le, pi, vj_le, pj = pairs[l]
+            if not (merkle_verify(roots[l], blake3(vi_le), idx, pi) and merkle_verify(roots[l], blake3(vj_le), j, pj)):
+                return f"FRI Merkle path failed at layer {l}"
+            vi, vj = fe(vi_le), fe(vj_le)
+            lower, upper = (vi, vj) if idx < half else (vj, vi)
+            v_fold = (lower + betas[l] * upper) % P
+            if pos[l + 1] != idx % half:
+                return f"FRI index propagation failed at layer {l}"
+            if l + 1 < nl - 1:
+                if fe(pairs[l + 1][0]) != v_fold:
+                    return f"FRI fold mismatch at layer {l}"
+            elif struct.pack("<Q", v_fold) != bytes(final):
+                return "final FRI value mismatch"
+            idx, ln = idx % half, half
+    return None

@@ -15,9 +15,24 @@
 
 namespace sezkp {
 
-void Comm::wait(hipStream_t st, double) {
-  const hipError_t e = hipStreamSynchronize(st);
-  if (e != hipSuccess) throw std::runtime_error(std::string("stream sync: ") + hipGetErrorString(e));
+// Poll the stream against the deadline (every transport: a peer that failed
+// never joins a collective this rank has enqueued, and a plain stream sync
+// would then block forever). Short proofs finish in a few ms: spin first,
+// then back off.
+void Comm::wait(hipStream_t st, double timeout_s) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (int spin = 0;; spin++) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) throw std::runtime_error(std::string("stream: ") + hipGetErrorString(q));
+    const std::string ae = async_error();
+    if (!ae.empty()) throw std::runtime_error("collective failed: " + ae);
+    if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_s)
+      throw std::runtime_error("collective timeout: no progress within " + std::to_string(timeout_s) +
+                               " s (SEZKP_COLL_TIMEOUT_S); a peer rank failed or stalled");
+    if (spin > 200) std::this_thread::sleep_for(std::chrono::microseconds(spin > 2000 ? 1000 : 50));
+  }
 }
 
 namespace {
@@ -42,22 +57,11 @@ struct RcclComm final : Comm {
   ~RcclComm() override {
     if (c) (void)ncclCommDestroy(c);
   }
-  void wait(hipStream_t st, double timeout_s) override {
-    using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
-    for (int spin = 0;; spin++) {
-      const hipError_t q = hipStreamQuery(st);
-      if (q == hipSuccess) return;
-      if (q != hipErrorNotReady) throw std::runtime_error(std::string("stream: ") + hipGetErrorString(q));
-      ncclResult_t ae = ncclSuccess;
-      if (c && ncclCommGetAsyncError(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
-        throw std::runtime_error(std::string("collective failed: ") + ncclGetErrorString(ae));
-      if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_s)
-        throw std::runtime_error("collective timeout: no progress within " + std::to_string(timeout_s) +
-                                 " s (SEZKP_COLL_TIMEOUT_S); a peer rank failed or stalled");
-      // short proofs finish in a few ms: spin first, then back off
-      if (spin > 200) std::this_thread::sleep_for(std::chrono::microseconds(spin > 2000 ? 1000 : 50));
-    }
+  std::string async_error() override {
+    ncclResult_t ae = ncclSuccess;
+    if (c && ncclCommGetAsyncError(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+      return ncclGetErrorString(ae);
+    return {};
   }
   void abort() override {
     if (c) (void)ncclCommAbort(c);

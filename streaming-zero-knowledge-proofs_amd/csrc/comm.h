@@ -25,12 +25,14 @@ struct Comm {
   virtual void group_start() {}
   virtual void group_end() {}
   virtual std::string name() const = 0;
-  // Wait for `st` (which may hold collectives). RCCL: polls the stream and
-  // ncclCommGetAsyncError, and throws once `timeout_s` passes or the
-  // communicator reports an error (a peer that failed never joins a
-  // collective this rank has enqueued, so a plain stream sync would block
-  // forever). Host collectives complete inside their calls: a plain sync.
-  virtual void wait(hipStream_t st, double timeout_s);
+  // Wait for `st` (which may hold collectives): polls the stream and
+  // async_error(), and throws once `timeout_s` passes or the communicator
+  // reports an error (a peer that failed never joins a collective this rank
+  // has enqueued, so a plain stream sync would block forever). The same
+  // policy for every transport (host collectives are tested with it).
+  void wait(hipStream_t st, double timeout_s);
+  // non-empty: the transport saw an asynchronous failure (RCCL: ncclCommGetAsyncError)
+  virtual std::string async_error() { return {}; }
   // Tear the communicator down so that enqueued collectives stop waiting for
   // peers (ncclCommAbort); the owner is unusable afterwards.
   virtual void abort() {}

@@ -756,12 +756,6 @@ __global__ void __launch_bounds__(512, 2) k_ntt_dif9(NttPassArgs P) {
   }
 }
 
-// SEZKP_NTT_NO_NARROW=1: sL = 0 passes load and store their rows directly (A/B comparison)
-static bool narrow_disabled() {
-  static const bool off = getenv("SEZKP_NTT_NO_NARROW") != nullptr;
-  return off;
-}
-
 // launch one pass with the register kernel when its shape allows, else false
 template <bool DIF, bool INV>
 static bool launch_ntt4(hipStream_t st, const NttPassArgs& P, unsigned tiles) {
@@ -771,14 +765,14 @@ static bool launch_ntt4(hipStream_t st, const NttPassArgs& P, unsigned tiles) {
   // sL = 0 passes stage their tile through the LDS image (k_ntt4 NARROW)
 #define SEZKP_NTT4(M1, M2, SK)                                                                                \
   do {                                                                                                         \
-    if (P.sL == 0 && !narrow_disabled())                                                                     \
+    if (P.sL == 0)                                                                                           \
       hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, SK, false, true>), dim3(tiles), dim3(NTT_THREADS), 0, st, P); \
     else                                                                                                       \
       hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, SK>), dim3(tiles), dim3(NTT_THREADS), 0, st, P);           \
   } while (0)
   if (P.m > NTT_MMAX) {  // NARROW + in-tile radix-16 (plan_passes_x16)
     // plain passes, or the LDE's DEEP-polynomial first pass (all its stages: no skip)
-    if (P.sL != 0 || skip || (P.src && !P.dp_rlo) || narrow_disabled()) return false;
+    if (P.sL != 0 || skip || (P.src && !P.dp_rlo)) return false;
 #define SEZKP_NTT4X(M1, M2) \
   hipLaunchKernelGGL((k_ntt4<DIF, INV, M1, M2, 0, false, true, true>), dim3(tiles), dim3(NTT_THREADS), 0, st, P)
     switch (P.m) {
@@ -1162,11 +1156,6 @@ hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scrat
 }
 
 // ------------------------------------------------------------------ host side
-// SEZKP_NTT_RADIX2=1 forces the radix-2 LDS passes (A/B comparison)
-static bool ntt4_disabled() {
-  static const bool off = getenv("SEZKP_NTT_RADIX2") != nullptr;
-  return off;
-}
 static void plan_passes(int logN, int first_min, int* ms, int* np) {
   int passes = (logN + NTT_MMAX - 1) / NTT_MMAX;
   if (passes < 1) passes = 1;
@@ -1182,7 +1171,6 @@ static void plan_passes(int logN, int first_min, int* ms, int* np) {
 // m in [6, 8] (the register kernels). Returns false when it saves nothing.
 // The sL = 0 pass is first for DIT and last for DIF.
 static bool plan_passes_x16(int logN, bool dif, int* ms, int* np) {
-  if (ntt4_disabled() || narrow_disabled()) return false;
   const int cur = std::max(1, (logN + NTT_MMAX - 1) / NTT_MMAX);
   for (int f = 12; f >= 10; f--) {
     const int r = logN - f;
@@ -1203,17 +1191,13 @@ static bool plan_passes_x16(int logN, bool dif, int* ms, int* np) {
 // A 2^21-point DIF (the prover's INTT at T = 2^21) as a 9-stage wide pass
 // (k_ntt_dif9) + the 12-stage X16 narrow pass: 2 HBM round trips instead of
 // 3 passes of 7 (round 3, tools/ab_intt_dif9.sh: intt stage 97 -> 91 us per
-// proof, in flight +0.7-1.1%). SEZKP_NTT_DIF9X16=0: the three passes (A/B).
-static bool dif9x16_enabled() {
-  static const bool on = !(getenv("SEZKP_NTT_DIF9X16") && atoi(getenv("SEZKP_NTT_DIF9X16")) == 0);
-  return on;
-}
+// proof, in flight +0.7-1.1%).
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T) {
   if (logN == 0) return hipSuccess;
   int ms[8], np;
   const bool x16 = plan_passes_x16(logN, true, ms, &np);
   if (!x16) plan_passes(logN, 1, ms, &np);
-  if (logN == 21 && dif9x16_enabled() && !ntt4_disabled() && !narrow_disabled()) {
+  if (logN == 21) {
     NttPassArgs P{};
     P.a = a; P.tw = T; P.m = 9; P.sL = 12; P.inverse = inverse ? 1 : 0; P.logC = 4;
     const unsigned tiles = (unsigned)((1ULL << logN) >> (9 + 4));
@@ -1240,9 +1224,8 @@ hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
       if (!ok) return hipErrorInvalidValue;
       continue;
     }
-    const bool fast = !ntt4_disabled() &&
-                      (inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
-                               : launch_ntt4<true, false>(st, P, (unsigned)tiles));
+    const bool fast = inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
+                              : launch_ntt4<true, false>(st, P, (unsigned)tiles);
     if (!fast) hipLaunchKernelGGL(k_ntt_pass<true>, dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
   }
   return hipGetLastError();
@@ -1251,10 +1234,6 @@ hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
 // DIT from bit-reversed input. If src != nullptr, the first pass loads the
 // replicated, scaled coefficients (LDE) and skips the 3 stages replication
 // makes trivial (blowup 8).
-static bool deep_fused_disabled() {  // SEZKP_NO_DEEP_FUSE=1: separate k_deep (A/B comparison)
-  static const bool off = getenv("SEZKP_NO_DEEP_FUSE") != nullptr;
-  return off;
-}
 hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T,
                    const uint64_t* src, int log_src, uint64_t inv_n, uint64_t coset_e, const DeepFuse* deep,
                    bool* fused, const DeepPoly* dpoly, int src_logP) {
@@ -1290,7 +1269,7 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
       continue;
     }
     // last pass, forward, 16 wide columns, M1 = 4 (m = 7 or 8), not the replicated first pass
-    if (deep && fused && i == np - 1 && i > 0 && !inverse && !ntt4_disabled() && !deep_fused_disabled() &&
+    if (deep && fused && i == np - 1 && i > 0 && !inverse &&
         logC == 4 && P.sL >= 4 && (P.m == 8 || P.m == 7)) {
       P.deep_z = deep->z; P.deep_logN = deep->logN; P.deep_logP = deep->logP; P.deep_g = deep->g;
       if (P.m == 8)
@@ -1301,33 +1280,21 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
       sL += ms[i];
       continue;
     }
-    const bool fast = !ntt4_disabled() &&
-                      (inverse ? launch_ntt4<false, true>(st, P, (unsigned)tiles)
-                               : launch_ntt4<false, false>(st, P, (unsigned)tiles));
+    const bool fast = inverse ? launch_ntt4<false, true>(st, P, (unsigned)tiles)
+                              : launch_ntt4<false, false>(st, P, (unsigned)tiles);
     if (!fast) hipLaunchKernelGGL(k_ntt_pass<false>, dim3((unsigned)tiles), dim3(NTT_THREADS), 0, st, P);
     sL += ms[i];
   }
   return hipGetLastError();
 }
 
-// SEZKP_NTT_BITREV_PASS=1: natural-order transforms keep the separate in-place
-// bit reversal (A/B comparison)
-static bool nat_disabled() {
-  static const bool off = getenv("SEZKP_NTT_BITREV_PASS") != nullptr;
-  return off;
-}
-// SEZKP_NTT_NAT_TR=0: 2^23..2^26 keep the separate bit reversal (A/B comparison)
-static bool nat_tr_disabled() {
-  static const bool off = getenv("SEZKP_NTT_NAT_TR") && atoi(getenv("SEZKP_NTT_NAT_TR")) == 0;
-  return off;
-}
 // Natural order through the transposed last pass (nat_tr): passes of <= 9
 // stages, then 8 (2^23: 8+7+8, 2^24: 8+8+8, 2^25: 9+8+8, 2^26: 9+9+8). The
 // first pass reads `a` and writes `scratch`, the middle ones run in place on
 // scratch, the last gathers from scratch and writes `a` in natural order.
 static bool ntt_dif_natural_tr(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse,
                                const NttTables& T, uint64_t scale, hipError_t* err) {
-  if (logN < 23 || logN > 26 || nat_tr_disabled() || ntt4_disabled() || narrow_disabled()) return false;
+  if (logN < 23 || logN > 26) return false;
   int plan[3];
   plan[2] = 8;
   const int rest = logN - 8;              // 15..18
@@ -1363,11 +1330,6 @@ static bool ntt_dif_natural_tr(hipStream_t st, uint64_t* a, uint64_t* scratch, i
 // bit-reversal pass. The first
 // pass reads `a` and writes `scratch`, the middle ones run in place on
 // scratch, the last one writes `a` (n^-1 on its pre-twiddle chain).
-// SEZKP_NTT_NAT_DIT=0: keep the DIF forms below (A/B).
-static bool nat_dit_disabled() {
-  static const bool off = getenv("SEZKP_NTT_NAT_DIT") && atoi(getenv("SEZKP_NTT_NAT_DIT")) == 0;
-  return off;
-}
 static bool ntt_dit_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, bool inverse,
                             const NttTables& T, uint64_t scale, hipError_t* err) {
   // measured (round 3, profiles/r03/ntt_nat_ab2.txt, fwd + inv round trips):
@@ -1375,7 +1337,7 @@ static bool ntt_dit_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int 
   // vs 283.2, 2^24 498.5 vs 508.7 (584.8 with the bit-reversal pass); the
   // X16 plans' point gather loses (2^25 1267 vs 1053, 2^26 2493 vs 2109), so
   // those sizes keep the DIF forms
-  if (logN < 21 || logN > 24 || nat_dit_disabled() || ntt4_disabled() || narrow_disabled()) return false;
+  if (logN < 21 || logN > 24) return false;
   int ms[8], np;
   if (plan_passes_x16(logN, false, ms, &np)) return false;
   plan_passes(logN, 1, ms, &np);
@@ -1404,7 +1366,7 @@ bool ntt_dif_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, b
   if (scratch && scratch != a && ntt_dif_natural_tr(st, a, scratch, logN, inverse, T, scale, err)) return true;
   // measured (profiles/r02_ntt_nat_ab.txt): 1-5% faster at 2^19..2^22, slower from 2^24 (where the
   // scattered lines no longer merge in L2 before write-back: 687 vs 577 us at 2^24)
-  if (!scratch || scratch == a || logN < 19 || logN > 22 || nat_disabled() || ntt4_disabled() || narrow_disabled())
+  if (!scratch || scratch == a || logN < 19 || logN > 22)
     return false;
   int ms[8], np;
   const bool x16 = plan_passes_x16(logN, true, ms, &np);
@@ -1441,11 +1403,10 @@ hipError_t bitrev_permute(hipStream_t st, const uint64_t* in, uint64_t* out, int
   return hipGetLastError();
 }
 
-// SEZKP_BITREV_A=4|5|6 overrides the tile side 2^A (A/B measurements)
+// tile side 2^A; measured (round 2): 2^26 round trip 2910 / 2782 / 2819 us at
+// A = 4 / 5 / 6; 2^24 (MALL-resident) best at 4
 static int bitrev_tile_log(int logN) {
-  static const int forced = getenv("SEZKP_BITREV_A") ? atoi(getenv("SEZKP_BITREV_A")) : 0;
-  // measured (round 2): 2^26 round trip 2910 / 2782 / 2819 us at A = 4 / 5 / 6; 2^24 (MALL-resident) best at 4
-  int A = forced >= 4 && forced <= 6 ? forced : (logN >= 25 ? 5 : 4);
+  int A = logN >= 25 ? 5 : 4;
   while (A > 4 && logN < 2 * A) A--;
   return A;
 }
@@ -1453,8 +1414,7 @@ hipError_t bitrev_inplace(hipStream_t st, uint64_t* a, int logN, uint64_t scale,
   if (logN < 8) return hipErrorInvalidValue;
   const int A = bitrev_tile_log(logN);
   const dim3 grid(1u << (logN - 2 * A));
-  if (A == 6) hipLaunchKernelGGL(k_bitrev_inplace<6>, grid, dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
-  else if (A == 5) hipLaunchKernelGGL(k_bitrev_inplace<5>, grid, dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
+  if (A == 5) hipLaunchKernelGGL(k_bitrev_inplace<5>, grid, dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
   else hipLaunchKernelGGL(k_bitrev_inplace<4>, grid, dim3(256), 0, st, a, logN, scale, do_scale ? 1 : 0);
   return hipGetLastError();
 }

@@ -151,17 +151,6 @@ struct AsyncSlot {
   size_t len = 0;
 };
 
-// SEZKP_MAPPED_ROOTS=1: the tree kernels store the Merkle roots straight into
-// mapped host memory, so no copy is launched at the three transcript points.
-// Measured (round 2, two alternating A/B runs each): one proof at a time
-// 2.51 against 2.56 ms, but 3 proofs in flight 8.06-8.10 against 8.13·10^9
-// (each root store waits on a PCIe write at the kernel's end), so the default
-// keeps the roots in device memory and copies them.
-static bool roots_copied() {
-  static const bool on = getenv("SEZKP_MAPPED_ROOTS") == nullptr;
-  return on;
-}
-
 static int worker_delay_us() {
   static const int us = [] {
     const char* e = getenv("SEZKP_TEST_WORKER_DELAY_US");
@@ -189,8 +178,6 @@ struct sezkp_ctx {
     uint8_t* raw = nullptr;     // step arrays as the view holds them (row-major), before k_trace_image
     uint64_t* h_tab = nullptr;  // pinned staging of bw | bi | bo
     hipEvent_t ready = nullptr;
-    hipEvent_t consumed = nullptr;  // image_on_main: k_trace_image (main stream) has read `raw`
-    bool raw_pending = false;        // image_on_main: `raw` holds a staged trace not yet transposed
   };
   TraceSlot slot[2];
   int active = 0;
@@ -262,7 +249,6 @@ struct sezkp_ctx {
   ForestLayer* d_forest = nullptr;
   uint64_t* d_tailbuf = nullptr;   // single device: fold-replay scratch of the small-layer workgroups
   int n_forest = 0;
-  std::vector<uint32_t> forest_wg_start;  // host copy of d_forest[i].wg_start
   uint32_t forest_wgs = 0;
   UpperJob* d_jobs = nullptr;  // upper-level passes: layer 0, then all fold layers
   std::vector<std::pair<size_t, int>> jobs0, jobsF;
@@ -295,6 +281,9 @@ struct sezkp_ctx {
   std::vector<CollStat> coll_stats;
   std::vector<hipEvent_t> coll_ev;
   size_t coll_used = 0;
+  // test hook (SEZKP_DEBUG_STALL_AFTER): a mapped word the stream waits on
+  // after a collective, so that the collective looks stuck; set at destroy
+  uint32_t* stall_word = nullptr;
 
   static void* take_spare(std::multimap<size_t, void*>& m, size_t bytes) {
     auto it = m.find(bytes);
@@ -405,6 +394,7 @@ struct sezkp_ctx {
     }
   }
   ~sezkp_ctx() {
+    if (stall_word) __atomic_store_n(stall_word, 1u, __ATOMIC_SEQ_CST);  // release a stalled stream
     if (async) {  // let a proof in flight finish, then stop the worker
       {
         std::unique_lock<std::mutex> lk(async->mu);
@@ -430,11 +420,10 @@ struct sezkp_ctx {
     if (stc) (void)hipStreamSynchronize(stc);
     for (auto& sl : slot)
       if (sl.ready) (void)hipEventDestroy(sl.ready);
-    for (auto& sl : slot)
-      if (sl.consumed) (void)hipEventDestroy(sl.consumed);
     if (st) (void)hipStreamDestroy(st);
     if (st2 && st2 != st) (void)hipStreamDestroy(st2);
     if (stc) (void)hipStreamDestroy(stc);
+    if (stall_word) (void)hipHostFree(stall_word);
   }
 
   void upload(const sezkp_block_view& v);
@@ -442,7 +431,7 @@ struct sezkp_ctx {
   void stage(const sezkp_block_view& v);
   void alloc_slot(TraceSlot& t);
   // block tables + step arrays of `v` into slot t, async on stream s
-  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, bool image = true);
+  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s);
   void check_shape_same(const sezkp_block_view& v) const;
   void take_staged();
   // proves into the pinned staging buffer; returns its size (bytes at h_proof)
@@ -457,51 +446,20 @@ static double coll_timeout_s() {
   static const double t = getenv("SEZKP_COLL_TIMEOUT_S") ? atof(getenv("SEZKP_COLL_TIMEOUT_S")) : 60.0;
   return t > 0 ? t : 60.0;
 }
+static bool hook_match(const char* spec, int rank, const char* name) {
+  if (!spec) return false;
+  const char* colon = strchr(spec, ':');
+  return colon && atoi(spec) == rank && strcmp(colon + 1, name) == 0;
+}
 // test hook: SEZKP_DEBUG_FAIL_AT=<rank>:<collective> makes that rank fail
 // right before that collective of every sharded prove (tests/test_gpu_sharded.py)
 static void fail_point(int rank, const char* name) {
   static const char* spec = getenv("SEZKP_DEBUG_FAIL_AT");
-  if (!spec) return;
-  const char* colon = strchr(spec, ':');
-  if (!colon || atoi(spec) != rank || strcmp(colon + 1, name) != 0) return;
+  if (!hook_match(spec, rank, name)) return;
   throw Err{SEZKP_E_DEVICE, std::string("injected failure before collective ") + name + " on rank " +
                                 std::to_string(rank)};
 }
 
-// SEZKP_FOREST_EARLY=1 (A/B): the FRI forest's first-fold-pass layers
-// hashed on the side stream beside the later fold passes instead of one
-// forest launch after the whole chain (measured round 3, tools/
-// ab_forest_early.sh: fri_fold_trees 0.709 -> 0.725 ms, the forest's
-// workgroups starve the later folds; off)
-static bool forest_early() {
-  static const bool on = getenv("SEZKP_FOREST_EARLY") && atoi(getenv("SEZKP_FOREST_EARLY")) != 0;
-  return on;
-}
-// SEZKP_TABLES_EARLY=1 (A/B): k_col_tables beside expand (measured round 3,
-// tools/ab_tables_early.sh: expand 37.7 -> 54.1 us, expand + col_commit
-// 0.481 -> 0.511 ms; off)
-static bool tables_early_on() {
-  static const bool on = getenv("SEZKP_TABLES_EARLY") && atoi(getenv("SEZKP_TABLES_EARLY")) != 0;
-  return on;
-}
-// SEZKP_SIDE_AT=0|1|2 (A/B): where the side-stream columns (tables, dense,
-// piecewise) start: 0 right after expand, beside the whole dictionary chain;
-// 1 after the dictionary plan; 2 after the table levels, beside the commit
-// kernel only (measured: the commit kernel then starves k_col_tables,
-// 37 -> 337 us, and the stage is 35 us longer)
-static int side_at() {
-  static const int v = getenv("SEZKP_SIDE_AT") ? atoi(getenv("SEZKP_SIDE_AT")) : 0;
-  return v;
-}
-// The query requests (a few KB per proof) live in mapped host memory that the
-// path / opening kernels read directly, so no small H2D copy queues behind a
-// staged trace upload on the copy engine (round 3, tools/ab_req_mapped.sh:
-// host -> proof 7.91 -> 7.97e9 mean of three alternating runs, spread 2.5% ->
-// 0.3%). SEZKP_REQ_MAPPED=0: the H2D copy into device memory (A/B).
-static bool req_mapped() {
-  static const bool on = !(getenv("SEZKP_REQ_MAPPED") && atoi(getenv("SEZKP_REQ_MAPPED")) == 0);
-  return on;
-}
 
 void sezkp_ctx::upload(const sezkp_block_view& v) {
   HIP_OR_THROW(hipSetDevice(device));
@@ -548,10 +506,9 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   staged = false;
   active = 0;
   {
-    hipEvent_t keep = slot[1].ready, keep_c = slot[1].consumed;
+    hipEvent_t keep = slot[1].ready;
     slot[1] = TraceSlot{};
     slot[1].ready = keep;
-    slot[1].consumed = keep_c;
   }
   alloc_slot(slot[0]);
   uint64_t* d_bs = dalloc<uint64_t>(nblk + 1);
@@ -688,7 +645,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   up(d_work, work.data(), work.size());
   outer_stride = tree_stored_nodes(logChunks, 0);
   d_outer = dalloc<uint32_t>((size_t)ncols * outer_stride * 8);
-  d_colroots = roots_copied() ? dalloc<uint32_t>((size_t)ncols * 8) : hmapped<uint32_t>((size_t)ncols * 8);
+  d_colroots = dalloc<uint32_t>((size_t)ncols * 8);
 
   // ---- LDE / FRI workspace
   // Layer r has 2^(k-r) leaves. Run layers (r <= rR, >= 4096 P leaves) are
@@ -722,7 +679,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   }
   d_fri = dalloc<uint64_t>(run_vals + 1);
   d_rep = dalloc<uint64_t>(rep_vals + 1);
-  d_roots = roots_copied() ? dalloc<uint32_t>((size_t)(k + 2) * 8) : hmapped<uint32_t>((size_t)(k + 2) * 8);
+  d_roots = dalloc<uint32_t>((size_t)(k + 2) * 8);
   uint32_t* root_dummy = d_roots + 8 * (k + 1);
   uint64_t total_nodes = 0;
   for (int r = 0; r <= k; r++) {
@@ -773,8 +730,6 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     }
     n_forest = (int)fl.size();
     forest_wgs = wgs;
-    forest_wg_start.clear();
-    for (auto& f : fl) forest_wg_start.push_back(f.wg_start);
     d_forest = dalloc<ForestLayer>(fl.size() + 1);
     if (!fl.empty()) up(d_forest, fl.data(), fl.size());
     d_tailbuf = sharded() ? nullptr : dalloc<uint64_t>((size_t)TAIL_MAX << TAIL_MAX);
@@ -801,13 +756,12 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   }
   max_fri_req = (size_t)NUM_QUERIES * 2 * k;
   max_open_req = (size_t)NUM_QUERIES * (3 + 9 * tau);
-  if (req_mapped()) {  // the path / opening kernels read the requests over PCIe: no H2D copy
-    h_req = hmapped<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
-    d_req = h_req;
-  } else {
-    d_req = dalloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
-    h_req = halloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
-  }
+  // The query requests (a few KB per proof) live in mapped host memory that
+  // the path / opening kernels read directly, so no small H2D copy queues
+  // behind a staged trace upload on the copy engine (round 3,
+  // tools/ab_req_mapped.sh: host -> proof 7.91 -> 7.97e9, mean of three)
+  h_req = hmapped<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
+  d_req = h_req;
   // ---- proof layout (proof.rs:80-98, bincode fixint LE)
   {
     BinWriter w;
@@ -856,32 +810,16 @@ void sezkp_ctx::alloc_slot(TraceSlot& t) {
   t.raw = dalloc<uint8_t>(4 * cells);  // wsym (2-byte aligned first), mv, has_write
   t.h_tab = halloc<uint64_t>(3 * nt + 1);
   if (!t.ready) HIP_OR_THROW(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
-  if (!t.consumed) {
-    HIP_OR_THROW(hipEventCreateWithFlags(&t.consumed, hipEventDisableTiming));
-    HIP_OR_THROW(hipEventRecord(t.consumed, st));
-  }
-  t.raw_pending = false;
-}
-
-// SEZKP_IMAGE_ON_MAIN=1: a staged trace's transposition (k_trace_image) runs
-// on the main stream when the proof takes the trace, so the copy stream holds
-// only the PCIe copies (no kernel waiting behind them in a hardware queue that
-// other streams share); 0 = the transposition follows the copies on the copy
-// stream (round 2)
-static bool image_on_main() {
-  static const bool on = getenv("SEZKP_IMAGE_ON_MAIN") && atoi(getenv("SEZKP_IMAGE_ON_MAIN")) != 0;
-  return on;
 }
 
 // Per-block tables on the host (window lengths, head offsets: tau * n_blocks
 // values), then every array over PCIe asynchronously on `s` and the row-major
 // step arrays transposed to the tape-major image on the device.
-void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, bool image) {
+void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s) {
   const size_t cells = (size_t)tau * n, nt = (size_t)tau * nblk;
-  // the previous copy out of h_tab (an earlier stage into this slot) must be done
+  // the previous copy out of h_tab (an earlier stage into this slot, and its
+  // transposition of `raw` on the same stream) must be done
   HIP_OR_THROW(hipEventSynchronize(t.ready));
-  // and the raw arrays it filled must have been transposed already
-  if (s != st) HIP_OR_THROW(hipStreamWaitEvent(s, t.consumed, 0));
   for (uint32_t k = 0; k < nblk; k++)
     for (uint32_t r = 0; r < tau; r++) {
       const size_t i = (size_t)k * tau + r, o = (size_t)r * nblk + k;
@@ -894,12 +832,11 @@ void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t
   // each array in copies of <= 4 MB, so a proof's D2H copy queued on the same
   // copy engine waits for one chunk, not for the rest of a 67 MB upload
   // (round 3, tools/ab_upload_chunk.sh: host -> proof 7.89 -> 7.94e9, within
-  // the run-to-run spread). SEZKP_UPLOAD_CHUNK_MB=<m>: m MB, 0 = one copy.
-  static const size_t chunk =
-      (getenv("SEZKP_UPLOAD_CHUNK_MB") ? (size_t)atol(getenv("SEZKP_UPLOAD_CHUNK_MB")) : (size_t)4) << 20;
+  // the run-to-run spread)
+  constexpr size_t chunk = (size_t)4 << 20;
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     for (size_t o = 0; o < bytes;) {
-      const size_t b = chunk ? std::min(chunk, bytes - o) : bytes - o;
+      const size_t b = std::min(chunk, bytes - o);
       HIP_OR_THROW(hipMemcpyAsync((uint8_t*)dst + o, (const uint8_t*)src + o, b, hipMemcpyHostToDevice, s));
       o += b;
     }
@@ -912,8 +849,7 @@ void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t
   cp(raw_hw, v.has_write, cells);
   cp(t.imv, v.input_mv, n);
   cp(t.bw, t.h_tab, 3 * nt * 8);
-  if (image) HIP_OR_THROW(launch_trace_image(s, raw_mv, raw_hw, raw_ws, n, tau, t.mv, t.wf, t.ws));
-  t.raw_pending = !image;
+  HIP_OR_THROW(launch_trace_image(s, raw_mv, raw_hw, raw_ws, n, tau, t.mv, t.wf, t.ws));
   HIP_OR_THROW(hipEventRecord(t.ready, s));
 }
 
@@ -939,7 +875,7 @@ void sezkp_ctx::stage(const sezkp_block_view& v) {
   TraceSlot& t = slot[1 - active];
   if (!t.imv) alloc_slot(t);  // first stage on this workspace: the spare image
   staged = false;             // (re)filling the spare slot
-  write_trace(t, v, stc, !image_on_main());
+  write_trace(t, v, stc);
   staged = true;
 }
 
@@ -961,13 +897,6 @@ void sezkp_ctx::take_staged() {
     T.blk_offin = t.bi;
     T.blk_offout = t.bo;
     HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
-    if (t.raw_pending) {  // image_on_main: transpose on the main stream, ahead of the proof
-      const size_t cells = (size_t)tau * n;
-      HIP_OR_THROW(launch_trace_image(st, reinterpret_cast<int8_t*>(t.raw + 2 * cells), t.raw + 3 * cells,
-                                      reinterpret_cast<uint16_t*>(t.raw), n, tau, t.mv, t.wf, t.ws));
-      HIP_OR_THROW(hipEventRecord(t.consumed, st));
-      t.raw_pending = false;
-    }
   }
 }
 
@@ -1056,49 +985,40 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     }
     HIP_OR_THROW(hipEventRecord(b, st));
     coll_stats.push_back(CollStat{name, wire, a, b});
+    // test hook: SEZKP_DEBUG_STALL_AFTER=<rank>:<collective> holds that rank's
+    // stream after the collective (a wait on a mapped word released only at
+    // destroy), so the next wait must give up at SEZKP_COLL_TIMEOUT_S
+    static const char* stall = getenv("SEZKP_DEBUG_STALL_AFTER");
+    if (hook_match(stall, rank, name)) {
+      if (!stall_word) {
+        HIP_OR_THROW(hipHostMalloc(&stall_word, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        *stall_word = 0;
+      }
+      HIP_OR_THROW(hipStreamWaitValue32(st, stall_word, 1, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    }
   };
   const uint64_t P1 = (uint64_t)world - 1;
   rec(0);
   // ---- column commitments (openings.rs:306-398): this rank's chunks, then
   // every rank gathers all chunk roots and builds the outer trees
-  // SEZKP_TABLES_EARLY=1: the piecewise columns' U tables (they need only
-  // the block tables) on the side stream beside expand instead of beside the
-  // dictionary chain's head
-  const bool tables_early = tables_early_on() && side_at() == 0;
-  if (tables_early) {
-    HIP_OR_THROW(hipEventRecord(ev_fold, st));
-    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
-    ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
-  }
-  ok(launch_expand(st, T, blk_lo, blk_cnt), "expand");
+  ok(launch_expand(st, T, blk_lo, blk_cnt, d_err), "expand");
   rec(1);
   const uint64_t row_lo = n >= 1024 ? ch_lo << COL_CHUNK_LOG2 : 0;
   const uint64_t row_hi = n >= 1024 ? ch_hi << COL_CHUNK_LOG2 : n;
   // piecewise / table / dense columns on the side stream, concurrent with the
-  // (VALU-bound) dictionary columns; disjoint outer-tree leaves
-  auto side_columns = [&](hipEvent_t after) {
-    HIP_OR_THROW(hipStreamWaitEvent(st2, after, 0));
-    if (!tables_early)
-      ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
-    ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
-    ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
-                            outer_stride, d_err), "col_commit_pw");
-    HIP_OR_THROW(hipEventRecord(ev_cols, st2));
-  };
-  if (side_at() > 0) {
-    // the latency-bound head of the dictionary chain (ranges, plan; with 2 the
-    // table levels too) alone on the chip, the side-stream columns after it
-    ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
-                          row_hi - row_lo, d_dlev, ev_expand, side_at()),
-       "col_commit_dict");
-    side_columns(ev_expand);
-  } else {
-    HIP_OR_THROW(hipEventRecord(ev_expand, st));
-    side_columns(ev_expand);
-    ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
-                          row_hi - row_lo, d_dlev),
-       "col_commit_dict");
-  }
+  // (VALU-bound) dictionary columns; disjoint outer-tree leaves. (Starting
+  // them later, beside part of the dictionary chain only, or on a CU-masked
+  // stream, measured even or slower in round 3.)
+  HIP_OR_THROW(hipEventRecord(ev_expand, st));
+  HIP_OR_THROW(hipStreamWaitEvent(st2, ev_expand, 0));
+  ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
+  ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
+  ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
+                          outer_stride, d_err), "col_commit_pw");
+  HIP_OR_THROW(hipEventRecord(ev_cols, st2));
+  ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
+                        row_hi - row_lo, d_dlev),
+     "col_commit_dict");
   HIP_OR_THROW(hipStreamWaitEvent(st, ev_cols, 0));
   if (sharded) {
     const size_t bytes = (size_t)(ch_hi - ch_lo) * 32;
@@ -1124,16 +1044,19 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   static const char* trip = getenv("SEZKP_DEBUG_TRIP_GUARD");
   if (trip && atoi(trip) == rank) HIP_OR_THROW(hipMemsetAsync(d_err, 0x7f, 1, st));
   if (sharded) coll("guard_words", P1 * 4, [&] { comm->allgather(d_err, d_err + 8, 4, st); });
-  const bool copy_roots = roots_copied();
-  if (copy_roots) HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
   HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * ncols, sharded ? d_err + 8 : d_err, 4 * nguard, hipMemcpyDeviceToHost, st));
   sync();
   mark("sync1");
-  const uint32_t* colroots_h = copy_roots ? h_small : d_colroots;  // mapped: the kernels' own stores
-  for (int r = 0; r < nguard; r++)
-    if (h_small[8 * ncols + r])
-      throw Err{SEZKP_E_DEVICE, "column commitment guard tripped on rank " + std::to_string(sharded ? r : rank) +
-                                    " (code " + std::to_string(h_small[8 * ncols + r]) + ")"};
+  const uint32_t* colroots_h = h_small;
+  for (int r = 0; r < nguard; r++) {
+    const uint32_t g = h_small[8 * ncols + r];
+    const std::string who = " on rank " + std::to_string(sharded ? r : rank);
+    if (g & GUARD_HEAD_RANGE)
+      throw Err{SEZKP_E_INVALID, "a block's head position leaves the i32 range" + who +
+                                     " (block too long for its moves: block length x max |mv| must stay below 2^31)"};
+    if (g) throw Err{SEZKP_E_DEVICE, "column commitment guard tripped" + who + " (code " + std::to_string(g) + ")"};
+  }
   std::vector<uint8_t> colroots((const uint8_t*)colroots_h, (const uint8_t*)colroots_h + (size_t)ncols * 32);
   for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
 
@@ -1275,10 +1198,10 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     rec(ST_L0TREE + 1);
   }
   rec(ST_L0UP + 1);
-  if (copy_roots) HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
   sync();
   mark("sync2");
-  const uint32_t* roots_h = copy_roots ? h_small : d_roots;
+  const uint32_t* roots_h = h_small;
   std::vector<uint8_t> roots((size_t)(k + 1) * 32);
   memcpy(roots.data(), roots_h, 32);
   tr.absorb("fri_layer_root", roots.data(), 32);
@@ -1308,17 +1231,13 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     ok(launch_fri_tail(st2, ta), "fri_tail");
     HIP_OR_THROW(hipEventRecord(ev_tail, st2));
   };
-  static const int fold_max = getenv("SEZKP_FOLD_MAX") ? std::max(2, std::min(FOLD_MAX, atoi(getenv("SEZKP_FOLD_MAX"))))
-                                                      : FOLD_MAX;
   mark("folds");
-  static const bool tail_separate = getenv("SEZKP_TAIL_SEPARATE") != nullptr;
-  const bool tail_merged = !sharded && tail_first <= k && n_forest > 0 && d_tailbuf && !tail_separate;
-  // SEZKP_FOREST_EARLY=1: the layers of the first fold pass (15/16 of the
-  // forest's work) are hashed on the side stream as soon as that pass is
-  // done, beside the later fold passes; the rest (and the tail) follows them
-  int forest_split = 0;  // layers 1..forest_split go to the early launch
-  for (int r = 0; r < rR;) {  // fold chain, up to fold_max layers per pass
-    const int F = std::min(fold_max, rR - r);
+  const bool tail_merged = !sharded && tail_first <= k && n_forest > 0 && d_tailbuf;
+  // fold chain, up to FOLD_MAX layers per pass (2 measured even); the forest
+  // follows the whole chain (hashing the first pass's layers beside the later
+  // folds measured slower in round 3: the forest starves the folds)
+  for (int r = 0; r < rR;) {
+    const int F = std::min(FOLD_MAX, rR - r);
     if (F >= 2) {
       FoldOuts fo{};
       for (int m = 1; m <= F; m++) {
@@ -1331,23 +1250,13 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
       ok(launch_fold(st, lvals[r], lvals[r + 1], ltrees[r + 1].logLen, beta_of(r)), "fri_fold");
       r += 1;
     }
-    if (forest_split == 0 && r < rR && tail_merged && forest_early()) {
-      forest_split = r;
-      HIP_OR_THROW(hipEventRecord(ev_fold, st));
-      HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
-      ok(launch_forest16(st2, d_forest, r, forest_wg_start[r], nullptr, nullptr, 0), "fri_forest_early");
-      HIP_OR_THROW(hipEventRecord(ev_tail, st2));
-    }
   }
   const uint64_t* rep_src = rR >= 0 ? lvals[rR] : d_lde;  // full values of the layer above the replicated ones
   // single device: the small layers ride in the forest launch's first
-  // workgroups (SEZKP_TAIL_SEPARATE=1: their own kernel on the side stream)
+  // workgroups (sharded: their own kernel on the side stream)
   if (tail_merged) {
     const TailArgs ta = tail_args(rep_src);
-    const uint32_t base = forest_split ? forest_wg_start[forest_split] : 0;
-    ok(launch_forest16(st, d_forest + forest_split, n_forest - forest_split, forest_wgs - base, &ta, d_tailbuf, base),
-       "fri_forest");
-    if (forest_split) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
+    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf, 0), "fri_forest");
   } else {
     if (!sharded) launch_tail(rep_src);
     ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
@@ -1377,7 +1286,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
   if (tail_first <= k && !tail_merged) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
   rec(ST_FRI + 1);
-  if (copy_roots) HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
   sync();
   mark("sync3");
   memcpy(roots.data(), roots_h, (size_t)(k + 1) * 32);
@@ -1450,8 +1359,6 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     push_open(0, row);  // input_mv
   }
   mark("req_copy");
-  if (d_req != h_req)
-    HIP_OR_THROW(hipMemcpyAsync(d_req, h_req, (3 * max_fri_req + OPEN_REQ_WORDS * no) * 4, hipMemcpyHostToDevice, st));
   if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
   // openings first: their section of the proof (~70% of it) goes back over
   // PCIe on the side stream while the FRI path kernel runs
@@ -1566,24 +1473,7 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     HIP_OR_THROW(hipSetDevice(device));
     HIP_OR_THROW(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto& e : c->ev) HIP_OR_THROW(hipEventCreate(&e));
-    // SEZKP_ONE_STREAM=1: the side-stream work runs on the main stream (one
-    // hardware queue per context when many contexts share the GPU)
-    // SEZKP_SIDE_CU_EVERY=<k> (A/B): the side stream may use only every k-th
-    // CU (hipExtStreamCreateWithCUMask), so its latency-bound kernels cannot
-    // take the whole chip from the main stream's chain
-    const int cu_every = getenv("SEZKP_SIDE_CU_EVERY") ? atoi(getenv("SEZKP_SIDE_CU_EVERY")) : 0;
-    if (getenv("SEZKP_ONE_STREAM")) {
-      c->st2 = c->st;
-    } else if (cu_every > 1) {
-      hipDeviceProp_t prop;
-      HIP_OR_THROW(hipGetDeviceProperties(&prop, device));
-      const int ncu = prop.multiProcessorCount;
-      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-      for (int cu = 0; cu < ncu; cu += cu_every) mask[(size_t)cu / 32] |= 1u << (cu % 32);
-      HIP_OR_THROW(hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)mask.size(), mask.data()));
-    } else {
-      HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
-    }
+    HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));

@@ -137,9 +137,12 @@ struct TraceDev {
   const uint64_t* blk_offout; // [tau][nblk]
   uint32_t* row_blk;          // [n]   (derived)
   uint8_t* row_flags;         // [n]   bit0 first, bit1 last (derived)
-  int32_t* head;              // [tau][n] post-move head (derived; block-local, |head| <= block length < 2^29)
+  int32_t* head;              // [tau][n] post-move head (derived; block-local; k_expand rejects |head| >= 2^31)
   int64_t* head_rng;          // [tau][nblk][2] per-block min / max of head (derived by k_expand)
 };
+
+// guard word bits (d_err): a kernel saw input it cannot represent
+constexpr uint32_t GUARD_HEAD_RANGE = 0x100u;  // k_expand: a head outside i32
 
 struct Alphas {
   uint64_t bool_flag, mv_domain, head_update, head_bits_bool, head_reconstruct, slack_bits_bool,
@@ -230,7 +233,8 @@ struct ProofLayout {
 // row-major step arrays [n][tau] -> tape-major trace image [tau][n]
 hipError_t launch_trace_image(hipStream_t st, const int8_t* raw_mv, const uint8_t* raw_hw, const uint16_t* raw_ws,
                               uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws);
-hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt);
+// d_err: guard word, GUARD_HEAD_RANGE is or-ed in when a head leaves the i32 range
+hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt, uint32_t* d_err);
 hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_tab_cols,
                              int n_tab_cols, uint64_t tab_entries, uint32_t* tabs, uint32_t blk_lo, uint32_t blk_cnt);
 hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_work,
@@ -238,8 +242,7 @@ hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplat
 // rows [row0, row0 + nrows) of every dictionary column (row0, nrows multiples of 4096 or the whole trace)
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev,
-                              hipEvent_t ev_side = nullptr, int side_at = 2);
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev);
 hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);

@@ -156,7 +156,10 @@ __global__ void __launch_bounds__(TR_THREADS) k_trace_image8(const int8_t* __res
 // ------------------------------------------------------------ expansion
 // One workgroup per block: row -> block id, first/last flags, and the
 // post-move head prefix sums per tape (head starts at 0 in every block).
-__global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) {
+// The head columns are stored as i32 (the reference keeps i64 heads,
+// air.rs:54): a block whose head leaves the i32 range (more than ~2^24 rows of
+// large moves) sets the guard word to GUARD_HEAD_RANGE and the proof fails.
+__global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0, uint32_t* __restrict__ err) {
   const uint32_t b = b0 + blockIdx.x;
   const uint64_t s = T.blk_start[b], e = T.blk_start[b + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -217,6 +220,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_expand(TraceDev T, uint32_t b0) 
     if (lane == 0) {
       T.head_rng[2 * ((uint64_t)tp * T.nblk + b)] = lo;
       T.head_rng[2 * ((uint64_t)tp * T.nblk + b) + 1] = hi;
+      if (lo < (int64_t)INT32_MIN || hi > (int64_t)INT32_MAX) atomicOr(err, GUARD_HEAD_RANGE);
     }
   }
 }
@@ -1341,15 +1345,13 @@ __device__ __forceinline__ void reduce_parts(const int64_t* pp, uint32_t nparts,
   __syncthreads();
 }
 
-// SEZKP_DICT_MISS_PEN=<q8> (A/B): gather-miss price of the table planner
-constexpr uint64_t DICT_PEN_ENTRIES = 32768;
-static uint32_t dict_miss_pen() {
-  static const uint32_t v = getenv("SEZKP_DICT_MISS_PEN") ? (uint32_t)atoi(getenv("SEZKP_DICT_MISS_PEN")) : 0;
-  return v;
-}
+// Table level K by cost: table entries + n / 2^K gathered nodes (one hash
+// each). Pricing gathers from tables of > 1 MB higher (they miss the reading
+// XCD's L2) was measured slower in round 3: the extra compressions of the
+// lower levels cost more than the misses save.
 __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restrict__ part, uint32_t nparts,
                                                           uint64_t n, const DictCol* __restrict__ dcols,
-                                                          DictPlan* __restrict__ plans, uint32_t pen_q8) {
+                                                          DictPlan* __restrict__ plans) {
   __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
   const int tid = threadIdx.x;
   int64_t lo, hi, mlo = 0, mhi = -1;
@@ -1373,9 +1375,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restr
       if (open) {
         P.pw[k] = (uint32_t)sz;
         tabcost += sz;
-        // pen_q8 / 256: extra cost of a gather from a table of > DICT_PEN_ENTRIES
-        // entries (1 MB: it misses the reading XCD's L2) relative to a hash
-        const uint64_t cost = tabcost + (((n >> k) * (256 + (sz > DICT_PEN_ENTRIES ? pen_q8 : 0))) >> 8);
+        const uint64_t cost = tabcost + (n >> k);
         if (cost < best) { best = cost; P.K = k; }
         sz = sz * sz;
       }
@@ -1480,21 +1480,16 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __
   }
 }
 
-template <bool PF, int D, class Prov>
-__device__ __forceinline__ void lane_tree_sel(const Prov& P, uint32_t (&h)[8]) {
-  if constexpr (PF) lane_tree_pf<D>(P, h);
-  else lane_tree<D>(P, h);
-}
-template <typename Key, bool PF>
+template <typename Key>
 __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const uint32_t* tab,
                                           const ColTemplate* ct, uint32_t (&h)[8]) {
   // a lane covers 2^(6 + dict_extra(K)) rows: 2^(6+a-K) table nodes
   switch (P.K) {
-    case 0: lane_tree_sel<PF, 6>(DictNodes<Key, 0>{p, tab, P.min, P.R}, h); break;
-    case 1: lane_tree_sel<PF, 5>(DictNodes<Key, 1>{p, tab + 8 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 2: lane_tree_sel<PF, 5>(DictNodes<Key, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 3: lane_tree_sel<PF, 5>(DictNodes<Key, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 4: lane_tree_sel<PF, 4>(DictNodes<Key, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 0: lane_tree_pf<6>(DictNodes<Key, 0>{p, tab, P.min, P.R}, h); break;
+    case 1: lane_tree_pf<5>(DictNodes<Key, 1>{p, tab + 8 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 2: lane_tree_pf<5>(DictNodes<Key, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 3: lane_tree_pf<5>(DictNodes<Key, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+    case 4: lane_tree_pf<4>(DictNodes<Key, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
     default: lane_tree<6>(RawLeaves<Key>{p, ct}, h); break;
   }
 }
@@ -1502,29 +1497,16 @@ __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const
 // 64-lane WG = 4096 rows of one dictionary column (4 chunks): each lane folds
 // 64 rows to a level-6 node, 4 LDS levels give the 4 chunk roots, written as
 // leaves of the column's outer tree. Requires n >= 1024 (n % 64 == 0).
-template <bool PF>
 __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                         const DictCol* __restrict__ dcols,
                                                         const DictPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ tabs, uint32_t* __restrict__ outer,
                                                         uint64_t outer_stride, uint64_t row0, uint64_t row_end,
-                                                        uint32_t* __restrict__ dlev, uint32_t ndict, uint32_t xcd_gx) {
+                                                        uint32_t* __restrict__ dlev) {
   __shared__ uint32_t lds[8][64];
-  // xcd_gx != 0: XCD-interleaved order. Workgroup b runs on XCD b mod 8; XCD
-  // x takes the columns c = x, x + 8, x + 16, ... one after the other (gx =
-  // xcd_gx row blocks each), so the ~512 workgroups one XCD holds at a time
-  // gather from one column's tables (<= 2 MB: they stay in that XCD's 4 MB
-  // L2) instead of eight columns' (16 MB). Columns of one kind are tau
-  // consecutive indices, so every XCD gets about the same mix of table
-  // levels (a contiguous range per XCD measured 347 -> 580 us, round 1: the
-  // XCDs holding the wsym / head columns did 4x the work of the others).
-  uint32_t by = blockIdx.y, bx = blockIdx.x;
-  if (xcd_gx) {
-    const uint32_t b = blockIdx.x, x = b & 7, k = b >> 3;
-    by = x + 8 * (k / xcd_gx);
-    bx = k % xcd_gx;
-    if (by >= ndict) return;
-  }
+  // (XCD-interleaved column orders, so that one XCD's workgroups gather
+  // from one column's tables at a time, measured slower in rounds 1 and 3)
+  const uint32_t by = blockIdx.y, bx = blockIdx.x;
   const DictCol dc = dcols[by];
   const ColTemplate* ctp = tmpl + dc.col;
   const ColTemplate ct = *ctp;
@@ -1542,17 +1524,17 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
   if (lrow < row_end) {
     uint32_t h[8];
     switch (ct.kind) {
-      case 0: case 3: dict_lane<int8_t, PF>(dict_keys<int8_t>(T, ct) + lrow, P, tab, ctp, h); break;
-      case 4: dict_lane<uint8_t, PF>(dict_keys<uint8_t>(T, ct) + lrow, P, tab, ctp, h); break;
-      case 5: dict_lane<uint16_t, PF>(dict_keys<uint16_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      case 0: case 3: dict_lane<int8_t>(dict_keys<int8_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      case 4: dict_lane<uint8_t>(dict_keys<uint8_t>(T, ct) + lrow, P, tab, ctp, h); break;
+      case 5: dict_lane<uint16_t>(dict_keys<uint16_t>(T, ct) + lrow, P, tab, ctp, h); break;
       default:
         if (P.delta) {
           const uint64_t o = (uint64_t)ct.tape * T.n + lrow;
-          lane_tree_sel<PF, 5>(DeltaNodes{T.head + o, T.mv + o, T.row_flags + lrow, tab + 8 * (uint64_t)DICT_CAP,
+          lane_tree_pf<5>(DeltaNodes{T.head + o, T.mv + o, T.row_flags + lrow, tab + 8 * (uint64_t)DICT_CAP,
                                   tab + 16 * (uint64_t)DICT_CAP, P.min, P.dmin, P.R, P.dR},
                        h);
         } else {
-          dict_lane<int32_t, PF>(dict_keys<int32_t>(T, ct) + lrow, P, tab, ctp, h);
+          dict_lane<int32_t>(dict_keys<int32_t>(T, ct) + lrow, P, tab, ctp, h);
         }
         break;
     }
@@ -1602,9 +1584,7 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
 hipError_t launch_trace_image(hipStream_t st, const int8_t* raw_mv, const uint8_t* raw_hw, const uint16_t* raw_ws,
                               uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws) {
   if (n == 0 || tau <= 0) return hipSuccess;
-  // SEZKP_TRACE_IMAGE_BYTES=1: the byte-wise kernel for tau = 8 too (A/B)
-  static const bool bytes = getenv("SEZKP_TRACE_IMAGE_BYTES") && atoi(getenv("SEZKP_TRACE_IMAGE_BYTES")) != 0;
-  if (tau == 8 && !bytes) {
+  if (tau == 8) {
     const uint64_t g8 = ((n + 7) / 8 + TR_THREADS - 1) / TR_THREADS;
     if (g8 > 0x7FFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_trace_image8, dim3((unsigned)g8), dim3(TR_THREADS), 0, st, raw_mv, raw_hw, raw_ws, n, mv, wf,
@@ -1617,10 +1597,10 @@ hipError_t launch_trace_image(hipStream_t st, const int8_t* raw_mv, const uint8_
                      wf, ws);
   return hipGetLastError();
 }
-hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt) {
+hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt, uint32_t* d_err) {
   if (blk_cnt == 0) return hipSuccess;
   if ((uint64_t)blk_lo + blk_cnt > T.nblk) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_expand, dim3(blk_cnt), dim3(TR_THREADS), 0, st, T, blk_lo);
+  hipLaunchKernelGGL(k_expand, dim3(blk_cnt), dim3(TR_THREADS), 0, st, T, blk_lo, d_err);
   return hipGetLastError();
 }
 hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_tab_cols,
@@ -1634,14 +1614,8 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
 }
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev,
-                              hipEvent_t ev_side, int side_at) {
-  // ev_side (optional) is recorded after the plan (side_at = 1) or after the
-  // table levels (side_at = 2): the caller starts its side-stream work there
-  if (ndict == 0) {
-    if (ev_side) return hipEventRecord(ev_side, st);
-    return hipSuccess;
-  }
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev) {
+  if (ndict == 0) return hipSuccess;
   if (T.n < (1ULL << COL_CHUNK_LOG2)) return hipErrorInvalidValue;
   if (row0 + nrows > T.n || (nrows != T.n && (row0 % DICT_WG_ROWS || nrows % DICT_WG_ROWS))) return hipErrorInvalidValue;
   const uint32_t nparts = (uint32_t)((nrows + DICT_RANGE_ROWS - 1) / DICT_RANGE_ROWS);
@@ -1649,10 +1623,8 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
                      row0, row0 + nrows);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_dcols, d_plans,
-                     dict_miss_pen());
+  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_dcols, d_plans);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (ev_side && side_at == 1 && (e = hipEventRecord(ev_side, st)) != hipSuccess) return e;
   for (int l = 0; l < DICT_LEVELS; l++) {
     // one flat launch per level (and per DICT_FLAT_MAX columns): all WGs
     // share every column's entries
@@ -1663,23 +1635,9 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
   }
-  if (ev_side && side_at == 2 && (e = hipEventRecord(ev_side, st)) != hipSuccess) return e;
   const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
-  // measured slower (round 3, single-proof k_col_commit_dict 335 -> 355 us,
-  // tools/ab_dict_xcd.sh): off by default, SEZKP_DICT_XCD=1 for A/B
-  static const bool xcd = getenv("SEZKP_DICT_XCD") && atoi(getenv("SEZKP_DICT_XCD")) != 0;
-  // SEZKP_DICT_PF=0: the rolled lane_tree without gather prefetch (A/B)
-  static const bool pf = !(getenv("SEZKP_DICT_PF") && atoi(getenv("SEZKP_DICT_PF")) == 0);
-  const auto kern = pf ? k_col_commit_dict<true> : k_col_commit_dict<false>;
-  if (xcd && ndict > 8) {
-    const uint64_t per_xcd = (uint64_t)((ndict + 7) / 8) * gx;  // work items of the busiest XCD
-    hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per_xcd)), dim3(64), 0, st, T, d_tmpl, d_dcols,
-                       d_plans, d_dtabs, outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev,
-                       (uint32_t)ndict, gx);
-  } else {
-    hipLaunchKernelGGL(kern, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
-                       outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev, (uint32_t)ndict, 0u);
-  }
+  hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
+                     outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev);
   return hipGetLastError();
 }
 
@@ -1702,18 +1660,15 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
 hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
                           const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows) {
   if (row0 + nrows > T.n) return hipErrorInvalidValue;
-  const char* rw_s = getenv("SEZKP_COMPOSE_ROWS");  // read per launch: tests switch it
-  const int rw_env = rw_s ? atoi(rw_s) : 2;
-  for (int rw : {4, 2}) {  // SEZKP_COMPOSE_ROWS caps the rows per lane (A/B)
-    if (rw > rw_env || T.n < (uint64_t)rw || (row0 | nrows) % rw) continue;
-    const unsigned g = (unsigned)((nrows / rw + TR_THREADS - 1) / TR_THREADS);
+  // two adjacent rows per lane (4 measured even in round 2); the one-row
+  // kernel for n = 1 and odd row ranges. SEZKP_COMPOSE_ROWS=1 forces the
+  // one-row kernel (read per launch: the parity test switches it).
+  const char* rw_s = getenv("SEZKP_COMPOSE_ROWS");
+  if (!(rw_s && atoi(rw_s) == 1) && T.n >= 2 && (row0 | nrows) % 2 == 0) {
+    const unsigned g = (unsigned)((nrows / 2 + TR_THREADS - 1) / TR_THREADS);
     if (g == 0) return hipSuccess;
-    if (rw == 4)
-      hipLaunchKernelGGL(k_compose_rows<4>, dim3(g), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3],
-                         tw, logn, out, row0, row0 + nrows);
-    else
-      hipLaunchKernelGGL(k_compose_rows<2>, dim3(g), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3],
-                         tw, logn, out, row0, row0 + nrows);
+    hipLaunchKernelGGL(k_compose_rows<2>, dim3(g), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3],
+                       tw, logn, out, row0, row0 + nrows);
     return hipGetLastError();
   }
   const unsigned grid = (unsigned)((nrows + TR_THREADS - 1) / TR_THREADS);

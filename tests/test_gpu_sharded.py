@@ -321,3 +321,94 @@ def test_sharded_rccl_abort_after_failure(gpu_ok, product):
     assert "injected failure before collective lde_alltoall on rank 0" in lines[0], lines
     assert "context unusable" in lines[1], lines
     assert lines[2] == "closed"
+
+
+def _stall_worker(rank, world, port, q):
+    """Rank 1's stream is held after the proof's last collective (test hook):
+    its wait must give up at SEZKP_COLL_TIMEOUT_S through the transport-
+    agnostic deadline of Comm::wait, and destroy must not hang."""
+    import datetime
+    import time
+    sys.path[:0] = [PKG, ORACLE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      SEZKP_DEBUG_STALL_AFTER="1:proof_allreduce", SEZKP_COLL_TIMEOUT_S="3")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=20))
+    res = [rank]
+    try:
+        import sezkp_amd
+        blocks = sezkp_amd.synthetic_blocks(1 << 13, 512, 2, 42)
+        ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
+        ctx.upload(blocks)
+        t0 = time.monotonic()
+        try:
+            ctx.prove(blocks.manifest_root())
+            res += ["no error", time.monotonic() - t0]
+        except Exception as e:
+            res += [str(e), time.monotonic() - t0]
+        if rank == 1:
+            try:
+                ctx.prove(blocks.manifest_root())
+                res.append("no error")
+            except Exception as e:
+                res.append(str(e))
+        else:
+            res.append("")
+        t1 = time.monotonic()
+        ctx.close()
+        res.append(time.monotonic() - t1)
+    except Exception as e:
+        res += [f"setup: {e}", 0.0, "", 0.0]
+    q.put(tuple(res))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+def test_sharded_stalled_stream_hits_the_deadline(gpu_ok):
+    """the collective deadline (poll + timeout + abort) used to
+    live in the RCCL transport only and never ran with a stuck peer. Rank 1's
+    stream now stalls after its last collective: rank 1 returns the timeout
+    error within the 3 s deadline (+ margin), refuses later proofs, and its
+    context is destroyed without hanging; rank 0 is unaffected."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_stall_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=150) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert res[0][1] == "no error", res[0]
+    assert "collective timeout" in res[1][1] and 2.5 < res[1][2] < 20, res[1]
+    assert "context unusable" in res[1][3], res[1]
+    assert res[1][4] < 20, res[1]
+
+
+def test_sharded_rccl_stalled_stream_aborts(gpu_ok):
+    """The same deadline on a one-rank RCCL communicator: the wait times out,
+    the communicator is aborted (ncclCommAbort), the stalled stream is released
+    at destroy, and destroy returns (in a child: the switches are read once)."""
+    import subprocess
+    code = ("import sys, time; sys.path[:0]=[%r]\n"
+            "import sezkp_amd as S\n"
+            "bl=S.synthetic_blocks(1<<12,512,2,3); c=S.ShardedProverContext(0,1,device=0,comm='rccl'); c.upload(bl)\n"
+            "t0=time.monotonic()\n"
+            "try:\n"
+            "    c.prove(bl.manifest_root()); print('no error')\n"
+            "except Exception as e:\n"
+            "    print('ERR', e)\n"
+            "print('T %%.2f' %% (time.monotonic()-t0))\n"
+            "c.close(); print('closed')\n" % PKG)
+    env = dict(os.environ, SEZKP_FORCE_SHARDED="1", SEZKP_DEBUG_STALL_AFTER="0:proof_allreduce",
+               SEZKP_COLL_TIMEOUT_S="3")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-1500:]
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith(("ERR", "no error", "closed", "T "))]
+    assert "collective timeout" in lines[0], lines
+    assert 2.5 < float(lines[1].split()[1]) < 20, lines
+    assert lines[2] == "closed", lines
