@@ -286,6 +286,18 @@ int32_t sezkp_manifest_decode(const uint8_t* data, size_t len, int32_t is_json, 
 /* BLAKE3 hash with extendable output (host). */
 void sezkp_blake3(const uint8_t* data, size_t len, uint8_t* out, size_t out_len);
 
+/* Fiat-Shamir transcript challenges on the device (replaces the host side of
+ * Blake3Transcript::challenge_bytes, crates/sezkp-crypto/src/lib.rs:102-123,
+ * for a batch): out_i = BLAKE3-XOF(stream[0..pos[i]) || suffix_i, out_len[i])
+ * with suffix_i the next sfx_len[i] bytes of `suffixes` (a transcript passes
+ * "challenge" || u32 LE len || label). Outputs are concatenated in `out`
+ * (sum of out_len bytes). The prover runs the same kernel with the stream
+ * template of its schedule; this entry point is its known-answer interface.
+ * Limits: stream_len + the suffix bytes <= 40960, nchal <= 16, every
+ * out_len a multiple of 8. Host buffers; synchronous on `stream`. */
+int32_t sezkp_fs_xof(const uint8_t* stream_bytes, size_t stream_len, const uint32_t* pos, const uint8_t* suffixes,
+                     const uint32_t* sfx_len, const uint32_t* out_len, uint32_t nchal, uint8_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -142,8 +142,10 @@ __global__ void __launch_bounds__(MK_THREADS) k_deep(uint64_t* __restrict__ y, i
 // fold == 0: leaves are in[i];  fold == 1: leaves y'_i = in[i] + beta*in[i+len],
 // written to out (the next FRI layer). One WG = 1024 leaves (or the whole layer).
 __global__ void __launch_bounds__(MK_THREADS) k_leaf_subtree(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
-                                                             int logLen, int fold, uint64_t beta, TreeDev T) {
+                                                             int logLen, int fold, uint64_t beta,
+                                                             const uint64_t* __restrict__ dbeta, TreeDev T) {
   __shared__ uint32_t lds[8][MK_THREADS];
+  if (dbeta) beta = *dbeta;
   const int tid = threadIdx.x;
   const uint64_t len = 1ULL << logLen;
   const uint64_t wg = blockIdx.x;
@@ -325,15 +327,18 @@ __device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint
 }
 
 __global__ void __launch_bounds__(MK_THREADS) k_layer16(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
-                                                        int logLen, int fold, uint64_t beta, TreeDev T, int stop) {
+                                                        int logLen, int fold, uint64_t beta,
+                                                        const uint64_t* __restrict__ dbeta, TreeDev T, int stop) {
   __shared__ uint32_t lds[8][MK_THREADS];
+  if (dbeta) beta = *dbeta;
   layer16_wg(in, out, logLen, fold, beta, T, blockIdx.x, lds, stop);
 }
 
 // FRI fold y'_i = y_i + beta * y_{i+len} (prover.rs:200-239), 4 per lane.
 __global__ void __launch_bounds__(MK_THREADS) k_fold(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
-                                                     int logLen, uint64_t beta) {
+                                                     int logLen, uint64_t beta, const uint64_t* __restrict__ dbeta) {
   const uint64_t len = 1ULL << logLen;
+  if (dbeta) beta = *dbeta;
   const uint64_t i = ((uint64_t)blockIdx.x * MK_THREADS + threadIdx.x) * 4;
   if (i >= len) return;
   const ulonglong2* p = reinterpret_cast<const ulonglong2*>(in + i);
@@ -572,9 +577,10 @@ __global__ void __launch_bounds__(256) k_runroots_scatter(const uint32_t* __rest
 // One 64-lane workgroup per (layer, index): recompute the 64-leaf group that
 // holds the index (levels < lstore), then read stored siblings above.
 __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict__ layers, const uint32_t* __restrict__ req,
-                                                  ProofLayout P) {
+                                                  const uint32_t* __restrict__ count, ProofLayout P) {
   __shared__ uint32_t lds[8][64];
   const int lane = threadIdx.x;
+  if (count && blockIdx.x >= *count) return;  // grid sized for the most requests a rank can own
   const uint32_t r = req[3 * blockIdx.x];
   const uint64_t idx = req[3 * blockIdx.x + 1];
   const uint32_t ord = req[3 * blockIdx.x + 2];  // q*2k + 2r + side
@@ -678,16 +684,17 @@ hipError_t launch_runroots_scatter(hipStream_t st, const uint32_t* gathered, Tre
 }
 
 hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold,
-                               uint64_t beta, TreeDev tree) {
+                               uint64_t beta, TreeDev tree, const uint64_t* dbeta) {
   if (logLen >= L16_LOG) {
-    hipError_t e = launch_layer16(st, in, out_vals, logLen, fold, beta, tree);
+    hipError_t e = launch_layer16(st, in, out_vals, logLen, fold, beta, tree, L16_LOG, dbeta);
     if (e != hipSuccess) return e;
     if (logLen == L16_LOG) return hipSuccess;  // the single WG wrote the root
     return launch_tree_upper(st, &tree, 1, 0, 0, L16_LOG);
   }
   const int sub_log = logLen < 10 ? logLen : 10;
   const unsigned grid = (unsigned)(1ULL << (logLen - sub_log));
-  hipLaunchKernelGGL(k_leaf_subtree, dim3(grid), dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, tree);
+  hipLaunchKernelGGL(k_leaf_subtree, dim3(grid), dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, dbeta,
+                     tree);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   int from = sub_log;
@@ -704,18 +711,19 @@ hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out
 }
 
 hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
-                          TreeDev tree, int stop) {
+                          TreeDev tree, int stop, const uint64_t* dbeta) {
   if (logLen < L16_LOG || stop < tree.lstore || stop > L16_LOG) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_layer16, dim3((unsigned)(1ULL << (logLen - L16_LOG))), dim3(MK_THREADS), 0, st, in, out_vals,
-                     logLen, fold, beta, tree, stop);
+                     logLen, fold, beta, dbeta, tree, stop);
   return hipGetLastError();
 }
 
-hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta) {
+hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta,
+                       const uint64_t* dbeta) {
   if (logLen < 2) return hipErrorInvalidValue;
   const uint64_t per = (uint64_t)MK_THREADS * 4;
   const unsigned grid = (unsigned)(((1ULL << logLen) + per - 1) / per);
-  hipLaunchKernelGGL(k_fold, dim3(grid), dim3(MK_THREADS), 0, st, in, out, logLen, beta);
+  hipLaunchKernelGGL(k_fold, dim3(grid), dim3(MK_THREADS), 0, st, in, out, logLen, beta, dbeta);
   return hipGetLastError();
 }
 
@@ -788,10 +796,10 @@ hipError_t launch_tree_upper(hipStream_t st, TreeDev* trees, int ntrees, uint64_
 }
 
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
-                            const ProofLayout& P) {
+                            const ProofLayout& P, const uint32_t* d_count) {
   if (nreq == 0) return hipSuccess;
   if ((uint64_t)nreq > (uint64_t)P.nq * 2 * P.k) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_fri_paths, dim3(nreq), dim3(64), 0, st, d_layers, d_req, P);
+  hipLaunchKernelGGL(k_fri_paths, dim3(nreq), dim3(64), 0, st, d_layers, d_req, d_count, P);
   return hipGetLastError();
 }
 

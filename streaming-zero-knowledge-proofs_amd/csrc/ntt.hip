@@ -983,8 +983,10 @@ __global__ void __launch_bounds__(256) k_bintt_dft_twiddle(uint64_t* __restrict_
 // allgather their partials, so every rank reduces the same sum).
 constexpr int DQ_PER = 16;
 __global__ void __launch_bounds__(NTT_THREADS) k_inv_base(const uint64_t* __restrict__ C, uint64_t* __restrict__ inv,
-                                                          uint64_t* __restrict__ partial, int logn, uint64_t z,
-                                                          NttTables T, uint64_t row0, uint64_t nrows) {
+                                                          uint64_t* __restrict__ partial, int logn,
+                                                          const DevChal* __restrict__ ch, NttTables T, uint64_t row0,
+                                                          uint64_t nrows) {
+  const uint64_t z = ch->z;
   __shared__ uint64_t wtot[NTT_THREADS / 64];
   __shared__ uint64_t s_inv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1100,9 +1102,10 @@ hipError_t launch_scale_pow_bitrev(hipStream_t st, uint64_t* a, int logn, uint64
 // rlo[t] = r^t, rhi[t] = c' r^(4096 t).
 __global__ void __launch_bounds__(NTT_THREADS) k_q_tables(uint64_t* __restrict__ C, const uint64_t* __restrict__ inv,
                                                           const uint64_t* __restrict__ partial, uint32_t nparts,
-                                                          uint64_t row0, uint64_t nrows, uint64_t K1, uint64_t K2,
-                                                          uint64_t r, uint64_t r4096, uint64_t* __restrict__ rlo,
+                                                          uint64_t row0, uint64_t nrows,
+                                                          const DevChal* __restrict__ ch, uint64_t* __restrict__ rlo,
                                                           uint64_t* __restrict__ rhi, uint32_t nhi) {
+  const uint64_t K1 = ch->K1, K2 = ch->K2, r = ch->rho, r4096 = ch->rho4096;
   __shared__ uint64_t wsum[NTT_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint64_t acc = 0;
@@ -1122,17 +1125,16 @@ __global__ void __launch_bounds__(NTT_THREADS) k_q_tables(uint64_t* __restrict__
 }
 
 hipError_t launch_inv_base(hipStream_t st, const uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
-                           uint64_t z, const NttTables& T, uint64_t row0, uint64_t nrows) {
+                           const DevChal* ch, const NttTables& T, uint64_t row0, uint64_t nrows) {
   const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
   if (logn < 4 || nrows % DQ_PER || row0 % per || row0 + nrows > (1ULL << logn)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_inv_base, dim3((unsigned)((nrows + per - 1) / per)), dim3(NTT_THREADS), 0, st, C, inv_scratch,
-                     partial + row0 / per, logn, z, T, row0, nrows);
+                     partial + row0 / per, logn, ch, T, row0, nrows);
   return hipGetLastError();
 }
 
 hipError_t launch_q_tables(hipStream_t st, uint64_t* C, const uint64_t* inv_scratch, const uint64_t* partial, int logn,
-                           int logN, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096, uint64_t* rlo, uint64_t* rhi,
-                           uint64_t row0, uint64_t nrows) {
+                           int logN, const DevChal* ch, uint64_t* rlo, uint64_t* rhi, uint64_t row0, uint64_t nrows) {
   if (logn < 4 || logN < logn || logN > 32) return hipErrorInvalidValue;
   const uint64_t n = 1ULL << logn;
   const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
@@ -1140,19 +1142,18 @@ hipError_t launch_q_tables(hipStream_t st, uint64_t* C, const uint64_t* inv_scra
   const uint32_t nhi = logN > 12 ? (1u << (logN - 12)) : 1u;
   const uint64_t work = std::max<uint64_t>(nrows, std::max<uint64_t>(4096, nhi));
   const unsigned grid = (unsigned)std::min<uint64_t>(1024, (work + NTT_THREADS - 1) / NTT_THREADS);
-  hipLaunchKernelGGL(k_q_tables, dim3(grid), dim3(NTT_THREADS), 0, st, C, inv_scratch, partial, nparts, row0, nrows, K1,
-                     K2, r, r4096, rlo, rhi, nhi);
+  hipLaunchKernelGGL(k_q_tables, dim3(grid), dim3(NTT_THREADS), 0, st, C, inv_scratch, partial, nparts, row0, nrows, ch,
+                     rlo, rhi, nhi);
   return hipGetLastError();
 }
 
 hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
-                                int logN, uint64_t z, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096,
-                                uint64_t* rlo, uint64_t* rhi, const NttTables& T) {
+                                int logN, const DevChal* ch, uint64_t* rlo, uint64_t* rhi, const NttTables& T) {
   if (logn < 4 || logN < logn || logN > 32) return hipErrorInvalidValue;
   const uint64_t n = 1ULL << logn;
-  hipError_t e = launch_inv_base(st, C, inv_scratch, partial, logn, z, T, 0, n);
+  hipError_t e = launch_inv_base(st, C, inv_scratch, partial, logn, ch, T, 0, n);
   if (e != hipSuccess) return e;
-  return launch_q_tables(st, C, inv_scratch, partial, logn, logN, K1, K2, r, r4096, rlo, rhi, 0, n);
+  return launch_q_tables(st, C, inv_scratch, partial, logn, logN, ch, rlo, rhi, 0, n);
 }
 
 // ------------------------------------------------------------------ host side

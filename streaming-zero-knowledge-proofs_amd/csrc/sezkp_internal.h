@@ -9,6 +9,8 @@
 
 namespace sezkp {
 
+struct DevChal;  // transcript-derived values in device memory (below)
+
 // w_{2^K}^e = hi[e >> S] * lo[e & (2^S - 1)]; p3_* likewise for 3^e.
 struct NttTables {
   const uint64_t* hi;
@@ -67,18 +69,17 @@ struct DeepPoly {
   const uint64_t* rlo;  // 4096 entries: r^t
   const uint64_t* rhi;  // N >> 12 entries: c' r^(4096 t)
 };
+// z, K1 = (1 - z^n) / n, K2 = c' / f(z), r (rho) and r^4096 from ch (device memory)
 hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
-                                int logN, uint64_t z, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096,
-                                uint64_t* rlo, uint64_t* rhi, const NttTables& T);
+                                int logN, const DevChal* ch, uint64_t* rlo, uint64_t* rhi, const NttTables& T);
 // the two halves of launch_deep_quotient over a block of base rows [row0,
 // row0 + nrows) (row0 a multiple of 4096): inverses + this block's partial
 // sums (at partial[row0 / 4096 ...]), then q(w^j) of the block once every
 // partial of the n rows is in `partial` (sharded ranks allgather them between)
 hipError_t launch_inv_base(hipStream_t st, const uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
-                           uint64_t z, const NttTables& T, uint64_t row0, uint64_t nrows);
+                           const DevChal* ch, const NttTables& T, uint64_t row0, uint64_t nrows);
 hipError_t launch_q_tables(hipStream_t st, uint64_t* C, const uint64_t* inv_scratch, const uint64_t* partial, int logn,
-                           int logN, uint64_t K1, uint64_t K2, uint64_t r, uint64_t r4096, uint64_t* rlo, uint64_t* rhi,
-                           uint64_t row0, uint64_t nrows);
+                           int logN, const DevChal* ch, uint64_t* rlo, uint64_t* rhi, uint64_t row0, uint64_t nrows);
 
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
 // natural order in and out through `scratch` (n words): the first pass reads a
@@ -228,6 +229,73 @@ struct ProofLayout {
   uint32_t tau;
 };
 
+// ------------------------------------------------- Fiat-Shamir challenges
+// The transcript-derived values every challenge-dependent kernel reads from
+// device memory: written by the device transcript (transcript.hip) or, in the
+// host-transcript mode, copied from the host.
+constexpr int FS_NQ = 30;           // NUM_QUERIES (params.rs:31)
+constexpr int FS_MAX_BETAS = 64;
+struct DevChal {
+  uint64_t alpha[8];                // derive_alphas (params.rs:82-92); reuse of prover.rs:86-98 in the kernels
+  uint64_t mask[4];                 // derive_mask_coeffs (masking.rs:56-79)
+  uint64_t z, zn, K1, K2, rho, rho4096;  // OOD point (nudged) and the DEEP-polynomial constants
+  uint64_t beta[FS_MAX_BETAS];      // derive_betas_for_fri (params.rs:109-119)
+  uint64_t rows[FS_NQ], frows[FS_NQ];    // derive_queries mod n / mod N (prover.rs:248, 297)
+  uint32_t counts[2];               // FRI path / opening requests this rank owns
+  uint32_t pad[2];
+};
+
+// Device transcript (transcript.hip): the stream S (template from the host,
+// roots filled in on the device), the chaining values of its blocks and
+// chunks, and one workgroup per transcript point.
+constexpr int FS_S_MAX = 40960;     // stream + suffix bytes held in LDS
+constexpr int FS_MAX_CHAL = 16;     // challenges per point
+constexpr uint32_t FS_SRC_MROOT = 0, FS_SRC_COL = 1, FS_SRC_FRI = 0x10000;
+struct FsChal {
+  uint32_t pos;      // stream bytes before the challenge
+  uint32_t sfx_off;  // its suffix "challenge" || u32 len || label, at S[sfx_off ..)
+  uint32_t sfx_len;
+  uint32_t out_len;
+  uint32_t out_off;  // into the output bytes
+};
+struct FsFill {
+  uint32_t s_off;  // 32 root bytes at S[s_off ..)
+  uint32_t src;    // FS_SRC_MROOT, FS_SRC_COL + column, FS_SRC_FRI + layer
+};
+struct FsQueryArgs {  // point 3: requests and proof-body fields
+  ProofLayout PL;
+  uint32_t* req;          // FRI requests (3 words) then opening requests at 3 * max_fri_req
+  uint64_t max_fri_req;
+  const uint32_t* dict_of;
+  const uint64_t* final_val;  // the last FRI layer
+  uint64_t ch_lo, ch_hi;
+  uint32_t tau, sharded, world, rank;
+  int rR;
+};
+struct FsArgs {
+  const uint8_t* S;
+  uint32_t s_bytes;        // template bytes (stream + suffix area)
+  uint32_t B0, B1;         // stream blocks this point chains
+  uint32_t* cvs;           // chaining value in front of block b (8 words each)
+  uint32_t* ccv;           // chunk chaining values
+  const FsFill* fills;
+  uint32_t nfill;
+  const FsChal* chal;
+  uint32_t nchal;
+  uint8_t* out;
+  uint32_t mroot[8];
+  const uint32_t* colroots;
+  const uint32_t* friroots;
+  int point;               // 0 raw outputs (KAT), 1 alphas/masks/z, 2 betas, 3 queries
+  DevChal* ch;
+  uint32_t* status;        // [1] <- 1: z off the DEEP-polynomial domain (host re-proves)
+  uint32_t out_alpha, out_beta, out_rowq;
+  int logn, logN, logP;
+  uint64_t inv3, threeN, inv_n, w_rank;
+  FsQueryArgs q;
+};
+hipError_t launch_fs_point(hipStream_t st, const FsArgs& a);
+
 // kernels launched by the host orchestrator (prover.cpp)
 // blocks [blk_lo, blk_lo + blk_cnt) only (a sharded rank's rows + one row of halo)
 // row-major step arrays [n][tau] -> tape-major trace image [tau][n]
@@ -247,8 +315,9 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);
 // rows [row0, row0 + nrows) (nrows = n for the whole trace)
-hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
-                          const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows);
+// alphas and mask coefficients from ch (device memory)
+hipError_t launch_compose(hipStream_t st, const TraceDev& T, const DevChal* ch, const NttTables& tw, int logn,
+                          uint64_t* out, uint64_t row0, uint64_t nrows);
 // DEEP divide of y[j] at x = shift * w_{2^logN}^(g + (j << logP)) (logP = 0, g = 0: natural layout)
 hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw, int logP = 0,
                        uint32_t g = 0, uint64_t shift = 3);
@@ -275,8 +344,9 @@ hipError_t launch_cyc_unpack(hipStream_t st, const uint64_t* recv, uint64_t* loc
 // gathered[d][k1] (run roots of rank d) -> level-12 node k1*P + d of `cap`
 hipError_t launch_runroots_scatter(hipStream_t st, const uint32_t* gathered, TreeDev cap, uint64_t nrun_per_rank,
                                    int logP);
+// dbeta != null: the fold challenge is read from device memory instead of `beta`
 hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold,
-                               uint64_t beta, TreeDev tree);
+                               uint64_t beta, TreeDev tree, const uint64_t* dbeta = nullptr);
 hipError_t launch_tree_upper(hipStream_t st, TreeDev* trees, int ntrees_same_shape, uint64_t tree_stride_nodes,
                              uint64_t root_stride_words, int from_level);
 // A FRI layer as seen by the path kernel. Unsharded: vals/tree hold the
@@ -305,14 +375,15 @@ constexpr int L16_LOG = 12;  // leaves per WG of the 16-leaves-per-lane layer ke
 // stop: highest level the WG reduces to (L16_LOG = its run root; LSTORE_FRI
 // leaves levels 7..12 to the upper jobs, whose lanes are all busy)
 hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
-                          TreeDev tree, int stop = L16_LOG);
+                          TreeDev tree, int stop = L16_LOG, const uint64_t* dbeta = nullptr);
 // Fold chain kernel (values only) and the one-launch forest of layer trees.
-hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta);
+hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta,
+                       const uint64_t* dbeta = nullptr);
 // F = 2..FOLD_MAX folds in one pass (k_foldm): out[m-1] = layer r + m, beta[m-1] its challenge
 constexpr int FOLD_MAX = 4;
 struct FoldOuts {
   uint64_t* out[FOLD_MAX];
-  uint64_t beta[FOLD_MAX];
+  const uint64_t* beta;  // device: beta[m - 1] folds layer r + m - 1 (the pass's first challenge)
 };
 hipError_t launch_foldm(hipStream_t st, const uint64_t* in, const FoldOuts& outs, int F, int logLenF);
 struct ForestLayer {
@@ -328,7 +399,7 @@ constexpr int TAIL_MAX = 12;
 struct TailArgs {
   const uint64_t* src;
   int Ls;
-  uint64_t beta[TAIL_MAX];
+  const uint64_t* beta;  // device: beta[j] folds into layer Ls - j
   uint64_t* vals[TAIL_MAX];
   TreeDev tree[TAIL_MAX];
 };
@@ -338,12 +409,14 @@ hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a);
 hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs,
                            const TailArgs* tail = nullptr, uint64_t* tailbuf = nullptr, uint32_t wg_base = 0);
 // requests: (layer, index, ordinal in the proof's FRI records) triples
+// d_count != null: the number of requests is read on the device (grid = nreq, the most possible)
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
-                            const ProofLayout& P);
+                            const ProofLayout& P, const uint32_t* d_count = nullptr);
 // requests: OPEN_REQ_WORDS words each
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
                            const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev,
-                           const DictPlan* d_plans, const uint32_t* d_dtabs, const DictCol* d_dcols);
+                           const DictPlan* d_plans, const uint32_t* d_dtabs, const DictCol* d_dcols,
+                           const uint32_t* d_count = nullptr);
 
 }  // namespace sezkp

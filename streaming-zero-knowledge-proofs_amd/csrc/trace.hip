@@ -559,10 +559,18 @@ __global__ void __launch_bounds__(PW_THREADS) k_col_commit_pw(TraceDev T, const 
 // construction, bit columns are boolean): every alpha*flag*(flag-1) and
 // alpha*flg*sum(b(b-1)) term is identically zero and is skipped; the bit
 // reconstructions equal x & 0xFFFF / x & 0xF of the canonical value.
-__global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, uint64_t m0, uint64_t m1, uint64_t m2,
-                                                        uint64_t m3, NttTables tw, int logn, uint64_t* __restrict__ out,
-                                                        uint64_t row0, uint64_t row_end) {
+// the alphas with the reuse of prover.rs:86-98 and the mask coefficients,
+// from the transcript's device record
+__device__ __forceinline__ Alphas alphas_of(const DevChal* ch) {
+  const uint64_t* a = ch->alpha;
+  return Alphas{a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[0], a[2], a[2]};
+}
+__global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, const DevChal* __restrict__ ch, NttTables tw,
+                                                        int logn, uint64_t* __restrict__ out, uint64_t row0,
+                                                        uint64_t row_end) {
   const uint64_t n = T.n;
+  const Alphas A = alphas_of(ch);
+  const uint64_t m0 = ch->mask[0], m1 = ch->mask[1], m2 = ch->mask[2], m3 = ch->mask[3];
   // one row per lane: each load instruction covers 64 consecutive rows
   // (coalesced), row i+1 shares the neighbour's cache line; many rows in
   // flight per CU hide the dependent loads of the tape loop
@@ -639,10 +647,11 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, Alphas A, ui
 // group itself, and the outputs are 16-byte stores. Needs row0 and the row
 // count to be multiples of RW (n >= RW).
 template <int RW>
-__global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, Alphas A, uint64_t m0, uint64_t m1,
-                                                             uint64_t m2, uint64_t m3, NttTables tw, int logn,
-                                                             uint64_t* __restrict__ out, uint64_t row0,
+__global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, const DevChal* __restrict__ ch, NttTables tw,
+                                                             int logn, uint64_t* __restrict__ out, uint64_t row0,
                                                              uint64_t row_end) {
+  const Alphas A = alphas_of(ch);
+  const uint64_t m0 = ch->mask[0], m1 = ch->mask[1], m2 = ch->mask[2], m3 = ch->mask[3];
   static_assert(RW == 2 || RW == 4, "2 or 4 rows per lane");
   using Narrow = typename std::conditional<RW == 2, uint16_t, uint32_t>::type;  // RW bytes
   using Wide = typename std::conditional<RW == 2, uint32_t, uint64_t>::type;    // RW u16
@@ -1114,8 +1123,10 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
                                                          const uint32_t* __restrict__ dlev,
                                                          const DictPlan* __restrict__ plans,
                                                          const uint32_t* __restrict__ dtabs,
-                                                         const DictCol* __restrict__ dcols) {
+                                                         const DictCol* __restrict__ dcols,
+                                                         const uint32_t* __restrict__ count) {
   __shared__ uint32_t lds[8][1024];
+  if (count && blockIdx.x >= *count) return;  // grid sized for the most requests a rank can own
   const uint32_t* rq = req + OPEN_REQ_WORDS * (uint64_t)blockIdx.x;
   const int c = rq[0];
   const uint64_t row = (uint64_t)rq[1] | ((uint64_t)rq[2] << 32);
@@ -1657,7 +1668,7 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
                      T, d_tmpl, d_pw_cols, n_pw_cols, d_chunks, nchunks, tabs, outer_nodes, outer_stride_nodes, d_err);
   return hipGetLastError();
 }
-hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, const uint64_t mask[4],
+hipError_t launch_compose(hipStream_t st, const TraceDev& T, const DevChal* ch,
                           const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows) {
   if (row0 + nrows > T.n) return hipErrorInvalidValue;
   // two adjacent rows per lane (4 measured even in round 2); the one-row
@@ -1667,24 +1678,23 @@ hipError_t launch_compose(hipStream_t st, const TraceDev& T, const Alphas& a, co
   if (!(rw_s && atoi(rw_s) == 1) && T.n >= 2 && (row0 | nrows) % 2 == 0) {
     const unsigned g = (unsigned)((nrows / 2 + TR_THREADS - 1) / TR_THREADS);
     if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compose_rows<2>, dim3(g), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3],
-                       tw, logn, out, row0, row0 + nrows);
+    hipLaunchKernelGGL(k_compose_rows<2>, dim3(g), dim3(TR_THREADS), 0, st, T, ch, tw, logn, out, row0, row0 + nrows);
     return hipGetLastError();
   }
   const unsigned grid = (unsigned)((nrows + TR_THREADS - 1) / TR_THREADS);
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_compose, dim3(grid), dim3(TR_THREADS), 0, st, T, a, mask[0], mask[1], mask[2], mask[3], tw,
-                     logn, out, row0, row0 + nrows);
+  hipLaunchKernelGGL(k_compose, dim3(grid), dim3(TR_THREADS), 0, st, T, ch, tw, logn, out, row0, row0 + nrows);
   return hipGetLastError();
 }
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,
                            uint64_t outer_stride_nodes, int logChunks, const uint32_t* d_req, int nreq,
                            const ProofLayout& P, const uint32_t* tabs, const uint32_t* d_dlev,
-                           const DictPlan* d_plans, const uint32_t* d_dtabs, const DictCol* d_dcols) {
+                           const DictPlan* d_plans, const uint32_t* d_dtabs, const DictCol* d_dcols,
+                           const uint32_t* d_count) {
   if (nreq == 0) return hipSuccess;
   if ((uint64_t)nreq > (uint64_t)P.nq * P.open_per_q) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_col_open, dim3(nreq), dim3(TR_THREADS), 0, st, T, d_tmpl, outer_nodes, outer_stride_nodes,
-                     logChunks, d_req, P, tabs, d_dlev, d_plans, d_dtabs, d_dcols);
+                     logChunks, d_req, P, tabs, d_dlev, d_plans, d_dtabs, d_dcols, d_count);
   return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ EXPORTS = [
     "sezkp_ctx_prove_async", "sezkp_ctx_wait", "sezkp_ctx_stage", "sezkp_host_register", "sezkp_host_unregister",
     "sezkp_fri_fold", "sezkp_blake3_leaves_u64", "sezkp_blake3_leaves_labeled", "sezkp_merkle_node_count",
     "sezkp_merkle_build", "sezkp_merkle_paths", "sezkp_manifest_frontier_root", "sezkp_ctx_comm_stats",
+    "sezkp_fs_xof",
 ]
 
 
