@@ -92,6 +92,18 @@ typedef struct sezkp_ctx sezkp_ctx;
 sezkp_ctx* sezkp_ctx_create(int32_t device, char* err, size_t err_len);
 void sezkp_ctx_destroy(sezkp_ctx* ctx);
 int32_t sezkp_ctx_upload(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* err, size_t err_len);
+/* Upload from a view whose step arrays (input_mv, mv, has_write, wsym) hold
+ * only rows [row0, row0 + nrows) (index 0 = row row0; block metadata and
+ * step_start stay global): a sharded rank's slice of the trace, as the sliced
+ * JSONL ingest decodes it. The slice must contain every row the context reads
+ * (sezkp_shard_rows); one device needs the whole trace. */
+int32_t sezkp_ctx_upload_rows(sezkp_ctx* ctx, const sezkp_block_view* blocks, uint64_t row0, uint64_t nrows,
+                              char* err, size_t err_len);
+/* The rows [*row0, *row0 + *nrows) (whole blocks) that rank `rank` of a
+ * `world`-GPU sharded prove reads, from the global block boundaries
+ * (step_start[0..n_blocks], n = step_start[n_blocks] a power of two). */
+int32_t sezkp_shard_rows(const uint64_t* step_start, uint32_t n_blocks, int32_t rank, int32_t world, uint64_t* row0,
+                         uint64_t* nrows);
 int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, sezkp_buf* proof_bytes,
                         char* err, size_t err_len);
 /* Pipelined upload of the NEXT trace: same shape as the uploaded one (tau,
@@ -266,6 +278,23 @@ int32_t sezkp_blocks_decode_jsonl(const uint8_t* data, size_t len, sezkp_blocks*
 int32_t sezkp_blocks_encode_jsonl(const sezkp_block_view* blocks, sezkp_buf* out);
 const sezkp_block_view* sezkp_blocks_view(const sezkp_blocks* b);
 void sezkp_blocks_free(sezkp_blocks* b);
+/* Sliced ingest (a multi-GPU launcher's rank reads its part of one file):
+ * the metadata of the JSONL lines that start in bytes [lo, hi) (cut just past
+ * the first newline at or after lo and hi; 0 and len map to themselves, so
+ * ranges [len g/P, len (g+1)/P) cover each line exactly once). Every field
+ * and each block's step count (step_start) are decoded, the steps are not:
+ * the view's step arrays are empty. Line byte offsets via
+ * sezkp_blocks_line_offsets, to fully decode a run of lines later with
+ * sezkp_blocks_decode_jsonl on data + off[a] .. data + off[b]. */
+int32_t sezkp_blocks_decode_jsonl_meta(const uint8_t* data, size_t len, uint64_t lo, uint64_t hi, sezkp_blocks** out,
+                                       char* err, size_t err_len);
+int32_t sezkp_blocks_line_offsets(const sezkp_blocks* b, const uint64_t** offsets, size_t* n);
+/* The manifest leaf hashes (sezkp-merkle lib.rs:85-117, 32 bytes per block)
+ * and a root over given leaves: the batch merkle_root (frontier = 0,
+ * lib.rs:140-157) or the Frontier (frontier = 1, lib.rs:167-208). A sharded
+ * launcher hashes each rank's blocks and reduces the gathered leaves. */
+int32_t sezkp_manifest_leaf_hashes(const sezkp_block_view* blocks, uint8_t* out);
+int32_t sezkp_merkle_root_of_leaves(const uint8_t* leaves, size_t n, int32_t frontier, uint8_t out[32]);
 /* Vec<BlockSummary> as CBOR, byte-identical to the reference's writer
  * (io.rs, ciborium; pins: the reference's blocks.cbor fixtures). */
 int32_t sezkp_blocks_encode_cbor(const sezkp_block_view* blocks, sezkp_buf* out);

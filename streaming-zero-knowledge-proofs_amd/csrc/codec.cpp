@@ -189,6 +189,37 @@ class Json {
   }
   uint64_t uint() { ws(); return digits(); }
   std::string text() { return str(); }
+  // Skip an array, counting its elements, without decoding them (string- and
+  // bracket-aware scan): the metadata pass of the sliced JSONL ingest.
+  uint64_t skip_count_array() {
+    ws();
+    expect('[');
+    uint64_t commas = 0;
+    bool any = false;
+    int depth = 1;
+    while (p_ < e_) {
+      const char c = *p_++;
+      if (c == '"') {
+        while (p_ < e_ && *p_ != '"') p_ += *p_ == '\\' ? 2 : 1;
+        if (p_ >= e_) break;
+        p_++;
+        any = true;
+      } else if (c == '[' || c == '{') {
+        depth++;
+        any = true;
+      } else if (c == ']' || c == '}') {
+        if (--depth == 0) {
+          first_ = false;
+          return any ? commas + 1 : 0;
+        }
+      } else if (c == ',') {
+        if (depth == 1) commas++;
+      } else if (!js_space(c)) {
+        any = true;
+      }
+    }
+    throw DecodeError("truncated JSON array");
+  }
   void skip() {
     ws();
     if (p_ >= e_) throw DecodeError("truncated JSON");
@@ -264,11 +295,14 @@ struct BlockShape {
   std::vector<uint32_t> ntape;  // per step
 };
 
-template <class P>
+// META: the block's fields and its step count only (movement_log.steps is
+// counted, not decoded; JSON only)
+template <class P, bool META = false>
 void decode_block(P& d, BlockStore& s, BlockShape& sh) {
   int64_t r = d.begin_map();
   uint32_t nwin = 0, nin = 0, nout = 0;
   const uint64_t steps_before = s.input_mv.size();
+  uint64_t meta_steps = 0;
   s.version.push_back(0); s.block_id.push_back(0); s.step_lo.push_back(0); s.step_hi.push_back(0);
   s.ctrl_in.push_back(0); s.ctrl_out.push_back(0); s.in_head_in.push_back(0); s.in_head_out.push_back(0);
   while (d.more(r)) {
@@ -310,6 +344,10 @@ void decode_block(P& d, BlockStore& s, BlockShape& sh) {
       while (d.more(m)) {
         const Key mk = d.key();
         if (mk != "steps") { d.skip(); continue; }
+        if constexpr (META) {
+          meta_steps += d.skip_count_array();
+          continue;
+        }
         int64_t a = d.begin_array();
         while (d.more(a)) {
           int64_t sm = d.begin_map();
@@ -338,7 +376,7 @@ void decode_block(P& d, BlockStore& s, BlockShape& sh) {
   sh.nwin.push_back(nwin);
   sh.nin.push_back(nin);
   sh.nout.push_back(nout);
-  s.step_start.push_back(s.step_start.back() + (s.input_mv.size() - steps_before));
+  s.step_start.push_back(s.step_start.back() + (META ? meta_steps : s.input_mv.size() - steps_before));
 }
 
 void finish_blocks(BlockStore& s, const BlockShape& sh);
@@ -546,6 +584,52 @@ bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::str
     return true;
   } catch (const std::exception& ex) {
     err = std::string("deserialize JSONL block summaries: ") + ex.what();
+    return false;
+  }
+}
+
+// Sliced ingest, metadata pass: the lines that START in [cut(lo), cut(hi))
+// (cut(x) = just past the first newline at or after byte x; cut(0) = 0,
+// cut(len) = len, so P ranks taking [len g/P, len (g+1)/P) cover every line
+// once). Every block's fields and step count, not its steps; line_off gets
+// each line's byte offset. Step arrays stay empty.
+bool decode_blocks_jsonl_meta(const char* data, size_t len, size_t lo, size_t hi, BlockStore& out,
+                              std::vector<uint64_t>& line_off, std::string& err) {
+  auto cut = [&](size_t x) -> size_t {
+    if (x == 0) return 0;
+    if (x >= len) return len;
+    const char* nl = static_cast<const char*>(memchr(data + x, '\n', len - x));
+    return nl ? (size_t)(nl - data) + 1 : len;
+  };
+  const size_t b = cut(lo), e = cut(std::max(lo, hi));
+  out = BlockStore{};
+  out.step_start.assign(1, 0);
+  line_off.clear();
+  BlockShape sh;
+  size_t p = b, line = 0;
+  try {
+    while (p < e) {
+      const char* nl = static_cast<const char*>(memchr(data + p, '\n', e - p));
+      const size_t end = nl ? (size_t)(nl - data) : e;
+      line++;
+      size_t le = end;
+      if (le > p && data[le - 1] == '\r') le--;
+      if (le == p) throw DecodeError("empty line");
+      line_off.push_back(p);
+      Json d(data + p, le - p);
+      decode_block<Json, true>(d, out, sh);
+      if (!d.done()) throw DecodeError("trailing bytes after the block object");
+      p = nl ? end + 1 : e;
+    }
+    out.tau = sh.nwin.empty() ? 0 : sh.nwin[0];
+    for (size_t k = 0; k < sh.nwin.size(); k++)
+      if (sh.nwin[k] != out.tau || sh.nin[k] != out.tau || sh.nout[k] != out.tau)
+        throw DecodeError("block " + std::to_string(k) + ": windows/head offsets length != tau");
+    out.bind();
+    return true;
+  } catch (const std::exception& ex) {
+    err = "parse jsonl line at byte " + std::to_string(line_off.empty() ? b : line_off.back()) + " (line " +
+          std::to_string(line) + " of the range): " + ex.what();
     return false;
   }
 }
@@ -772,10 +856,19 @@ void manifest_leaf_hash(const sezkp_block_view& v, uint32_t k, uint8_t out[32]) 
 }
 
 void manifest_root(const sezkp_block_view& v, uint8_t out[32]) {  // lib.rs:140-157, odd promotion
-  if (v.n_blocks == 0) { memset(out, 0, 32); return; }
   std::vector<uint8_t> lv(32ull * v.n_blocks);
   for (uint32_t k = 0; k < v.n_blocks; k++) manifest_leaf_hash(v, k, lv.data() + 32ull * k);
-  size_t n = v.n_blocks;
+  merkle_root_of_leaves(lv.data(), v.n_blocks, false, out);
+}
+
+void merkle_root_of_leaves(const uint8_t* leaves, size_t nleaves, bool frontier, uint8_t out[32]) {
+  if (frontier) {
+    frontier_root_of_leaves(leaves, nleaves, out);
+    return;
+  }
+  if (nleaves == 0) { memset(out, 0, 32); return; }
+  std::vector<uint8_t> lv(leaves, leaves + 32 * nleaves);
+  size_t n = nleaves;
   while (n > 1) {
     size_t m = 0;
     for (size_t i = 0; i < n; i += 2, m++) {
@@ -796,12 +889,18 @@ void manifest_root(const sezkp_block_view& v, uint8_t out[32]) {  // lib.rs:140-
 // leaves it does not, and the reference commits this value, so it
 // is restated as written.
 void manifest_frontier_root(const sezkp_block_view& v, uint8_t out[32]) {
+  std::vector<uint8_t> lv(32ull * v.n_blocks);
+  for (uint32_t k = 0; k < v.n_blocks; k++) manifest_leaf_hash(v, k, lv.data() + 32ull * k);
+  frontier_root_of_leaves(lv.data(), v.n_blocks, out);
+}
+
+void frontier_root_of_leaves(const uint8_t* leaves, size_t nleaves, uint8_t out[32]) {
   uint8_t level[64][32];  // level[l]: the pending 2^l-leaf subtree root (bit l of the count)
   uint64_t occupied = 0;
   uint8_t node[64];       // left || right of one parent
-  for (uint32_t k = 0; k < v.n_blocks; k++) {
+  for (size_t k = 0; k < nleaves; k++) {
     uint8_t h[32];
-    manifest_leaf_hash(v, k, h);
+    memcpy(h, leaves + 32 * k, 32);
     int l = 0;
     while (occupied >> l & 1) {  // a waiting left sibling: merge and carry
       memcpy(node, level[l], 32);

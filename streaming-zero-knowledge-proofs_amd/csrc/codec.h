@@ -28,6 +28,10 @@ struct BlockStore {
 bool decode_blocks_cbor(const uint8_t* data, size_t len, BlockStore& out, std::string& err);
 bool decode_blocks_json(const char* data, size_t len, BlockStore& out, std::string& err);
 bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::string& err);
+// sliced ingest: block fields + step counts of the lines starting in the byte
+// range [lo, hi) (cut at line ends), no steps; line_off = each line's offset
+bool decode_blocks_jsonl_meta(const char* data, size_t len, size_t lo, size_t hi, BlockStore& out,
+                              std::vector<uint64_t>& line_off, std::string& err);
 std::string encode_blocks_jsonl(const sezkp_block_view& v);
 std::vector<uint8_t> encode_blocks_cbor(const sezkp_block_view& v);
 // partition_trace (partition.rs:43-150) of a step-major movement log into blocks of b steps
@@ -72,5 +76,8 @@ void manifest_leaf_hash(const sezkp_block_view& v, uint32_t k, uint8_t out[32]);
 void manifest_root(const sezkp_block_view& v, uint8_t out[32]);
 // Frontier root of the .jsonl commit path (lib.rs:167-208, 259-330)
 void manifest_frontier_root(const sezkp_block_view& v, uint8_t out[32]);
+// the same two roots over given leaf hashes (distributed precheck)
+void merkle_root_of_leaves(const uint8_t* leaves, size_t n, bool frontier, uint8_t out[32]);
+void frontier_root_of_leaves(const uint8_t* leaves, size_t n, uint8_t out[32]);
 
 }  // namespace sezkp

@@ -444,12 +444,14 @@ struct sezkp_ctx {
     if (stall_word) (void)hipHostFree(stall_word);
   }
 
-  void upload(const sezkp_block_view& v);
+  // row0 / nrows: the view's step arrays hold only rows [row0, row0 + nrows)
+  // (metadata and step_start still global): a sharded rank's slice
+  void upload(const sezkp_block_view& v, uint64_t row0 = 0, uint64_t nrows = ~0ull);
   // stage the next trace (same shape) into the spare slot on the copy stream
   void stage(const sezkp_block_view& v);
   void alloc_slot(TraceSlot& t);
   // block tables + step arrays of `v` into slot t, async on stream s
-  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s);
+  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, uint64_t row0, uint64_t nrows);
   void check_shape_same(const sezkp_block_view& v) const;
   void take_staged();
   // proves into the pinned staging buffer; returns its size (bytes at h_proof)
@@ -483,7 +485,27 @@ static void fail_point(int rank, const char* name) {
 }
 
 
-void sezkp_ctx::upload(const sezkp_block_view& v) {
+// The column chunks [ch_lo, ch_hi) rank g of 2^logP commits (all of them on
+// one device) and the blocks holding their rows [ch_lo * 1024, ch_hi * 1024]
+// (the extra row: compose and the next_* openings read row i + 1; the last
+// row's wrap to row 0 is never read: row n - 1 is a block's last row, where
+// the head-update term vanishes, and its next_* openings belong to rank 0).
+static void shard_range(const uint64_t* step_start, uint32_t nblk, int logn, int rank, int logP, uint64_t& ch_lo,
+                        uint64_t& ch_hi, uint32_t& blk_lo, uint32_t& blk_cnt) {
+  const uint64_t n = 1ULL << logn;
+  const int logChunks = logn > COL_CHUNK_LOG2 ? logn - COL_CHUNK_LOG2 : 0;
+  const uint64_t nchunks = 1ULL << logChunks, chunk_rows = n < 1024 ? n : 1024;
+  ch_lo = (nchunks >> logP) * (uint64_t)rank;
+  ch_hi = ch_lo + (nchunks >> logP);
+  const uint64_t r0 = ch_lo * chunk_rows, r1 = std::min<uint64_t>(ch_hi * chunk_rows, n - 1);
+  auto block_of = [&](uint64_t row) {
+    return (uint32_t)(std::upper_bound(step_start, step_start + nblk + 1, row) - step_start - 1);
+  };
+  blk_lo = block_of(r0);
+  blk_cnt = block_of(r1) - blk_lo + 1;
+}
+
+void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows) {
   HIP_OR_THROW(hipSetDevice(device));
   // a stage() may still be copying into / transposing a slot on the copy
   // stream: it must finish before its buffers become spares for this upload
@@ -533,10 +555,26 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
     slot[1].ready = keep;
   }
   alloc_slot(slot[0]);
+  const uint64_t nchunks = 1ULL << logChunks, chunk_rows = n < 1024 ? n : 1024;
+  // sharded: this rank commits chunks [ch_lo, ch_hi) of every column
+  if (sharded()) {
+    if (logn < 12 + logP || logP > 3)
+      throw Err{SEZKP_E_INVALID, "sharded proving needs n >= 4096 * P rows and P <= 8 (n = " + std::to_string(n) +
+                                     ", P = " + std::to_string(world) + ")"};
+  }
+  shard_range(v.step_start, nblk, logn, sharded() ? rank : 0, sharded() ? logP : 0, ch_lo, ch_hi, blk_lo, blk_cnt);
   uint64_t* d_bs = dalloc<uint64_t>(nblk + 1);
   up(d_bs, v.step_start, nblk + 1);
   cur_step_start.assign(v.step_start, v.step_start + nblk + 1);
-  write_trace(slot[0], v, st);
+  if (nrows == ~0ull) nrows = n - row0;
+  {  // the rows this context reads: every row (one device) or the whole blocks over its chunks (+ the halo row)
+    const uint64_t need0 = v.step_start[blk_lo], need1 = v.step_start[blk_lo + blk_cnt];
+    if (row0 > need0 || row0 + nrows < need1 || row0 + nrows > n)
+      throw Err{SEZKP_E_INVALID, "step arrays hold rows [" + std::to_string(row0) + ", " + std::to_string(row0 + nrows) +
+                                     ") but this context needs rows [" + std::to_string(need0) + ", " +
+                                     std::to_string(need1) + ")"};
+  }
+  write_trace(slot[0], v, st, row0, nrows);
   HIP_OR_THROW(hipStreamSynchronize(st));
   TraceSlot& t0 = slot[0];
   T.n = n;
@@ -593,27 +631,6 @@ void sezkp_ctx::upload(const sezkp_block_view& v) {
   }
   // chunks whose rows cross few block boundaries go to the piecewise kernel;
   // the rest (many short blocks) are committed densely for every column
-  const uint64_t nchunks = 1ULL << logChunks, chunk_rows = n < 1024 ? n : 1024;
-  // sharded: this rank commits chunks [ch_lo, ch_hi) of every column
-  if (sharded()) {
-    if (logn < 12 + logP || logP > 3)
-      throw Err{SEZKP_E_INVALID, "sharded proving needs n >= 4096 * P rows and P <= 8 (n = " + std::to_string(n) +
-                                     ", P = " + std::to_string(world) + ")"};
-    ch_lo = (nchunks >> logP) * rank;
-    ch_hi = ch_lo + (nchunks >> logP);
-  } else {
-    ch_lo = 0;
-    ch_hi = nchunks;
-  }
-  {  // blocks holding rows [ch_lo * 1024, ch_hi * 1024] (the extra row: compose and
-     // next_* openings read row i + 1)
-    const uint64_t r0 = ch_lo * chunk_rows, r1 = std::min<uint64_t>(ch_hi * chunk_rows, n - 1);
-    auto block_of = [&](uint64_t row) {
-      return (uint32_t)(std::upper_bound(v.step_start, v.step_start + nblk + 1, row) - v.step_start - 1);
-    };
-    blk_lo = block_of(r0);
-    blk_cnt = block_of(r1) - blk_lo + 1;
-  }
   std::vector<uint32_t> work, pw_chunks;
   std::vector<uint8_t> dense_chunk(nchunks, 0);
   {
@@ -847,7 +864,7 @@ void sezkp_ctx::alloc_slot(TraceSlot& t) {
 // Per-block tables on the host (window lengths, head offsets: tau * n_blocks
 // values), then every array over PCIe asynchronously on `s` and the row-major
 // step arrays transposed to the tape-major image on the device.
-void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s) {
+void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, uint64_t row0, uint64_t nrows) {
   const size_t cells = (size_t)tau * n, nt = (size_t)tau * nblk;
   // the previous copy out of h_tab (an earlier stage into this slot, and its
   // transposition of `raw` on the same stream) must be done
@@ -876,12 +893,14 @@ void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t
   uint16_t* raw_ws = reinterpret_cast<uint16_t*>(t.raw);
   int8_t* raw_mv = reinterpret_cast<int8_t*>(t.raw + 2 * cells);
   uint8_t* raw_hw = t.raw + 3 * cells;
-  cp(raw_ws, v.wsym, cells * 2);
-  cp(raw_mv, v.mv, cells);
-  cp(raw_hw, v.has_write, cells);
-  cp(t.imv, v.input_mv, n);
+  const size_t c0 = (size_t)row0 * tau, nc = (size_t)nrows * tau;
+  (void)cells;
+  cp(raw_ws + c0, v.wsym, nc * 2);
+  cp(raw_mv + c0, v.mv, nc);
+  cp(raw_hw + c0, v.has_write, nc);
+  cp(t.imv + row0, v.input_mv, nrows);
   cp(t.bw, t.h_tab, 3 * nt * 8);
-  HIP_OR_THROW(launch_trace_image(s, raw_mv, raw_hw, raw_ws, n, tau, t.mv, t.wf, t.ws));
+  HIP_OR_THROW(launch_trace_image(s, raw_mv, raw_hw, raw_ws, n, tau, t.mv, t.wf, t.ws, row0, row0 + nrows));
   HIP_OR_THROW(hipEventRecord(t.ready, s));
 }
 
@@ -907,7 +926,7 @@ void sezkp_ctx::stage(const sezkp_block_view& v) {
   TraceSlot& t = slot[1 - active];
   if (!t.imv) alloc_slot(t);  // first stage on this workspace: the spare image
   staged = false;             // (re)filling the spare slot
-  write_trace(t, v, stc);
+  write_trace(t, v, stc, 0, n);
   staged = true;
 }
 
@@ -1316,7 +1335,6 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   }
   // ---- composition (this rank's rows), DEEP quotient, INTT
   mark("z_done");
-  ok(launch_compose(st, T, d_chal, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
   // single device: DEEP as the LDE of H = q + c S (DeepPoly); the base
   // evaluations become q(w^j) before the INTT. Not when z^n = 1 (z on the
   // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
@@ -1334,10 +1352,6 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   // are [g n/P, (g+1) n/P) (n >= 4096 P). SEZKP_REPLICATED_INTT=1 gathers the
   // n values and runs the n-point INTT on every rank instead.
   const bool dist_intt = sharded && world > 1 && !getenv("SEZKP_REPLICATED_INTT");
-  if (sharded && !dq && !dist_intt)
-    coll("base_values", P1 * (row_hi - row_lo) * 8,
-         [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
-  rec(4);
   DeepPoly dpoly{d_dq_rlo, d_dq_rhi};
   if (dq && host_tr) {
     const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
@@ -1364,6 +1378,11 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   }
   if (host_tr)  // alphas, masks and the DEEP constants for the kernels below
     HIP_OR_THROW(hipMemcpyAsync(d_chal, h_chal, offsetof(DevChal, beta), hipMemcpyHostToDevice, st));
+  ok(launch_compose(st, T, d_chal, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
+  if (sharded && !dq && !dist_intt)
+    coll("base_values", P1 * (row_hi - row_lo) * 8,
+         [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
+  rec(4);
   if (dq) {
     if (sharded) {
       const uint64_t nrows = row_hi - row_lo, per = 4096;
@@ -1831,6 +1850,38 @@ int32_t sezkp_ctx_upload(sezkp_ctx* ctx, const sezkp_block_view* blocks, char* e
     set_err(err, err_len, e.what());
     return SEZKP_E_NOMEM;
   }
+}
+
+int32_t sezkp_ctx_upload_rows(sezkp_ctx* ctx, const sezkp_block_view* blocks, uint64_t row0, uint64_t nrows,
+                              char* err, size_t err_len) {
+  try {
+    if (!ctx || !blocks) throw Err{SEZKP_E_INVALID, "null argument"};
+    if (ctx->busy()) throw Err{SEZKP_E_INVALID, "a proof is in flight on this context (call sezkp_ctx_wait)"};
+    ctx->upload(*blocks, row0, nrows);
+    return SEZKP_OK;
+  } catch (const Err& e) {
+    set_err(err, err_len, e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, err_len, e.what());
+    return SEZKP_E_NOMEM;
+  }
+}
+int32_t sezkp_shard_rows(const uint64_t* step_start, uint32_t n_blocks, int32_t rank, int32_t world, uint64_t* row0,
+                         uint64_t* nrows) {
+  if (!step_start || !row0 || !nrows || !n_blocks || world < 1 || world > 8 || (world & (world - 1)) || rank < 0 ||
+      rank >= world)
+    return SEZKP_E_INVALID;
+  const uint64_t n = step_start[n_blocks];
+  if (!n || (n & (n - 1))) return SEZKP_E_INVALID;
+  const int logn = ilog2(n), logP = ilog2((uint64_t)world);
+  if (world > 1 && logn < 12 + logP) return SEZKP_E_INVALID;
+  uint64_t ch_lo, ch_hi;
+  uint32_t blk_lo, blk_cnt;
+  shard_range(step_start, n_blocks, logn, rank, logP, ch_lo, ch_hi, blk_lo, blk_cnt);
+  *row0 = step_start[blk_lo];
+  *nrows = step_start[blk_lo + blk_cnt] - *row0;
+  return SEZKP_OK;
 }
 
 int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, sezkp_buf* proof_bytes,
@@ -2308,7 +2359,36 @@ int32_t sezkp_manifest_frontier_root(const sezkp_block_view* blocks, uint8_t out
 
 struct sezkp_blocks {
   BlockStore s;
+  std::vector<uint64_t> line_off;  // sezkp_blocks_decode_jsonl_meta: each line's byte offset
 };
+int32_t sezkp_blocks_decode_jsonl_meta(const uint8_t* data, size_t len, uint64_t lo, uint64_t hi, sezkp_blocks** out,
+                                       char* err, size_t err_len) {
+  if (!out || (!data && len) || lo > hi) return SEZKP_E_INVALID;
+  std::unique_ptr<sezkp_blocks> b(new sezkp_blocks());
+  std::string e;
+  if (!decode_blocks_jsonl_meta(reinterpret_cast<const char*>(data), len, lo, hi, b->s, b->line_off, e)) {
+    set_err(err, err_len, e);
+    return SEZKP_E_DECODE;
+  }
+  *out = b.release();
+  return SEZKP_OK;
+}
+int32_t sezkp_blocks_line_offsets(const sezkp_blocks* b, const uint64_t** offsets, size_t* n) {
+  if (!b || !offsets || !n) return SEZKP_E_INVALID;
+  *offsets = b->line_off.data();
+  *n = b->line_off.size();
+  return SEZKP_OK;
+}
+int32_t sezkp_manifest_leaf_hashes(const sezkp_block_view* blocks, uint8_t* out) {
+  if (!blocks || (!out && blocks->n_blocks)) return SEZKP_E_INVALID;
+  for (uint32_t k = 0; k < blocks->n_blocks; k++) manifest_leaf_hash(*blocks, k, out + 32ull * k);
+  return SEZKP_OK;
+}
+int32_t sezkp_merkle_root_of_leaves(const uint8_t* leaves, size_t n, int32_t frontier, uint8_t out[32]) {
+  if (!out || (!leaves && n)) return SEZKP_E_INVALID;
+  merkle_root_of_leaves(leaves, n, frontier != 0, out);
+  return SEZKP_OK;
+}
 int32_t sezkp_blocks_decode_cbor(const uint8_t* data, size_t len, sezkp_blocks** out, char* err, size_t err_len) {
   if (!out || (!data && len)) return SEZKP_E_INVALID;
   std::unique_ptr<sezkp_blocks> b(new sezkp_blocks());

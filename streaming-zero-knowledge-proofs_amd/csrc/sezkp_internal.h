@@ -298,9 +298,10 @@ hipError_t launch_fs_point(hipStream_t st, const FsArgs& a);
 
 // kernels launched by the host orchestrator (prover.cpp)
 // blocks [blk_lo, blk_lo + blk_cnt) only (a sharded rank's rows + one row of halo)
-// row-major step arrays [n][tau] -> tape-major trace image [tau][n]
+// row-major step arrays [n][tau] -> tape-major trace image [tau][n], rows [r0, r1)
 hipError_t launch_trace_image(hipStream_t st, const int8_t* raw_mv, const uint8_t* raw_hw, const uint16_t* raw_ws,
-                              uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws);
+                              uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws, uint64_t r0 = 0,
+                              uint64_t r1 = ~0ull);
 // d_err: guard word, GUARD_HEAD_RANGE is or-ed in when a head leaves the i32 range
 hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt, uint32_t* d_err);
 hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_tab_cols,

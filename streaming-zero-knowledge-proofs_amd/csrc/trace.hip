@@ -31,9 +31,9 @@ __global__ void __launch_bounds__(TR_THREADS) k_trace_image(const int8_t* __rest
                                                           const uint8_t* __restrict__ raw_hw,
                                                           const uint16_t* __restrict__ raw_ws, uint64_t n, int tau,
                                                           int8_t* __restrict__ mv, uint8_t* __restrict__ wf,
-                                                          uint16_t* __restrict__ ws) {
-  const uint64_t s = (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
-  if (s >= n) return;
+                                                          uint16_t* __restrict__ ws, uint64_t r0, uint64_t r1) {
+  const uint64_t s = r0 + (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
+  if (s >= r1) return;
   const size_t i0 = (size_t)s * tau;
   for (int r = 0; r < tau; r++) {
     const size_t o = (size_t)r * n + s;
@@ -100,11 +100,12 @@ __global__ void __launch_bounds__(TR_THREADS) k_trace_image8(const int8_t* __res
                                                            const uint8_t* __restrict__ raw_hw,
                                                            const uint16_t* __restrict__ raw_ws, uint64_t n,
                                                            int8_t* __restrict__ mv, uint8_t* __restrict__ wf,
-                                                           uint16_t* __restrict__ ws) {
-  const uint64_t s0 = ((uint64_t)blockIdx.x * TR_THREADS + threadIdx.x) * 8;
-  if (s0 >= n) return;
-  if (s0 + 8 > n) {  // ragged tail: element by element
-    for (uint64_t s = s0; s < n; s++)
+                                                           uint16_t* __restrict__ ws, uint64_t r0, uint64_t r1) {
+  // rows [r0, r1): r0 a multiple of 8
+  const uint64_t s0 = r0 + ((uint64_t)blockIdx.x * TR_THREADS + threadIdx.x) * 8;
+  if (s0 >= r1) return;
+  if (s0 + 8 > r1) {  // ragged tail: element by element
+    for (uint64_t s = s0; s < r1; s++)
       for (int r = 0; r < 8; r++) {
         const bool w = raw_hw[s * 8 + r] != 0;
         mv[(uint64_t)r * n + s] = raw_mv[s * 8 + r];
@@ -1593,19 +1594,21 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
 
 // ------------------------------------------------------------------ host
 hipError_t launch_trace_image(hipStream_t st, const int8_t* raw_mv, const uint8_t* raw_hw, const uint16_t* raw_ws,
-                              uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws) {
-  if (n == 0 || tau <= 0) return hipSuccess;
+                              uint64_t n, int tau, int8_t* mv, uint8_t* wf, uint16_t* ws, uint64_t r0, uint64_t r1) {
+  if (r1 > n) r1 = n;
+  if (r0 >= r1 || tau <= 0) return hipSuccess;
   if (tau == 8) {
-    const uint64_t g8 = ((n + 7) / 8 + TR_THREADS - 1) / TR_THREADS;
+    r0 &= ~7ull;  // the rows in front of the slice are the raw buffer's other contents: never read
+    const uint64_t g8 = ((r1 - r0 + 7) / 8 + TR_THREADS - 1) / TR_THREADS;
     if (g8 > 0x7FFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_trace_image8, dim3((unsigned)g8), dim3(TR_THREADS), 0, st, raw_mv, raw_hw, raw_ws, n, mv, wf,
-                       ws);
+                       ws, r0, r1);
     return hipGetLastError();
   }
-  const uint64_t g = (n + TR_THREADS - 1) / TR_THREADS;
+  const uint64_t g = (r1 - r0 + TR_THREADS - 1) / TR_THREADS;
   if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_trace_image, dim3((unsigned)g), dim3(TR_THREADS), 0, st, raw_mv, raw_hw, raw_ws, n, tau, mv,
-                     wf, ws);
+                     wf, ws, r0, r1);
   return hipGetLastError();
 }
 hipError_t launch_expand(hipStream_t st, const TraceDev& T, uint32_t blk_lo, uint32_t blk_cnt, uint32_t* d_err) {

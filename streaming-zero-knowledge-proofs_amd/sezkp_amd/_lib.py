@@ -32,7 +32,8 @@ EXPORTS = [
     "sezkp_ctx_prove_async", "sezkp_ctx_wait", "sezkp_ctx_stage", "sezkp_host_register", "sezkp_host_unregister",
     "sezkp_fri_fold", "sezkp_blake3_leaves_u64", "sezkp_blake3_leaves_labeled", "sezkp_merkle_node_count",
     "sezkp_merkle_build", "sezkp_merkle_paths", "sezkp_manifest_frontier_root", "sezkp_ctx_comm_stats",
-    "sezkp_fs_xof",
+    "sezkp_fs_xof", "sezkp_ctx_upload_rows", "sezkp_shard_rows", "sezkp_blocks_decode_jsonl_meta",
+    "sezkp_blocks_line_offsets", "sezkp_manifest_leaf_hashes", "sezkp_merkle_root_of_leaves",
 ]
 
 
@@ -147,6 +148,16 @@ def _load():
     L.sezkp_host_register.argtypes = [C.c_void_p, C.c_size_t]
     L.sezkp_host_unregister.argtypes = [C.c_void_p]
     L.sezkp_ctx_dist_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32] + E
+    L.sezkp_fs_xof.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_uint32), C.c_char_p, C.POINTER(C.c_uint32),
+                               C.POINTER(C.c_uint32), C.c_uint32, C.c_char_p, C.c_void_p]
+    L.sezkp_ctx_upload_rows.argtypes = [C.c_void_p, C.POINTER(BlockView), C.c_uint64, C.c_uint64] + E
+    L.sezkp_shard_rows.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint64)]
+    L.sezkp_blocks_decode_jsonl_meta.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint64,
+                                                 C.POINTER(C.c_void_p)] + E
+    L.sezkp_blocks_line_offsets.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.c_size_t)]
+    L.sezkp_manifest_leaf_hashes.argtypes = [C.POINTER(BlockView), C.c_void_p]
+    L.sezkp_merkle_root_of_leaves.argtypes = [C.c_char_p, C.c_size_t, C.c_int32, C.c_char_p]
     return L
 
 

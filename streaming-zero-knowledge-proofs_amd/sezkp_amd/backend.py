@@ -116,6 +116,13 @@ class ProverContext:
         check(lib.sezkp_ctx_upload(self._h, C.byref(blocks.view()), err, 1024), err)
         self.tau = blocks.tau
 
+    def upload_rows(self, blocks: BlockSoA, row0: int, nrows: int) -> None:
+        """Upload from a view whose step arrays hold only rows [row0, row0 +
+        nrows) (a sharded rank's slice, sezkp_ctx_upload_rows)."""
+        err = C.create_string_buffer(1024)
+        check(lib.sezkp_ctx_upload_rows(self._h, C.byref(blocks.view()), row0, nrows, err, 1024), err)
+        self.tau = blocks.tau
+
     def stage(self, blocks: BlockSoA) -> None:
         """Pipelined upload of the next trace (same shape as the uploaded one):
         async H2D into the spare trace image, allowed while a proof is in

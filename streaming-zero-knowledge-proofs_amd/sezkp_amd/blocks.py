@@ -32,6 +32,12 @@ class BlockSoA:
         self.n_blocks = int(self.version.size)
         self._view = None
 
+    def __getstate__(self):  # pickled across ranks (sliced ingest): arrays only, no ctypes view
+        return {"tau": self.tau, **{f: getattr(self, f) for f, _ in VIEW_FIELDS}}
+
+    def __setstate__(self, st):
+        self.__init__(st.pop("tau"), **st)
+
     # total trace rows n = sum(step_hi - step_lo + 1)
     @property
     def n_rows(self) -> int:
@@ -137,9 +143,75 @@ class BlockSoA:
             raise SezkpError(rc, err.value.decode())
         return cls._take(h)
 
+    def leaf_hashes(self) -> bytes:
+        """The manifest leaf hash of every block (sezkp-merkle lib.rs:85-117),
+        32 bytes each: needs the blocks' fields and step counts only."""
+        out = C.create_string_buffer(32 * max(1, self.n_blocks))
+        rc = lib.sezkp_manifest_leaf_hashes(C.byref(self.view()), out)
+        if rc != 0:
+            raise SezkpError(rc, "leaf hashes")
+        return out.raw[:32 * self.n_blocks]
+
     @classmethod
-    def _take(cls, h) -> "BlockSoA":
-        """Copy a library-owned sezkp_blocks into numpy arrays and free it."""
+    def from_jsonl_meta(cls, data, lo: int, hi: int) -> tuple:
+        """The metadata of the JSONL lines starting in bytes [lo, hi) of `data`
+        (bytes or a uint8 numpy array / memmap; cut at line ends): every field
+        and step count, no steps (empty step arrays). Returns (BlockSoA, line
+        byte offsets) (sezkp_blocks_decode_jsonl_meta)."""
+        ptr, n = _addr(data)
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = lib.sezkp_blocks_decode_jsonl_meta(ptr, n, lo, hi, C.byref(h), err, 512)
+        if rc != 0:
+            raise SezkpError(rc, err.value.decode())
+        p = C.POINTER(C.c_uint64)()
+        cnt = C.c_size_t()
+        lib.sezkp_blocks_line_offsets(h, C.byref(p), C.byref(cnt))
+        offs = np.ctypeslib.as_array(p, shape=(cnt.value,)).copy() if cnt.value else np.zeros(0, np.uint64)
+        return cls._take(h, meta=True), offs
+
+    @classmethod
+    def from_jsonl_range(cls, data, lo: int, hi: int) -> "BlockSoA":
+        """Full decode of the whole lines in bytes [lo, hi) of `data`."""
+        ptr, n = _addr(data)
+        if not 0 <= lo <= hi <= n:
+            raise SezkpError(-1, "bad byte range")
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = lib.sezkp_blocks_decode_jsonl(C.cast(C.c_void_p(ptr + lo), C.c_char_p), hi - lo, C.byref(h), err, 512)
+        if rc != 0:
+            raise SezkpError(rc, err.value.decode())
+        return cls._take(h)
+
+    @classmethod
+    def concat_meta(cls, parts: list) -> "BlockSoA":
+        """Blocks of several metadata-only parts, in order (step_start rebuilt
+        from the parts' step counts)."""
+        parts = [p for p in parts if p.n_blocks]
+        tau = parts[0].tau if parts else 0
+        arr = {}
+        for f, t in VIEW_FIELDS:
+            if f == "step_start":
+                counts = np.concatenate([np.diff(p.step_start) for p in parts]) if parts else np.zeros(0, np.uint64)
+                arr[f] = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+            elif f in ("input_mv", "mv", "has_write", "wsym"):
+                arr[f] = np.zeros(0, _NP[t])
+            else:
+                arr[f] = np.concatenate([getattr(p, f) for p in parts]) if parts else np.zeros(0, _NP[t])
+        return cls(tau, **arr)
+
+    def with_steps(self, slice_blocks: "BlockSoA") -> "BlockSoA":
+        """These (global) block fields with the step arrays of `slice_blocks`
+        (a run of whole blocks): the view sezkp_ctx_upload_rows takes."""
+        arr = {f: getattr(self, f) for f, _ in VIEW_FIELDS}
+        for f in ("input_mv", "mv", "has_write", "wsym"):
+            arr[f] = getattr(slice_blocks, f)
+        return BlockSoA(self.tau, **arr)
+
+    @classmethod
+    def _take(cls, h, meta: bool = False) -> "BlockSoA":
+        """Copy a library-owned sezkp_blocks into numpy arrays and free it
+        (meta: the step arrays are empty, step_start holds the step counts)."""
         try:
             v = lib.sezkp_blocks_view(h).contents
             nb, tau = v.n_blocks, v.tau
@@ -149,7 +221,7 @@ class BlockSoA:
             for f in ("win_left", "win_right", "off_in", "off_out"):
                 base[f] = nb * tau
             step_start = np.ctypeslib.as_array(v.step_start, shape=(nb + 1,)).copy() if nb else np.zeros(1, np.uint64)
-            S = int(step_start[-1])
+            S = 0 if meta else int(step_start[-1])
             base.update(step_start=nb + 1, input_mv=S, mv=S * tau, has_write=S * tau, wsym=S * tau)
             for f, t in VIEW_FIELDS:
                 cnt = base[f]
@@ -159,6 +231,37 @@ class BlockSoA:
             return cls(tau, **arr)
         finally:
             lib.sezkp_blocks_free(h)
+
+
+def _addr(data) -> tuple:
+    """(address, length) of bytes or a contiguous uint8 numpy array / memmap."""
+    if isinstance(data, bytes):  # no copy: the caller keeps `data` alive
+        return C.cast(C.c_char_p(data), C.c_void_p).value or 0, len(data)
+    a = np.frombuffer(data, dtype=np.uint8) if isinstance(data, bytearray) else data
+    if not (isinstance(a, np.ndarray) and a.dtype == np.uint8 and a.flags.c_contiguous):
+        raise SezkpError(-1, "data must be bytes or a contiguous uint8 array")
+    return a.ctypes.data, a.size
+
+
+def merkle_root_of_leaves(leaves: bytes, frontier: bool) -> bytes:
+    """The batch merkle_root (lib.rs:140-157) or the Frontier root (lib.rs:
+    167-208) over 32-byte leaf hashes (sezkp_merkle_root_of_leaves)."""
+    out = C.create_string_buffer(32)
+    rc = lib.sezkp_merkle_root_of_leaves(leaves, len(leaves) // 32, 1 if frontier else 0, out)
+    if rc != 0:
+        raise SezkpError(rc, "merkle root of leaves")
+    return out.raw
+
+
+def shard_rows(step_start, rank: int, world: int) -> tuple:
+    """The rows (row0, nrows) rank `rank` of a `world`-GPU sharded prove reads
+    (whole blocks; sezkp_shard_rows)."""
+    ss = np.ascontiguousarray(step_start, dtype=np.uint64)
+    r0, nr = C.c_uint64(), C.c_uint64()
+    rc = lib.sezkp_shard_rows(ss.ctypes.data, ss.size - 1, rank, world, C.byref(r0), C.byref(nr))
+    if rc != 0:
+        raise SezkpError(rc, "shard_rows: n must be a power of two >= 4096 * world")
+    return r0.value, nr.value
 
 
 def simulate(t: int, tau: int, seed: int = 42):

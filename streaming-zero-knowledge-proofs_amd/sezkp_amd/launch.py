@@ -14,6 +14,13 @@ precheck uses the streaming Frontier root as the reference's
 verify_block_file_against_manifest does (sezkp-merkle lib.rs:302-330).
 --gpus 1 runs the single-GPU context. --comm host runs every rank on GPU 0
 with host-staged collectives (tests).
+
+With several GPUs a .jsonl/.ndjson file is read in slices (sezkp_amd.ingest):
+each rank decodes the metadata of 1/P of the lines, the metadata and the
+manifest leaf hashes are allgathered (rank 0 reduces the leaves to the root
+and broadcasts the precheck verdict), and each rank fully decodes and uploads
+only the lines of the blocks over its own rows plus the halo row
+(--full-ingest: every rank decodes the whole file, as before).
 """
 from __future__ import annotations
 
@@ -59,22 +66,38 @@ def _precheck(blocks, path: str, root: bytes, n_leaves: int) -> None:
                            f"recomputed={blocks.n_blocks}")
 
 
+def _is_jsonl(path: str) -> bool:
+    return path.rsplit(".", 1)[-1].lower() in ("jsonl", "ndjson") if "." in path else False
+
+
 def _worker(rank: int, world: int, port: int, args, q) -> None:
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # this rank's share of the host threads for block decoding (codec.cpp decode_threads)
+    if "SEZKP_HOST_THREADS" not in os.environ:
+        cpus = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        os.environ["SEZKP_HOST_THREADS"] = str(max(1, cpus // world))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from . import ShardedProverContext
         from .blocks import BlockSoA
         t0 = time.perf_counter()
-        blocks = BlockSoA.from_file(args.blocks)
-        t_load = time.perf_counter() - t0
         root, n_leaves = _read_manifest(args.manifest)
-        if not args.assume_committed:
-            _precheck(blocks, args.blocks, root, n_leaves)
         dev = 0 if args.comm == "host" else rank
-        ctx = ShardedProverContext(rank, world, device=dev, comm=args.comm)
-        ctx.upload(blocks)
+        if _is_jsonl(args.blocks) and not args.full_ingest:
+            from .ingest import TorchComm, sliced_ingest
+            ing = sliced_ingest(args.blocks, rank, world, TorchComm(), None if args.assume_committed else root,
+                                n_leaves, frontier=True)
+            t_load = time.perf_counter() - t0
+            ctx = ShardedProverContext(rank, world, device=dev, comm=args.comm)
+            ctx.upload_rows(ing["blocks"], ing["row0"], ing["nrows"])
+        else:
+            blocks = BlockSoA.from_file(args.blocks)
+            t_load = time.perf_counter() - t0
+            if not args.assume_committed:
+                _precheck(blocks, args.blocks, root, n_leaves)
+            ctx = ShardedProverContext(rank, world, device=dev, comm=args.comm)
+            ctx.upload(blocks)
         t1 = time.perf_counter()
         art = ctx.prove(root, streaming=args.stream)
         t_prove = time.perf_counter() - t1
@@ -182,6 +205,8 @@ def main(argv=None) -> int:
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--comm", default="rccl", choices=["rccl", "host"])
     p.add_argument("--timeout", type=float, default=1800.0)
+    p.add_argument("--full-ingest", action="store_true",
+                   help="every rank decodes the whole block file (default for .jsonl with --gpus > 1: sliced)")
     args = ap.parse_args(argv)
     return prove(args)
 

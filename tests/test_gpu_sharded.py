@@ -412,3 +412,62 @@ def test_sharded_rccl_stalled_stream_aborts(gpu_ok):
     assert "collective timeout" in lines[0], lines
     assert 2.5 < float(lines[1].split()[1]) < 20, lines
     assert lines[2] == "closed", lines
+
+
+def _sliced_worker(rank, world, port, path, q):
+    sys.path[:0] = [PKG, ORACLE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sezkp_amd
+        from sezkp_amd.ingest import TorchComm, sliced_ingest
+        ing = sliced_ingest(path, rank, world, TorchComm(), None)
+        ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
+        ctx.upload_rows(ing["blocks"], ing["row0"], ing["nrows"])
+        p = ctx.prove(ing["root"]).proof_bytes
+        ctx.close()
+        q.put((rank, hashlib.sha256(p).hexdigest(), ing["row0"], ing["nrows"]))
+    except Exception as e:
+        q.put((rank, f"ERR {type(e).__name__}: {e}", 0, 0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_sliced_upload_matches_full(gpu_ok, product, oracle, tmp_path, world):
+    """each rank ingests only its slice of a JSONL file (the
+    metadata of 1/P of the lines, then the lines over its own rows plus the
+    halo) and uploads it with sezkp_ctx_upload_rows. Ragged 333-step blocks
+    cross every rank boundary. Every rank's proof equals the oracle's proof of
+    the whole trace (bound to the file's Frontier root), and no rank holds
+    the whole trace (row slices of about n / P)."""
+    import socket
+    T, b, tau, seed = 1 << 15, 333, 3, 17
+    blocks = product.synthetic_blocks(T, b, tau, seed)
+    path = tmp_path / "b.jsonl"
+    path.write_bytes(blocks.to_jsonl())
+    root = blocks.manifest_frontier_root()
+    want = hashlib.sha256(oracle.prove_v1(blocks, root)).hexdigest()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sliced_worker, args=(r, world, port, str(path), q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for rank, digest, row0, nrows in res:
+        assert digest == want, f"rank {rank}: {digest}"
+        assert nrows < T // world + 2 * b + 2, (rank, row0, nrows)
+    # a slice that misses rows the context reads is refused
+    full = product.BlockSoA.from_jsonl(path.read_bytes())
+    c = product.ProverContext(0)
+    with pytest.raises(product.SezkpError, match="needs rows"):
+        c.upload_rows(full.with_steps(product.BlockSoA.from_jsonl_range(path.read_bytes(), 0, 0)), 0, 0)
+    c.close()

@@ -158,10 +158,12 @@ def test_prove_device_vs_host_transcript(gpu_ok, product, oracle, monkeypatch, T
     want = oracle.prove_v1(blocks, mroot)
     ctx = product.ProverContext(0)
     ctx.upload(blocks)
-    assert ctx.prove(mroot).proof_bytes == want
+    # host first, on a fresh workspace: its challenge record must not lean on
+    # what an earlier device-transcript proof left in device memory
     monkeypatch.setenv("SEZKP_HOST_TRANSCRIPT", "1")
     assert ctx.prove(mroot).proof_bytes == want
     monkeypatch.delenv("SEZKP_HOST_TRANSCRIPT")
+    assert ctx.prove(mroot).proof_bytes == want
     monkeypatch.setenv("SEZKP_DEBUG_FS_RARE", "1")
     assert ctx.prove(mroot).proof_bytes == want
     monkeypatch.delenv("SEZKP_DEBUG_FS_RARE")

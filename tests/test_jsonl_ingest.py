@@ -74,3 +74,91 @@ def test_jsonl_parallel_ranges_match_sequential(product, monkeypatch):
     monkeypatch.setenv("SEZKP_HOST_THREADS", "6")
     with pytest.raises(product.SezkpError, match=f"line {n // 3 + 1}: empty line"):
         product.BlockSoA.from_jsonl(b"\n".join(bad))
+
+
+# ------------------------------------------------ sliced ingest (config 5)
+def _sliced_worker(rank, world, port, path, q):
+    import hashlib
+    import os
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sezkp_amd.ingest import TorchComm, sliced_ingest
+        r = sliced_ingest(path, rank, world, TorchComm(), None)
+        b = r["blocks"]
+        dig = hashlib.sha256(b.input_mv.tobytes() + b.mv.tobytes() + b.has_write.tobytes() + b.wsym.tobytes())
+        q.put((rank, r["row0"], r["nrows"], dig.hexdigest(), r["root"], int(b.n_blocks), r["seconds"]["total"]))
+    except Exception as e:
+        q.put((rank, f"ERR {type(e).__name__}: {e}", 0, "", b"", 0, 0.0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sliced_ingest_matches_full_decode(product, tmp_path, world):
+    """Each rank reads 1/P of the JSONL lines' metadata, the metadata and the
+    leaf hashes are allgathered (gloo), rank 0 reduces the Frontier root, and
+    each rank decodes only the lines over its rows: ragged blocks (333 steps)
+    cross every rank boundary. Every rank's step slice equals the full
+    decode's rows [row0, row0 + nrows), and the root is the file's Frontier root."""
+    import hashlib
+    import socket
+    import torch.multiprocessing as mp
+    import numpy as np
+    from sezkp_amd.blocks import shard_rows
+    blocks = product.synthetic_blocks(1 << 14, 333, 3, 11)
+    path = tmp_path / "b.jsonl"
+    path.write_bytes(blocks.to_jsonl())
+    full = product.BlockSoA.from_file(str(path))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sliced_worker, args=(r, world, port, str(path), q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    tau = full.tau
+    for rank, row0, nrows, dig, root, nb, _ in res:
+        assert not str(row0).startswith("ERR"), row0
+        assert (row0, nrows) == shard_rows(full.step_start, rank, world)
+        want = hashlib.sha256(full.input_mv[row0:row0 + nrows].tobytes() +
+                              full.mv[row0 * tau:(row0 + nrows) * tau].tobytes() +
+                              full.has_write[row0 * tau:(row0 + nrows) * tau].tobytes() +
+                              full.wsym[row0 * tau:(row0 + nrows) * tau].tobytes()).hexdigest()
+        assert dig == want and nb == full.n_blocks and root == full.manifest_frontier_root(), rank
+    # the row slices cover the trace, overlapping only in boundary blocks
+    assert res[0][1] == 0 and res[-1][1] + res[-1][2] == full.n_rows
+    assert all(res[i][1] <= res[i + 1][1] <= res[i][1] + res[i][2] for i in range(world - 1))
+
+
+def test_jsonl_meta_ranges_cover_every_line_once(product):
+    """The metadata pass's byte ranges [len g/P, len (g+1)/P) cut at line ends
+    cover each line once for any P (including ranges with no line start), and
+    the leaf hashes give both manifest roots."""
+    import numpy as np
+    from sezkp_amd.blocks import BlockSoA, merkle_root_of_leaves
+    blocks = product.synthetic_blocks(3000, 97, 2, 3)
+    jl = blocks.to_jsonl()
+    full = BlockSoA.from_jsonl(jl)
+    for P in (1, 2, 3, 7, 16, 64):
+        parts = [BlockSoA.from_jsonl_meta(jl, len(jl) * g // P, len(jl) * (g + 1) // P) for g in range(P)]
+        allm = BlockSoA.concat_meta([p[0] for p in parts])
+        offs = np.concatenate([p[1] for p in parts])
+        assert allm.n_blocks == full.n_blocks and np.array_equal(allm.step_start, full.step_start), P
+        assert np.array_equal(offs, np.sort(offs)) and len(set(offs.tolist())) == full.n_blocks
+        leaves = b"".join(p[0].leaf_hashes() for p in parts)
+        assert merkle_root_of_leaves(leaves, False) == full.manifest_root()
+        assert merkle_root_of_leaves(leaves, True) == full.manifest_frontier_root()
+        # the full decode of a run of lines from the offsets
+        a, b = 3, 9
+        sl = BlockSoA.from_jsonl_range(jl, int(offs[a]), int(offs[b]))
+        assert np.array_equal(sl.block_id, full.block_id[a:b])
