@@ -133,7 +133,9 @@ int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], 
 /* Per-stage device times (ms) of the last prove, measured with HIP events on
  * the context's stream. Order: expand, col_commit, col_outer, compose, intt,
  * lde_ntt, deep, layer0_tree, layer0_upper, fri_fold_trees, col_openings,
- * fri_paths, total, then host wall / sync-wait / final-wait / serialize.
+ * fri_paths, total, then host wall / sync-wait / final-wait / serialize,
+ * then single launches timed only when SEZKP_KERNEL_EVENTS=1 is set (else 0):
+ * the FRI forest (k_forest16) and the three device transcript points.
  * Returns the number of values written. */
 int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max);
 /* Asynchronous proving: the context's worker thread runs the proof; wait
@@ -172,6 +174,12 @@ typedef struct sezkp_host_comm {
 } sezkp_host_comm;
 sezkp_ctx* sezkp_ctx_create_sharded_host(int32_t device, int32_t rank, int32_t world, const sezkp_host_comm* comm,
                                          char* err, size_t err_len);
+/* Rank `rank` of a `world`-GPU sharded prove ALONE on `device` (the per-rank
+ * cost model of a multi-GPU run measured on one GPU): each collective keeps
+ * only this rank's own contribution, so the rank's kernels run with their
+ * real shapes while the proof bytes are meaningless; sezkp_ctx_comm_stats
+ * still reports the bytes every collective would put on the links. */
+sezkp_ctx* sezkp_ctx_create_sharded_solo(int32_t device, int32_t rank, int32_t world, char* err, size_t err_len);
 /* Failure handling of sharded proving: a rank that fails after the first
  * collective of a prove (a HIP error, a guard trip, a peer that stops
  * answering) aborts its RCCL communicator (ncclCommAbort) and returns

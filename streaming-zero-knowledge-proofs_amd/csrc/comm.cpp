@@ -130,8 +130,34 @@ struct HostComm final : Comm {
   std::string name() const override { return "host"; }
 };
 
+// One rank of a P-rank sharded prove alone on one GPU (the per-rank cost
+// model): every collective keeps only this rank's own contribution (a local
+// copy into its slot; the peers' slots hold whatever was there), so the
+// rank's kernels run with their real shapes and the bytes each collective
+// would put on the links are recorded by the caller. The proof bytes are
+// meaningless; the timings are the rank's.
+struct SoloComm final : Comm {
+  SoloComm(int r, int w) {
+    rank = r;
+    world = w;
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    uint8_t* dst = static_cast<uint8_t*>(recv) + (size_t)rank * bytes;
+    if (dst != send) hip_check(hipMemcpyAsync(dst, send, bytes, hipMemcpyDeviceToDevice, st), "solo allgather");
+  }
+  void alltoall(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    const size_t o = (size_t)rank * bytes;
+    hip_check(hipMemcpyAsync(static_cast<uint8_t*>(recv) + o, static_cast<const uint8_t*>(send) + o, bytes,
+                             hipMemcpyDeviceToDevice, st),
+              "solo alltoall");
+  }
+  void allreduce_sum_u8(void*, size_t, hipStream_t) override {}
+  std::string name() const override { return "solo"; }
+};
+
 }  // namespace
 
+Comm* make_solo_comm(int rank, int world) { return new SoloComm(rank, world); }
 Comm* make_rccl_comm(int rank, int world, const uint8_t unique_id[128]) { return new RcclComm(rank, world, unique_id); }
 Comm* make_host_comm(int rank, int world, const sezkp_host_comm& cb) { return new HostComm(rank, world, cb); }
 void rccl_unique_id(uint8_t out[128]) {

@@ -41,6 +41,8 @@ struct Comm {
 // throws std::runtime_error on failure
 Comm* make_rccl_comm(int rank, int world, const uint8_t unique_id[128]);
 Comm* make_host_comm(int rank, int world, const sezkp_host_comm& cb);
+// one rank alone on one GPU: own contributions only (the per-rank cost model)
+Comm* make_solo_comm(int rank, int world);
 void rccl_unique_id(uint8_t out[128]);
 
 }  // namespace sezkp

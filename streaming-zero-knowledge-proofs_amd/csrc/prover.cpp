@@ -165,7 +165,7 @@ struct sezkp_ctx {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // side stream: small FRI layers overlap the forest
   hipStream_t stc = nullptr;  // copy stream: staged uploads (sezkp_ctx_stage)
-  hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr;
+  hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr, ev_deep = nullptr;
   // Trace images, double-buffered: slot[active] feeds the proofs; stage()
   // fills slot[1 - active] on the copy stream while a proof runs, and the
   // next prove() switches to it (its kernels wait for the copy on the device).
@@ -280,6 +280,10 @@ struct sezkp_ctx {
   size_t max_fri_req = 0, max_open_req = 0;
   hipEvent_t ev[ST_NSTAGE + 1]{};
   double stage_ms[ST_NSTAGE + 1]{};
+  // SEZKP_KERNEL_EVENTS=1: event pairs around single launches (the forest,
+  // the three transcript points) for live per-kernel times (bench roofline)
+  hipEvent_t kev[8]{};
+  double kernel_ms[4]{};
   // host-side split of one prove(): wall, time blocked in stream syncs,
   // final D2H wait, proof serialization (after the last sync)
   double host_ms[4]{};
@@ -430,11 +434,14 @@ struct sezkp_ctx {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     for (auto& e : coll_ev) (void)hipEventDestroy(e);
+    for (auto& e : kev)
+      if (e) (void)hipEventDestroy(e);
     if (st2) (void)hipStreamSynchronize(st2);
     if (ev_fold) (void)hipEventDestroy(ev_fold);
     if (ev_tail) (void)hipEventDestroy(ev_tail);
     if (ev_expand) (void)hipEventDestroy(ev_expand);
     if (ev_cols) (void)hipEventDestroy(ev_cols);
+    if (ev_deep) (void)hipEventDestroy(ev_deep);
     if (stc) (void)hipStreamSynchronize(stc);
     for (auto& sl : slot)
       if (sl.ready) (void)hipEventDestroy(sl.ready);
@@ -1183,6 +1190,14 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   HIP_OR_THROW(hipSetDevice(device));
   const int k = logN;
   auto rec = [&](int s) { HIP_OR_THROW(hipEventRecord(ev[s], st)); };
+  const char* kev_env = getenv("SEZKP_KERNEL_EVENTS");
+  const bool kprobe = kev_env && atoi(kev_env) != 0;
+  bool kdone[4] = {false, false, false, false};
+  auto krec = [&](int i, bool end) {
+    if (!kprobe) return;
+    HIP_OR_THROW(hipEventRecord(kev[2 * i + (end ? 1 : 0)], st));
+    if (end) kdone[i] = true;
+  };
   static const bool sync_debug = getenv("SEZKP_SYNC_DEBUG") != nullptr;  // name the failing kernel
   auto ok = [&](hipError_t e, const char* what) {
     if (e == hipSuccess && sync_debug) e = hipStreamSynchronize(st);
@@ -1331,7 +1346,15 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     for (int j = 0; j < 4; j++) h_chal->mask[j] = mask[j];
     zn = hgl_pow(z, n);
   } else {
-    ok(launch_fs_point(st, fs_args(1, mroot)), "fs_point1");
+    const FsArgs a1 = fs_args(1, mroot);
+    krec(1, false);
+    ok(launch_fs_point(st, a1), "fs_point1");
+    krec(1, true);
+    // the DEEP constants' chain of products beside the composition (side stream)
+    HIP_OR_THROW(hipEventRecord(ev_fold, st));
+    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+    ok(launch_fs_deep(st2, a1), "fs_deep");
+    HIP_OR_THROW(hipEventRecord(ev_deep, st2));
   }
   // ---- composition (this rank's rows), DEEP quotient, INTT
   mark("z_done");
@@ -1384,19 +1407,18 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
          [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
   rec(4);
   if (dq) {
-    if (sharded) {
-      const uint64_t nrows = row_hi - row_lo, per = 4096;
-      ok(launch_inv_base(st, d_base, d_lde, d_dq_part, logn, d_chal, tw, row_lo, nrows), "inv_base");
+    // inverses + partial sums need z only; the q tables wait for the DEEP
+    // constants of the side-stream kernel (device transcript)
+    const uint64_t nrows = row_hi - row_lo, per = 4096;
+    ok(launch_inv_base(st, d_base, d_lde, d_dq_part, logn, d_chal, tw, row_lo, nrows), "inv_base");
+    if (sharded)
       coll("fz_partials", P1 * (nrows / per) * 8,
            [&] { comm->allgather(d_dq_part + row_lo / per, d_dq_part, (size_t)(nrows / per) * 8, st); });
-      ok(launch_q_tables(st, d_base, d_lde, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, row_lo, nrows),
-         "q_tables");
-      if (!dist_intt)
-        coll("q_values", P1 * nrows * 8, [&] { comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st); });
-    } else {
-      ok(launch_deep_quotient(st, d_base, d_lde, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, tw),
-         "deep_quotient");
-    }
+    if (!host_tr) HIP_OR_THROW(hipStreamWaitEvent(st, ev_deep, 0));
+    ok(launch_q_tables(st, d_base, d_lde, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, row_lo, nrows),
+       "q_tables");
+    if (sharded && !dist_intt)
+      coll("q_values", P1 * nrows * 8, [&] { comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st); });
   }
   if (dist_intt) {
     const uint64_t m = n >> logP, Q = m >> logP;
@@ -1462,7 +1484,9 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     for (int r = 0; r < k; r++) h_chal->beta[r] = rd64(bb.data() + 8 * r) % GL_P_HOST;
     HIP_OR_THROW(hipMemcpyAsync(d_chal->beta, h_chal->beta, 8 * (size_t)k, hipMemcpyHostToDevice, st));
   } else {
+    krec(2, false);
     ok(launch_fs_point(st, fs_args(2, mroot)), "fs_point2");
+    krec(2, true);
   }
 
   // ---- FRI folds + layer trees (prover.rs:192-239). Folds of run layers are
@@ -1513,7 +1537,9 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   // workgroups (sharded: their own kernel on the side stream)
   if (tail_merged) {
     const TailArgs ta = tail_args(rep_src);
+    krec(0, false);
     ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf, 0), "fri_forest");
+    krec(0, true);
   } else {
     if (!sharded) launch_tail(rep_src);
     ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
@@ -1620,7 +1646,9 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
       push_open(0, row);  // input_mv
     }
   } else {
+    krec(3, false);
     ok(launch_fs_point(st, fs_args(3, mroot)), "fs_point3");
+    krec(3, true);
     // grids sized for the most requests this rank can own; the kernels read the counts
     nf = sharded ? max_fri_req : (size_t)NUM_QUERIES * 2 * k;
     no = sharded ? max_open_req : (size_t)NUM_QUERIES * (3 + 9 * tau);
@@ -1672,6 +1700,10 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   float tot = 0;
   (void)hipEventElapsedTime(&tot, ev[0], ev[ST_NSTAGE]);
   stage_ms[ST_NSTAGE] = tot;
+  for (int i = 0; i < 4; i++) {
+    float ms = 0;
+    kernel_ms[i] = kdone[i] && hipEventElapsedTime(&ms, kev[2 * i], kev[2 * i + 1]) == hipSuccess ? ms : 0.0;
+  }
   have_times = true;
   // an event pair not recorded on this path fails above; that error must not
   // surface as the next launch's hipGetLastError()
@@ -1745,7 +1777,7 @@ static void to_buf(const std::vector<uint8_t>& v, sezkp_buf* out) {
 static void to_buf(const std::string& s, sezkp_buf* out) { to_buf(std::vector<uint8_t>(s.begin(), s.end()), out); }
 
 static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const uint8_t* uid,
-                             const sezkp_host_comm* hc, char* err, size_t err_len) {
+                             const sezkp_host_comm* hc, char* err, size_t err_len, bool solo = false) {
   try {
     if (world < 1 || world > 8 || (world & (world - 1)) || rank < 0 || rank >= world)
       throw Err{SEZKP_E_INVALID, "world must be a power of two <= 8 and 0 <= rank < world"};
@@ -1760,18 +1792,21 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     HIP_OR_THROW(hipSetDevice(device));
     HIP_OR_THROW(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto& e : c->ev) HIP_OR_THROW(hipEventCreate(&e));
+    for (auto& e : c->kev) HIP_OR_THROW(hipEventCreate(&e));
     HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_cols, hipEventDisableTiming));
+    HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_deep, hipEventDisableTiming));
     c->tw = tables_for_device(device);
     // SEZKP_FORCE_SHARDED=1 runs the sharded algorithm (and its RCCL calls)
     // with a one-rank communicator: tests it on a single GPU
     const bool force = uid && getenv("SEZKP_FORCE_SHARDED") != nullptr;
-    if (world > 1 || force) {
+    if (world > 1 || force || solo) {
       try {
-        c->comm.reset(hc ? make_host_comm(rank, world, *hc) : make_rccl_comm(rank, world, uid));
+        c->comm.reset(solo ? make_solo_comm(rank, world)
+                           : hc ? make_host_comm(rank, world, *hc) : make_rccl_comm(rank, world, uid));
       } catch (const std::exception& e) {
         throw Err{SEZKP_E_DEVICE, e.what()};
       }
@@ -1803,6 +1838,9 @@ sezkp_ctx* sezkp_ctx_create_sharded_host(int32_t device, int32_t rank, int32_t w
     return nullptr;
   }
   return ctx_create(device, rank, world, nullptr, comm, err, err_len);
+}
+sezkp_ctx* sezkp_ctx_create_sharded_solo(int32_t device, int32_t rank, int32_t world, char* err, size_t err_len) {
+  return ctx_create(device, rank, world, nullptr, nullptr, err, err_len, true);
 }
 int32_t sezkp_comm_unique_id(uint8_t out[128], char* err, size_t err_len) {
   try {
@@ -1987,6 +2025,7 @@ int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max)
   int cnt = 0;
   for (int s = 0; s <= ST_NSTAGE && cnt < max; s++) out_ms[cnt++] = ctx->stage_ms[s];
   for (int s = 0; s < 4 && cnt < max; s++) out_ms[cnt++] = ctx->host_ms[s];
+  for (int s = 0; s < 4 && cnt < max; s++) out_ms[cnt++] = ctx->kernel_ms[s];
   return cnt;
 }
 void* sezkp_ctx_stream(const sezkp_ctx* ctx) { return ctx ? (void*)ctx->st : nullptr; }

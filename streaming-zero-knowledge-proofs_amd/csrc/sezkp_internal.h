@@ -295,6 +295,9 @@ struct FsArgs {
   FsQueryArgs q;
 };
 hipError_t launch_fs_point(hipStream_t st, const FsArgs& a);
+// the DEEP-polynomial constants (DevChal z^n, K1, K2, rho, rho^4096, status)
+// from the z of point 1: one thread, meant for a side stream
+hipError_t launch_fs_deep(hipStream_t st, const FsArgs& a);
 
 // kernels launched by the host orchestrator (prover.cpp)
 // blocks [blk_lo, blk_lo + blk_cnt) only (a sharded rank's rows + one row of halo)

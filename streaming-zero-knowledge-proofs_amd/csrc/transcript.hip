@@ -126,12 +126,153 @@ struct RootNode {
 
 }  // namespace
 
+// Point 3: query rows (mod n) and FRI positions (mod N), the path and
+// opening requests this rank owns, in proof order, and the proof-body fields
+// the host used to write (counts, query headers, FRI roots, positions, final
+// value, manifest root; prover.rs:242-297, proof.rs:80-98). Items run in
+// canonical order, one contiguous run per thread; a workgroup scan of the
+// owned counts places them (every item is owned on one device).
+// FRI item i: query q = i / 2k, layer r, side (the ordinal is i); opening item
+// j: query q = j / (9 tau + 3), slot t = j % (9 tau + 3) (the ordinal is j).
+__device__ __forceinline__ void fri_item(const FsQueryArgs& Q, const uint64_t* pos0, int k, uint64_t N, uint32_t i,
+                                         uint32_t& r, uint64_t& idx, bool& own) {
+  const uint32_t q = i / (2 * k), rem = i % (2 * k), side = rem & 1;
+  r = rem >> 1;
+  const uint64_t p = pos0[q] & ((N >> r) - 1), half = N >> (r + 1);  // p_r = p_0 mod 2^(k - r)
+  idx = side ? (p ^ half) : p;
+  own = ((Q.sharded && (int)r <= Q.rR) ? (uint32_t)((idx >> L16_LOG) & (Q.world - 1)) : 0u) == Q.rank;
+}
+__device__ __forceinline__ void open_item(const FsQueryArgs& Q, const uint64_t* rows, uint64_t n, int logn,
+                                          uint32_t j, uint32_t& c, uint64_t& row, bool& own) {
+  const uint32_t tau = Q.tau, nopen = 9 * tau + 3, q = j / nopen, t = j % nopen;
+  const uint64_t rw = rows[q], ip1 = rw + 1 < n ? rw + 1 : 0;  // next_wrap
+  if (t < 9 * tau) {  // per tape: mv, next_mv, wflag, wsym, head, next_head, winlen, in_off, out_off
+    const uint32_t tp = t / 9, kd = t % 9;
+    const uint32_t kind = kd == 0 || kd == 1 ? 0 : kd == 2 ? 1 : kd == 3 ? 2 : kd == 4 || kd == 5 ? 3 : kd - 2;
+    c = 3 + kind * tau + tp;
+    row = (kd == 1 || kd == 5) ? ip1 : rw;
+  } else {  // is_first, is_last, input_mv
+    c = t == 9 * tau ? 1u : t == 9 * tau + 1 ? 2u : 0u;
+    row = rw;
+  }
+  const uint64_t chn = logn >= COL_CHUNK_LOG2 ? row >> COL_CHUNK_LOG2 : 0;
+  own = chn >= Q.ch_lo && chn < Q.ch_hi;
+}
+// exclusive workgroup scan of one count per thread
+__device__ __forceinline__ uint32_t wg_scan(uint32_t v, uint32_t* sm, uint32_t& total) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sm[wave] = x;
+  __syncthreads();
+  uint32_t base = 0;
+  total = 0;
+  for (int w = 0; w < FS_THREADS / 64; w++) {
+    if (w < wave) base += sm[w];
+    total += sm[w];
+  }
+  __syncthreads();
+  return base + x - v;
+}
+__device__ void fs_queries(const FsArgs& A, DevChal* D, int tid) {
+  __shared__ uint64_t s_row[FS_NQ], s_pos[FS_NQ];
+  __shared__ uint32_t s_sum[FS_THREADS / 64];
+  const FsQueryArgs& Q = A.q;
+  const uint64_t n = 1ULL << A.logn, N = 1ULL << A.logN;
+  const int k = A.logN;
+  if (tid < FS_NQ) {
+    s_row[tid] = rd64(A.out + A.out_rowq + 8 * tid) & (n - 1);
+    s_pos[tid] = rd64(A.out + A.out_rowq + 8 * FS_NQ + 8 * tid) & (N - 1);
+    D->rows[tid] = s_row[tid];
+    D->frows[tid] = s_pos[tid];
+  }
+  __syncthreads();
+  // FRI path requests (layer, index, ordinal)
+  const uint32_t MF = FS_NQ * 2 * (uint32_t)k, perF = (MF + FS_THREADS - 1) / FS_THREADS;
+  const uint32_t f0 = tid * perF, f1 = min(MF, f0 + perF);
+  uint32_t cnt = 0, total;
+  for (uint32_t i = f0; i < f1; i++) {
+    uint32_t r;
+    uint64_t idx;
+    bool own;
+    fri_item(Q, s_pos, k, N, i, r, idx, own);
+    cnt += own;
+  }
+  uint32_t at = wg_scan(cnt, s_sum, total);
+  for (uint32_t i = f0; i < f1; i++) {
+    uint32_t r;
+    uint64_t idx;
+    bool own;
+    fri_item(Q, s_pos, k, N, i, r, idx, own);
+    if (!own) continue;
+    uint32_t* rq = Q.req + 3 * (uint64_t)at++;
+    rq[0] = r;
+    rq[1] = (uint32_t)idx;
+    rq[2] = i;
+  }
+  if (tid == 0) D->counts[0] = total;
+  // column openings (column, row lo, row hi, ordinal, dictionary index)
+  const uint32_t MO = FS_NQ * (9 * Q.tau + 3), perO = (MO + FS_THREADS - 1) / FS_THREADS;
+  const uint32_t o0 = tid * perO, o1 = min(MO, o0 + perO);
+  cnt = 0;
+  for (uint32_t j = o0; j < o1; j++) {
+    uint32_t c;
+    uint64_t row;
+    bool own;
+    open_item(Q, s_row, n, A.logn, j, c, row, own);
+    cnt += own;
+  }
+  at = wg_scan(cnt, s_sum, total);
+  uint32_t* orq = Q.req + 3 * Q.max_fri_req;
+  for (uint32_t j = o0; j < o1; j++) {
+    uint32_t c;
+    uint64_t row;
+    bool own;
+    open_item(Q, s_row, n, A.logn, j, c, row, own);
+    if (!own) continue;
+    uint32_t* rq = orq + OPEN_REQ_WORDS * (uint64_t)at++;
+    rq[0] = c;
+    rq[1] = (uint32_t)row;
+    rq[2] = (uint32_t)(row >> 32);
+    rq[3] = j;
+    rq[4] = Q.dict_of[c];
+  }
+  if (tid == 0) D->counts[1] = total;
+  if (Q.rank != 0) return;  // sharded: one writer per byte (the image is byte-summed)
+  // body fields (proof.rs:80-98)
+  uint64_t* body = reinterpret_cast<uint64_t*>(Q.PL.base);
+  for (uint32_t i = tid; i < FS_NQ * ((uint32_t)k + 1); i += FS_THREADS) {  // FRI positions
+    const uint32_t q = i / (k + 1), r = i % (k + 1);
+    body[(Q.PL.fq_off + 8 + q * Q.PL.fq_bytes) / 8 + 1 + r] = s_pos[q] & ((N >> r) - 1);
+  }
+  if (tid < FS_NQ) {
+    uint64_t* fq = body + (Q.PL.fq_off + 8 + tid * Q.PL.fq_bytes) / 8;
+    fq[0] = (uint64_t)k + 1;
+    fq[2 + k] = (uint64_t)k;
+    uint64_t* qh = body + (8 + tid * Q.PL.q_bytes) / 8;
+    qh[0] = s_row[tid];
+    qh[1] = Q.tau;
+  }
+  if (tid == 0) {
+    body[0] = FS_NQ;
+    body[Q.PL.fr_off / 8] = (uint64_t)k + 1;
+    body[Q.PL.fq_off / 8] = FS_NQ;
+    body[Q.PL.tail_off / 8] = Q.final_val[0];
+  }
+  uint32_t* b32 = Q.PL.base;
+  for (int i = tid; i < 8 * (k + 1); i += FS_THREADS) b32[(Q.PL.fr_off + 8) / 4 + i] = A.friroots[i];
+  if (tid < 8) b32[(Q.PL.tail_off + 8) / 4 + tid] = A.mroot[tid];
+}
+
 __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   __shared__ __attribute__((aligned(16))) uint8_t S[FS_S_MAX];
   __shared__ uint32_t qm[FS_QUADS][16];
   __shared__ uint32_t qstack[FS_MAX_CHAL][10][8];
   __shared__ RootNode rn[FS_MAX_CHAL];
-  __shared__ uint32_t s_cnt[2][FS_NQ + 1];
   const int tid = threadIdx.x, li = tid & 3, quad = tid >> 2;
   uint32_t* m = qm[quad];
 
@@ -337,177 +478,67 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   DevChal* D = A.ch;
   if (A.point == 1) {
     const uint8_t* o = A.out + A.out_alpha;
-    if (tid < 8) D->alpha[tid] = gl_canon_mod(rd64(o + 8 * tid));
-    else if (tid < 12) D->mask[tid - 8] = gl_canon_mod(rd64(o + 64 + 8 * (tid - 8)));
+    if (tid >= 1 && tid < 9) D->alpha[tid - 1] = gl_canon_mod(rd64(o + 8 * (tid - 1)));
+    else if (tid >= 9 && tid < 13) D->mask[tid - 9] = gl_canon_mod(rd64(o + 64 + 8 * (tid - 9)));
     if (tid == 0) {
-      // OOD point + coset nudge (prover.rs:119-135): while (z / 3)^N == 1, z += 1
+      // OOD point + coset nudge (prover.rs:119-135): while (z / 3)^N == 1, z += 1.
+      // The DEEP constants follow in k_fs_deep, beside the composition.
       uint64_t z = gl_canon_mod(rd64(o + 96));
       for (;;) {
         const uint64_t t = gl_pow2k_dev(gl_mul(z, A.inv3), A.logN);
         if (t != 1) break;
         z = gl_add(z, 1);
       }
-      // DEEP as the LDE of q + c S (DeepPoly): z^n, f(z) = K1 S, c' = f(z) K2
-      const uint64_t zn = gl_pow2k_dev(z, A.logn);
-      const uint64_t zN = gl_pow2k_dev(zn, A.logN - A.logn);
-      const uint64_t Dd = gl_sub(A.threeN, zN);
-      // one inversion for 1/z and 1/(3^N - z^N)
-      const uint64_t inv_zD = (z == 0 || Dd == 0) ? 0 : gl_inv(gl_mul(z, Dd));
-      const uint64_t inv_z = gl_mul(inv_zD, Dd), inv_D = gl_mul(inv_zD, z);
-      const uint64_t K1 = gl_mul(gl_sub(1, zn), A.inv_n);
-      uint64_t K2 = gl_mul(gl_mul(zN, inv_z), inv_D);  // z^(N-1) / (3^N - z^N)
-      const uint64_t rho = gl_mul(gl_mul(3, inv_z), A.w_rank);
-      const uint64_t rhoM = gl_pow2k_dev(rho, A.logN - A.logP);
-      uint64_t G = 0, pw = 1;
-      for (int t = 0; t < (1 << A.logP); t++) {
-        G = gl_add(G, pw);
-        pw = gl_mul(pw, rhoM);
-      }
-      K2 = gl_mul(K2, G);
       D->z = z;
-      D->zn = zn;
-      D->K1 = K1;
-      D->K2 = K2;
-      D->rho = rho;
-      D->rho4096 = gl_pow2k_dev(rho, 12);
-      // the polynomial form needs z off the base domain and z != 0: otherwise
-      // the host proves again with its own transcript (per-point DEEP)
-      const uint32_t rare = (z == 0 || zn == 1 || Dd == 0) ? 1u : 0u;
-      A.status[1] = rare;
     }
   } else if (A.point == 2) {
     const uint8_t* o = A.out + A.out_beta;
     for (int r = tid; r < A.logN; r += FS_THREADS) D->beta[r] = gl_canon_mod(rd64(o + 8 * r));
   } else if (A.point == 3) {
-    const FsQueryArgs& Q = A.q;
-    const uint64_t n = 1ULL << A.logn, N = 1ULL << A.logN;
-    const int k = A.logN;
-    const uint32_t tau = Q.tau, nopen = 9 * tau + 3;
-    uint64_t row = 0, pos0 = 0;
-    uint32_t nf_q = 0, no_q = 0;
-    if (tid < FS_NQ) {
-      row = rd64(A.out + A.out_rowq + 8 * tid) & (n - 1);
-      pos0 = rd64(A.out + A.out_rowq + 8 * FS_NQ + 8 * tid) & (N - 1);
-      D->rows[tid] = row;
-      D->frows[tid] = pos0;
-      // requests this rank owns (run layers by run owner, the rest on rank 0;
-      // openings by the owner of the row's chunk)
-      uint64_t p = pos0, len = N;
-      for (int r = 0; r < k; r++) {
-        const uint64_t half = len >> 1;
-        for (int side = 0; side < 2; side++) {
-          const uint64_t idx = side ? (p ^ half) : p;
-          const uint32_t owner = (Q.sharded && r <= Q.rR) ? (uint32_t)((idx >> L16_LOG) & (Q.world - 1)) : 0u;
-          nf_q += owner == Q.rank;
-        }
-        p %= half;
-        len = half;
-      }
-      const uint64_t ip1 = row + 1 < n ? row + 1 : 0;
-      const uint64_t chr = A.logn >= COL_CHUNK_LOG2 ? row >> COL_CHUNK_LOG2 : 0;
-      const uint64_t chn = A.logn >= COL_CHUNK_LOG2 ? ip1 >> COL_CHUNK_LOG2 : 0;
-      const bool own_r = chr >= Q.ch_lo && chr < Q.ch_hi, own_n = chn >= Q.ch_lo && chn < Q.ch_hi;
-      no_q = (own_r ? 7 * tau + 3 : 0) + (own_n ? 2 * tau : 0);
-      s_cnt[0][tid + 1] = nf_q;
-      s_cnt[1][tid + 1] = no_q;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      s_cnt[0][0] = 0;
-      s_cnt[1][0] = 0;
-      for (int q = 1; q <= FS_NQ; q++) {
-        s_cnt[0][q] += s_cnt[0][q - 1];
-        s_cnt[1][q] += s_cnt[1][q - 1];
-      }
-      D->counts[0] = s_cnt[0][FS_NQ];
-      D->counts[1] = s_cnt[1][FS_NQ];
-    }
-    __syncthreads();
-    uint64_t* body = reinterpret_cast<uint64_t*>(Q.PL.base);
-    const bool write_body = Q.rank == 0;  // sharded: one writer per byte (the image is byte-summed)
-    if (tid < FS_NQ) {
-      const int q = tid;
-      // FRI path requests (layer, index, ordinal in the proof's FRI records)
-      uint32_t* fr = Q.req + 3 * s_cnt[0][q];
-      uint64_t p = pos0, len = N;
-      uint64_t* fq = body + (Q.PL.fq_off + 8 + q * Q.PL.fq_bytes) / 8;
-      if (write_body) {
-        fq[0] = (uint64_t)k + 1;
-        fq[1] = pos0;
-      }
-      uint32_t nf = 0;
-      for (int r = 0; r < k; r++) {
-        const uint64_t half = len >> 1;
-        for (int side = 0; side < 2; side++) {
-          const uint64_t idx = side ? (p ^ half) : p;
-          const uint32_t owner = (Q.sharded && r <= Q.rR) ? (uint32_t)((idx >> L16_LOG) & (Q.world - 1)) : 0u;
-          if (owner == Q.rank) {
-            fr[3 * nf] = (uint32_t)r;
-            fr[3 * nf + 1] = (uint32_t)idx;
-            fr[3 * nf + 2] = (uint32_t)(q * 2 * k + 2 * r + side);
-            nf++;
-          }
-        }
-        p %= half;
-        len = half;
-        if (write_body) fq[2 + r] = p;
-      }
-      if (write_body) {
-        fq[2 + k] = (uint64_t)k;
-        uint64_t* qh = body + (8 + q * Q.PL.q_bytes) / 8;
-        qh[0] = row;
-        qh[1] = tau;
-      }
-      // column openings in proof order (prover.rs:252-292, proof.rs:44-66)
-      uint32_t* orq = Q.req + 3 * Q.max_fri_req + OPEN_REQ_WORDS * s_cnt[1][q];
-      const uint64_t ip1 = row + 1 < n ? row + 1 : 0;
-      uint32_t no = 0, ord = (uint32_t)q * nopen;
-      auto push = [&](uint32_t c, uint64_t rw) {
-        const uint64_t chn = A.logn >= COL_CHUNK_LOG2 ? rw >> COL_CHUNK_LOG2 : 0;
-        if (chn >= Q.ch_lo && chn < Q.ch_hi) {
-          uint32_t* rq = orq + OPEN_REQ_WORDS * no;
-          rq[0] = c;
-          rq[1] = (uint32_t)rw;
-          rq[2] = (uint32_t)(rw >> 32);
-          rq[3] = ord;
-          rq[4] = Q.dict_of[c];
-          no++;
-        }
-        ord++;
-      };
-      for (uint32_t r = 0; r < tau; r++) {
-        push(3 + 0 * tau + r, row);
-        push(3 + 0 * tau + r, ip1);
-        push(3 + 1 * tau + r, row);
-        push(3 + 2 * tau + r, row);
-        push(3 + 3 * tau + r, row);
-        push(3 + 3 * tau + r, ip1);
-        push(3 + 4 * tau + r, row);
-        push(3 + 5 * tau + r, row);
-        push(3 + 6 * tau + r, row);
-      }
-      push(1, row);
-      push(2, row);
-      push(0, row);
-    }
-    if (write_body) {
-      // counts, FRI roots, final value, manifest root (proof.rs:80-98)
-      if (tid == 0) {
-        body[0] = FS_NQ;
-        body[Q.PL.fr_off / 8] = (uint64_t)k + 1;
-        body[Q.PL.fq_off / 8] = FS_NQ;
-        body[Q.PL.tail_off / 8] = Q.final_val[0];
-      }
-      uint32_t* b32 = Q.PL.base;
-      for (int i = tid; i < 8 * (k + 1); i += FS_THREADS) b32[(Q.PL.fr_off + 8) / 4 + i] = A.friroots[i];
-      if (tid < 8) b32[(Q.PL.tail_off + 8) / 4 + tid] = A.mroot[tid];
-    }
+    fs_queries(A, D, tid);
   }
+}
+
+// DEEP-polynomial constants from z (DeepPoly, sezkp_internal.h): z^n, K1 =
+// (1 - z^n) / n, K2 = z^(N-1) / (3^N - z^N) * G, rho = (3 / z) w_N^rank,
+// rho^4096 and the status flag for a z the polynomial form cannot use. One
+// serial chain of ~130 products: it runs on the side stream beside the
+// composition kernel, which needs only the alphas and masks.
+__global__ void __launch_bounds__(64) k_fs_deep(FsArgs A) {
+  if (threadIdx.x != 0) return;
+  DevChal* D = A.ch;
+  const uint64_t z = D->z;
+  const uint64_t zn = gl_pow2k_dev(z, A.logn);
+  const uint64_t zN = gl_pow2k_dev(zn, A.logN - A.logn);
+  const uint64_t Dd = gl_sub(A.threeN, zN);
+  // one inversion for 1/z and 1/(3^N - z^N)
+  const uint64_t inv_zD = (z == 0 || Dd == 0) ? 0 : gl_inv(gl_mul(z, Dd));
+  const uint64_t inv_z = gl_mul(inv_zD, Dd), inv_D = gl_mul(inv_zD, z);
+  uint64_t K2 = gl_mul(gl_mul(zN, inv_z), inv_D);  // z^(N-1) / (3^N - z^N)
+  const uint64_t rho = gl_mul(gl_mul(3, inv_z), A.w_rank);
+  const uint64_t rhoM = gl_pow2k_dev(rho, A.logN - A.logP);
+  uint64_t G = 0, pw = 1;
+  for (int t = 0; t < (1 << A.logP); t++) {
+    G = gl_add(G, pw);
+    pw = gl_mul(pw, rhoM);
+  }
+  D->zn = zn;
+  D->K1 = gl_mul(gl_sub(1, zn), A.inv_n);
+  D->K2 = gl_mul(K2, G);
+  D->rho = rho;
+  D->rho4096 = gl_pow2k_dev(rho, 12);
+  // the polynomial form needs z off the base domain and z != 0: otherwise
+  // the host proves again with its own transcript (per-point DEEP)
+  A.status[1] = (z == 0 || zn == 1 || Dd == 0) ? 1u : 0u;
 }
 
 hipError_t launch_fs_point(hipStream_t st, const FsArgs& a) {
   if (a.s_bytes > FS_S_MAX || a.nchal > FS_MAX_CHAL || (a.point == 3 && a.logN > 63)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_fs_point, dim3(1), dim3(FS_THREADS), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_fs_deep(hipStream_t st, const FsArgs& a) {
+  hipLaunchKernelGGL(k_fs_deep, dim3(1), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 

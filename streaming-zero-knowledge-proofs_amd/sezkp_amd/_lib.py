@@ -34,6 +34,7 @@ EXPORTS = [
     "sezkp_merkle_build", "sezkp_merkle_paths", "sezkp_manifest_frontier_root", "sezkp_ctx_comm_stats",
     "sezkp_fs_xof", "sezkp_ctx_upload_rows", "sezkp_shard_rows", "sezkp_blocks_decode_jsonl_meta",
     "sezkp_blocks_line_offsets", "sezkp_manifest_leaf_hashes", "sezkp_merkle_root_of_leaves",
+    "sezkp_ctx_create_sharded_solo",
 ]
 
 
@@ -158,6 +159,8 @@ def _load():
     L.sezkp_blocks_line_offsets.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.c_size_t)]
     L.sezkp_manifest_leaf_hashes.argtypes = [C.POINTER(BlockView), C.c_void_p]
     L.sezkp_merkle_root_of_leaves.argtypes = [C.c_char_p, C.c_size_t, C.c_int32, C.c_char_p]
+    L.sezkp_ctx_create_sharded_solo.restype = C.c_void_p
+    L.sezkp_ctx_create_sharded_solo.argtypes = [C.c_int32, C.c_int32, C.c_int32] + E
     return L
 
 

@@ -17,7 +17,9 @@ from .blocks import BlockSoA
 STAGES = ["expand", "col_commit", "col_outer", "compose", "intt", "lde_ntt", "deep", "layer0_tree",
           "layer0_upper", "fri_fold_trees", "col_openings", "fri_paths", "total",
           # host-side split of the same prove() call (wall clock)
-          "host_wall", "host_sync_wait", "host_final_wait", "host_serialize"]
+          "host_wall", "host_sync_wait", "host_final_wait", "host_serialize",
+          # single launches (SEZKP_KERNEL_EVENTS=1; 0 when not recorded)
+          "k_forest16", "fs_point1", "fs_point2", "fs_point3"]
 
 
 @dataclass
@@ -227,6 +229,8 @@ class ShardedProverContext(ProverContext):
     rank 0 and broadcast over the torch.distributed `group`. comm="host":
     the exchanges are staged through host memory and run over the (gloo)
     `group` by `sezkp_amd.dist.HostCollectives` — for tests on one GPU.
+    comm="solo": this rank alone on `device` with its own contributions only
+    (no group): the per-rank cost model; timings real, proof bytes not.
     """
 
     def __init__(self, rank: int, world: int, device: int = 0, comm: str = "rccl", group=None):
@@ -243,6 +247,8 @@ class ShardedProverContext(ProverContext):
             if world > 1:
                 dist.broadcast_object_list(obj, src=0, group=group)
             self._h = lib.sezkp_ctx_create_sharded(device, rank, world, obj[0], err, 1024)
+        elif comm == "solo":
+            self._h = lib.sezkp_ctx_create_sharded_solo(device, rank, world, err, 1024)
         elif comm == "host":
             from .dist import HostCollectives
             self._coll = HostCollectives(group)

@@ -59,6 +59,8 @@ def test_silent_death_is_noticed():
 
 def test_timeout_ends_the_job():
     ps, q = _spawn([_ok, _hang])
-    res, err = _collect(ps, q, 3)
-    assert err.startswith("timeout after 3 s (1 of 2 ranks reported)")
+    # long enough for the spawned rank to start and report under a loaded
+    # test run (a spawn child imports the launcher's module)
+    res, err = _collect(ps, q, 20)
+    assert err.startswith("timeout after 20 s (1 of 2 ranks reported)")
     assert not any(p.is_alive() for p in ps)
