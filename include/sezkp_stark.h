@@ -296,6 +296,11 @@ void sezkp_blocks_free(sezkp_blocks* b);
  * sezkp_blocks_decode_jsonl on data + off[a] .. data + off[b]. */
 int32_t sezkp_blocks_decode_jsonl_meta(const uint8_t* data, size_t len, uint64_t lo, uint64_t hi, sezkp_blocks** out,
                                        char* err, size_t err_len);
+/* The same lines decoded in full when steps != 0 (the blocks of
+ * sezkp_blocks_decode_jsonl on those lines, plus their offsets): a rank
+ * decodes its own byte range once and takes its row slice from it. */
+int32_t sezkp_blocks_decode_jsonl_lines(const uint8_t* data, size_t len, uint64_t lo, uint64_t hi, int32_t steps,
+                                        sezkp_blocks** out, char* err, size_t err_len);
 int32_t sezkp_blocks_line_offsets(const sezkp_blocks* b, const uint64_t** offsets, size_t* n);
 /* The manifest leaf hashes (sezkp-merkle lib.rs:85-117, 32 bytes per block)
  * and a root over given leaves: the batch merkle_root (frontier = 0,

@@ -10,6 +10,9 @@
 #include <stdexcept>
 #include <system_error>
 #include <thread>
+#include <type_traits>
+
+#include <emmintrin.h>
 
 #include "host_crypto.h"
 
@@ -194,8 +197,82 @@ class Json {
   uint64_t skip_count_array() {
     ws();
     expect('[');
+    ws();
+    if (p_ < e_ && *p_ == ']') {
+      p_++;
+      first_ = false;
+      return 0;
+    }
+    // 64 bytes per step: SSE2 byte masks of '"', '\\', '[' '{', ']' '}' and
+    // ',', the in-string mask as the prefix XOR of the quotes (carried across
+    // blocks), and only the structural bytes outside strings walked in order.
+    // A backslash sends the array to the exact byte scan.
+    const char* const start = p_;
+    const char* p = p_;
+    uint64_t carry = 0, commas = 0;
+    int depth = 1;
+    auto eq = [](__m128i v, char c) { return _mm_cmpeq_epi8(v, _mm_set1_epi8(c)); };
+    while (e_ - p >= 64) {
+      uint64_t Q = 0, B = 0, O = 0, C = 0, M = 0;
+      for (int i = 0; i < 4; i++) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * i));
+        const int sh = 16 * i;
+        Q |= (uint64_t)(uint32_t)_mm_movemask_epi8(eq(v, '"')) << sh;
+        B |= (uint64_t)(uint32_t)_mm_movemask_epi8(eq(v, '\\')) << sh;
+        O |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_or_si128(eq(v, '['), eq(v, '{'))) << sh;
+        C |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_or_si128(eq(v, ']'), eq(v, '}'))) << sh;
+        M |= (uint64_t)(uint32_t)_mm_movemask_epi8(eq(v, ',')) << sh;
+      }
+      if (B) return skip_count_exact(start);
+      uint64_t S = Q;  // prefix XOR: bit i = parity of the quotes at or before i
+      S ^= S << 1; S ^= S << 2; S ^= S << 4; S ^= S << 8; S ^= S << 16; S ^= S << 32;
+      S ^= carry;
+      carry = 0 - (S >> 63);
+      uint64_t X = (O | C | M) & ~S;
+      while (X) {
+        const uint64_t bit = X & (0 - X);
+        X ^= bit;
+        if (O & bit) {
+          depth++;
+        } else if (C & bit) {
+          if (--depth == 0) {
+            p_ = p + __builtin_ctzll(bit) + 1;
+            first_ = false;
+            return commas + 1;
+          }
+        } else {
+          commas += depth == 1;
+        }
+      }
+      p += 64;
+    }
+    // the last < 64 bytes (no backslash so far): byte by byte from the state
+    bool instr = carry & 1;
+    while (p < e_) {
+      const char c = *p++;
+      if (c == '\\') return skip_count_exact(start);
+      if (instr) {
+        instr = c != '"';
+      } else if (c == '"') {
+        instr = true;
+      } else if (c == '[' || c == '{') {
+        depth++;
+      } else if (c == ']' || c == '}') {
+        if (--depth == 0) {
+          p_ = p;
+          first_ = false;
+          return commas + 1;
+        }
+      } else if (c == ',') {
+        commas += depth == 1;
+      }
+    }
+    throw DecodeError("truncated JSON array");
+  }
+  // the same count byte by byte with escapes honoured, from the first element
+  uint64_t skip_count_exact(const char* start) {
+    p_ = start;
     uint64_t commas = 0;
-    bool any = false;
     int depth = 1;
     while (p_ < e_) {
       const char c = *p_++;
@@ -203,22 +280,76 @@ class Json {
         while (p_ < e_ && *p_ != '"') p_ += *p_ == '\\' ? 2 : 1;
         if (p_ >= e_) break;
         p_++;
-        any = true;
       } else if (c == '[' || c == '{') {
         depth++;
-        any = true;
       } else if (c == ']' || c == '}') {
         if (--depth == 0) {
           first_ = false;
-          return any ? commas + 1 : 0;
+          return commas + 1;
         }
       } else if (c == ',') {
-        if (depth == 1) commas++;
-      } else if (!js_space(c)) {
-        any = true;
+        commas += depth == 1;
       }
     }
     throw DecodeError("truncated JSON array");
+  }
+  // Fast paths for the canonical step encoding (serde's field order, no
+  // white space: what write_block_summaries_jsonl and the reference write).
+  // Each reads one exact form or consumes nothing and returns false, and the
+  // general parser then reads the same bytes (any other spacing, field
+  // order, value range or a malformed value).
+  // {"write":null|N,"mv":M} (a tape op, after more() of the tapes array)
+  bool fast_tape_op(int64_t& mv, bool& has, uint64_t& sym) {
+    const char* p = p_;
+    if (e_ - p < 16 || memcmp(p, "{\"write\":", 9)) return false;
+    p += 9;
+    if (*p == 'n') {
+      if (memcmp(p, "null", 4)) return false;
+      p += 4;
+      has = false;
+      sym = 0;
+    } else {
+      uint64_t v = 0;
+      int nd = 0;
+      while (p < e_ && js_digit(*p) && nd < 6) { v = v * 10 + (uint64_t)(*p++ - '0'); nd++; }
+      if (nd == 0 || nd == 6 || v > 0xffff) return false;
+      has = true;
+      sym = v;
+    }
+    if (e_ - p < 8 || memcmp(p, ",\"mv\":", 6)) return false;
+    p += 6;
+    const bool neg = *p == '-';
+    p += neg;
+    int64_t v = 0;
+    int nd = 0;
+    while (p < e_ && js_digit(*p) && nd < 4) { v = v * 10 + (*p++ - '0'); nd++; }
+    if (nd == 0 || nd == 4 || p >= e_ || *p != '}') return false;
+    v = neg ? -v : v;
+    if (v < -128 || v > 127) return false;
+    mv = v;
+    p_ = p + 1;
+    first_ = false;
+    return true;
+  }
+  // {"input_mv":M,"tapes":[ (a step object up to its first tape op; the
+  // tapes array is open as after begin_array)
+  bool fast_step_head(int64_t& imv) {
+    ws();
+    const char* p = p_;
+    if (e_ - p < 24 || memcmp(p, "{\"input_mv\":", 12)) return false;
+    p += 12;
+    const bool neg = *p == '-';
+    p += neg;
+    int64_t v = 0;
+    int nd = 0;
+    while (p < e_ && js_digit(*p) && nd < 4) { v = v * 10 + (*p++ - '0'); nd++; }
+    if (nd == 0 || nd == 4 || e_ - p < 10 || memcmp(p, ",\"tapes\":[", 10)) return false;
+    v = neg ? -v : v;
+    if (v < -128 || v > 127) return false;
+    imv = v;
+    p_ = p + 10;
+    first_ = true;
+    return true;
   }
   void skip() {
     ws();
@@ -270,10 +401,18 @@ class Json {
 
 template <class P>
 void decode_tape_op(P& d, BlockStore& s) {
-  int64_t r = d.begin_map();
   bool has = false;
   uint64_t sym = 0;
   int64_t mv = 0;
+  if constexpr (std::is_same_v<P, Json>) {
+    if (d.fast_tape_op(mv, has, sym)) {
+      s.mv.push_back((int8_t)mv);
+      s.has_write.push_back(has ? 1 : 0);
+      s.wsym.push_back(has ? (uint16_t)sym : 0);
+      return;
+    }
+  }
+  int64_t r = d.begin_map();
   while (d.more(r)) {
     const Key k = d.key();
     if (k == "write") {
@@ -350,9 +489,17 @@ void decode_block(P& d, BlockStore& s, BlockShape& sh) {
         }
         int64_t a = d.begin_array();
         while (d.more(a)) {
-          int64_t sm = d.begin_map();
           int64_t imv = 0;
           uint32_t ntape = 0;
+          int64_t sm = -1;
+          bool fast = false;
+          if constexpr (std::is_same_v<P, Json>) fast = d.fast_step_head(imv);
+          if (fast) {
+            int64_t ta = -1;
+            while (d.more(ta)) { decode_tape_op(d, s); ntape++; }
+          } else {
+            sm = d.begin_map();
+          }
           while (d.more(sm)) {
             const Key sk = d.key();
             if (sk == "input_mv") {
@@ -594,7 +741,7 @@ bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::str
 // once). Every block's fields and step count, not its steps; line_off gets
 // each line's byte offset. Step arrays stay empty.
 bool decode_blocks_jsonl_meta(const char* data, size_t len, size_t lo, size_t hi, BlockStore& out,
-                              std::vector<uint64_t>& line_off, std::string& err) {
+                              std::vector<uint64_t>& line_off, std::string& err, bool steps) {
   auto cut = [&](size_t x) -> size_t {
     if (x == 0) return 0;
     if (x >= len) return len;
@@ -605,21 +752,71 @@ bool decode_blocks_jsonl_meta(const char* data, size_t len, size_t lo, size_t hi
   out = BlockStore{};
   out.step_start.assign(1, 0);
   line_off.clear();
-  BlockShape sh;
-  size_t p = b, line = 0;
+  // one range per host thread, cut at line ends (as decode_blocks_jsonl)
+  const unsigned T = decode_threads(e - b);
+  std::vector<size_t> rc(T + 1, e);
+  rc[0] = b;
+  for (unsigned t = 1; t < T; t++) {
+    const size_t x = std::max(rc[t - 1], b + (e - b) / T * t);
+    const char* nl = x < e ? static_cast<const char*>(memchr(data + x, '\n', e - x)) : nullptr;
+    rc[t] = nl ? (size_t)(nl - data) + 1 : e;
+  }
+  std::vector<BlockStore> parts(T);
+  std::vector<BlockShape> shapes(T);
+  std::vector<std::vector<uint64_t>> offs(T);
+  std::vector<size_t> lines(T, 0);
+  std::vector<std::string> msg(T);
+  auto run = [&](unsigned t) {
+    BlockStore& s = parts[t];
+    s.step_start.assign(1, 0);
+    size_t p = rc[t];
+    const size_t pe = rc[t + 1];
+    try {
+      while (p < pe) {
+        const char* nl = static_cast<const char*>(memchr(data + p, '\n', pe - p));
+        const size_t end = nl ? (size_t)(nl - data) : pe;
+        lines[t]++;
+        size_t le = end;
+        if (le > p && data[le - 1] == '\r') le--;
+        offs[t].push_back(p);
+        if (le == p) throw DecodeError("empty line");
+        Json d(data + p, le - p);
+        if (steps) decode_block<Json, false>(d, s, shapes[t]);
+        else decode_block<Json, true>(d, s, shapes[t]);
+        if (!d.done()) throw DecodeError("trailing bytes after the block object");
+        p = nl ? end + 1 : pe;
+      }
+    } catch (const std::exception& ex) {
+      msg[t] = ex.what();
+      if (msg[t].empty()) msg[t] = "decode error";
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < T; t++) {
+    try {
+      th.emplace_back(run, t);
+    } catch (const std::system_error&) {
+      run(t);
+    }
+  }
+  run(0);
+  for (auto& x : th) x.join();
+  size_t before = 0;
+  for (unsigned t = 0; t < T; t++) {
+    if (!msg[t].empty()) {
+      err = "parse jsonl line at byte " + std::to_string(offs[t].empty() ? rc[t] : offs[t].back()) + " (line " +
+            std::to_string(before + lines[t]) + " of the range): " + msg[t];
+      return false;
+    }
+    before += lines[t];
+  }
   try {
-    while (p < e) {
-      const char* nl = static_cast<const char*>(memchr(data + p, '\n', e - p));
-      const size_t end = nl ? (size_t)(nl - data) : e;
-      line++;
-      size_t le = end;
-      if (le > p && data[le - 1] == '\r') le--;
-      if (le == p) throw DecodeError("empty line");
-      line_off.push_back(p);
-      Json d(data + p, le - p);
-      decode_block<Json, true>(d, out, sh);
-      if (!d.done()) throw DecodeError("trailing bytes after the block object");
-      p = nl ? end + 1 : e;
+    BlockShape sh;
+    merge_stores(parts, shapes, out, sh);
+    for (auto& o : offs) line_off.insert(line_off.end(), o.begin(), o.end());
+    if (steps) {
+      finish_blocks(out, sh);
+      return true;
     }
     out.tau = sh.nwin.empty() ? 0 : sh.nwin[0];
     for (size_t k = 0; k < sh.nwin.size(); k++)
@@ -628,8 +825,7 @@ bool decode_blocks_jsonl_meta(const char* data, size_t len, size_t lo, size_t hi
     out.bind();
     return true;
   } catch (const std::exception& ex) {
-    err = "parse jsonl line at byte " + std::to_string(line_off.empty() ? b : line_off.back()) + " (line " +
-          std::to_string(line) + " of the range): " + ex.what();
+    err = std::string("deserialize JSONL block metadata: ") + ex.what();
     return false;
   }
 }

@@ -28,10 +28,11 @@ struct BlockStore {
 bool decode_blocks_cbor(const uint8_t* data, size_t len, BlockStore& out, std::string& err);
 bool decode_blocks_json(const char* data, size_t len, BlockStore& out, std::string& err);
 bool decode_blocks_jsonl(const char* data, size_t len, BlockStore& out, std::string& err);
-// sliced ingest: block fields + step counts of the lines starting in the byte
-// range [lo, hi) (cut at line ends), no steps; line_off = each line's offset
+// sliced ingest: the lines starting in the byte range [lo, hi) (cut at line
+// ends): block fields + step counts (steps = false: the step arrays stay
+// empty) or the full blocks; line_off = each line's byte offset
 bool decode_blocks_jsonl_meta(const char* data, size_t len, size_t lo, size_t hi, BlockStore& out,
-                              std::vector<uint64_t>& line_off, std::string& err);
+                              std::vector<uint64_t>& line_off, std::string& err, bool steps = false);
 std::string encode_blocks_jsonl(const sezkp_block_view& v);
 std::vector<uint8_t> encode_blocks_cbor(const sezkp_block_view& v);
 // partition_trace (partition.rs:43-150) of a step-major movement log into blocks of b steps

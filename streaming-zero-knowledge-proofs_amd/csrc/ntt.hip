@@ -756,9 +756,186 @@ __global__ void __launch_bounds__(512, 2) k_ntt_dif9(NttPassArgs P) {
   }
 }
 
+// ---- 512-thread radix-8 DIF passes (8 points per lane, two waves per SIMD)
+// The two passes of a 2^20-point DIF ([8, 12] stages) and the 12-stage
+// narrow pass of other DIFs launch 256 workgroups of 4096 points: one
+// workgroup per CU. With 256 lanes (16 points each, k_ntt4) that is one wave
+// per SIMD and ~45% of its cycles wait on memory (round 3 PMC); with 512 lanes
+// each SIMD holds two waves. Radix-8 steps: a lane loads 8 points L apart,
+// runs an 8-point DIF (w_8 powers: shifts), multiplies slot q by
+// w_{8L}^(low * rev3(q)) and stores them back (the four-step identity of
+// k_ntt4's DIF, three stages per LDS exchange).
+constexpr int R8_NT = 512;
+__device__ __forceinline__ int r8_pad(int e) { return e + (e >> 3); }  // conflict-free strides 64 / 8 / 1
+// w_64 = 2^39, w_64^-1 = 2^153 (2 has order 192)
+template <bool INV>
+__device__ __forceinline__ constexpr int tw_exp64(int j) { return ((INV ? 153 : 39) * j) % 192; }
+// slot rev3(k) *= w1^k, k = 1..7 (w1 = w_{8L}^low)
+__device__ __forceinline__ void r8_twiddle(uint64_t (&x)[8], uint64_t w1) {
+  uint64_t t = w1;
+#pragma unroll
+  for (int k = 1; k < 8; k++) {
+    x[rev<3>(k)] = gl_mul(x[rev<3>(k)], t);
+    if (k < 7) t = gl_mul(t, w1);
+  }
+}
+
+// Wide DIF pass of 8 stages (tile = 16 columns x 256 rows, rows 2^sL apart),
+// 256 = 8 x 8 x 4: lane (c, g), g < 32. Same pass twiddle and out-of-place
+// store as k_ntt4's wide DIF pass.
+template <bool INV>
+__global__ void __launch_bounds__(R8_NT, 2) k_ntt_w8r8(NttPassArgs P) {
+  __shared__ uint64_t sh[256 * NTT_PADC];
+  const int tid = threadIdx.x, c = tid & (NTT_CMAX - 1), g = tid >> 4;
+  const NttTables& T = P.tw;
+  Tile G;
+  G.sL = P.sL;
+  G.m = 8;
+  G.tile = blockIdx.x;
+  G.wide = true;
+  const uint64_t tiles_per_blk = (1ULL << G.sL) / NTT_CMAX;
+  G.blk_base = (G.tile / tiles_per_blk) * (256ULL << G.sL);
+  G.low0 = (G.tile % tiles_per_blk) * NTT_CMAX;
+  uint64_t low;
+  uint64_t x[8];
+  // stages 7..5 (stride 32), straight from HBM
+#pragma unroll
+  for (int d = 0; d < 8; d++) x[d] = P.a[tile_pos(G, g + 32 * d, c, low)];
+  fft_dif_regs<3, INV>(x);
+  if (g) r8_twiddle(x, tw_pow(T, (uint64_t)g << (T.K - 8), INV));  // w_256^(g k)
+#pragma unroll
+  for (int q = 0; q < 8; q++) sh[(g + 32 * q) * NTT_PADC + c] = x[q];
+  __syncthreads();
+  {  // stages 4..2 (stride 4), twiddles w_32^(lo k): shifts
+    const int lo = g & 3, base = (g >> 2) * 32 + lo;
+#pragma unroll
+    for (int d = 0; d < 8; d++) x[d] = sh[(base + 4 * d) * NTT_PADC + c];
+    fft_dif_regs<3, INV>(x);
+    if (lo) {
+#pragma unroll
+      for (int k = 1; k < 8; k++) x[rev<3>(k)] = tw_small<INV>(x[rev<3>(k)], lo * k, 16);
+    }
+#pragma unroll
+    for (int d = 0; d < 8; d++) sh[(base + 4 * d) * NTT_PADC + c] = x[d];
+  }
+  __syncthreads();
+  // stages 1..0: 4-point groups t = 4h + d (h = g, g + 32), then the pass
+  // twiddle w_{2^(8+sL)}^(low rev8(t)), rev8(4h + rev2(k)) = 64 k + rev6(h)
+  const int tw_shift = T.K - 8 - G.sL;
+  uint64_t* dst = P.out ? P.out : P.a;
+#pragma unroll
+  for (int hh = 0; hh < 2; hh++) {
+    const int h = g + 32 * hh;
+    uint64_t y[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) y[d] = sh[(4 * h + d) * NTT_PADC + c];
+    fft_dif_regs<2, INV>(y);
+    (void)tile_pos(G, 0, c, low);
+    if (low) {
+      uint64_t a = tw_pow(T, (low * (uint64_t)(__brev((uint32_t)h) >> 26)) << tw_shift, INV);
+      const uint64_t b = tw_pow(T, (low * 64ULL) << tw_shift, INV);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        y[rev<2>(k)] = gl_mul(y[rev<2>(k)], a);
+        if (k < 3) a = gl_mul(a, b);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 4; d++) dst[tile_pos(G, 4 * h + d, c, low)] = y[d];
+  }
+}
+
+// Narrow DIF pass of 12 stages on 4096 contiguous points (sL = 0),
+// 4096 = 8^4: lane g < 512. nat_out: position p = 4096 tile + e goes to
+// out[bitrev(p)] * out_scale (workgroup order as k_ntt4's nat_out); else the
+// tile is stored in place (or to out) in bit-reversed order through the LDS.
+template <bool INV>
+__global__ void __launch_bounds__(R8_NT, 2) k_ntt_n12r8(NttPassArgs P) {
+  __shared__ uint64_t sh[4096 + 512];
+  const int g = threadIdx.x;
+  const NttTables& T = P.tw;
+  const uint64_t tile = P.nat_out ? nat_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t p0 = tile << 12;
+  uint64_t x[8];
+  // stages 11..9 (stride 512), straight from HBM
+#pragma unroll
+  for (int d = 0; d < 8; d++) x[d] = P.a[p0 + g + 512 * d];
+  fft_dif_regs<3, INV>(x);
+  if (g) r8_twiddle(x, tw_pow(T, (uint64_t)g << (T.K - 12), INV));  // w_4096^(g k)
+#pragma unroll
+  for (int q = 0; q < 8; q++) sh[r8_pad(g + 512 * q)] = x[q];
+  __syncthreads();
+  {  // stages 8..6 (stride 64)
+    const int lo = g & 63, base = (g >> 6) * 512 + lo;
+#pragma unroll
+    for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(base + 64 * d)];
+    fft_dif_regs<3, INV>(x);
+    if (lo) r8_twiddle(x, tw_pow(T, (uint64_t)lo << (T.K - 9), INV));  // w_512^(lo k)
+#pragma unroll
+    for (int d = 0; d < 8; d++) sh[r8_pad(base + 64 * d)] = x[d];
+  }
+  __syncthreads();
+  {  // stages 5..3 (stride 8), twiddles w_64^(lo k): shifts
+    const int lo = g & 7, base = (g >> 3) * 64 + lo;
+#pragma unroll
+    for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(base + 8 * d)];
+    fft_dif_regs<3, INV>(x);
+    if (lo) {
+#pragma unroll
+      for (int k = 1; k < 8; k++) x[rev<3>(k)] = gl_mul_pow2(x[rev<3>(k)], tw_exp64<INV>(lo * k));
+    }
+#pragma unroll
+    for (int d = 0; d < 8; d++) sh[r8_pad(base + 8 * d)] = x[d];
+  }
+  __syncthreads();
+  // stages 2..0 on 8 consecutive points
+#pragma unroll
+  for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(8 * g + d)];
+  fft_dif_regs<3, INV>(x);
+  if (P.nat_out) {
+    const int sh_r = 32 - P.nat_logN;
+    const bool scale = P.out_scale > 1;
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+      P.out[__brev((uint32_t)(p0 + 8 * g + q)) >> sh_r] = scale ? gl_mul(x[q], P.out_scale) : x[q];
+    return;
+  }
+  __syncthreads();  // every lane has read its points
+#pragma unroll
+  for (int q = 0; q < 8; q++) sh[r8_pad(8 * g + q)] = x[q];
+  __syncthreads();
+  uint64_t* dst = (P.out ? P.out : P.a) + p0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) dst[j * R8_NT + g] = sh[r8_pad(j * R8_NT + g)];
+}
+
+// the radix-8 forms of a DIF pass when its shape has one (wide m = 8 with 16
+// columns, narrow m = 12), else false. SEZKP_NTT_R8=0: the k_ntt4 forms (A/B)
+static bool launch_r8(hipStream_t st, const NttPassArgs& P, bool inverse, unsigned tiles) {
+  static const bool off = [] {
+    const char* e = getenv("SEZKP_NTT_R8");
+    return e && atoi(e) == 0;
+  }();
+  if (off || P.src || P.dp_rlo || P.nat_tr) return false;
+  if (P.m == 8 && P.logC == 4 && P.sL >= 4 && !P.nat_out) {
+    if (inverse) hipLaunchKernelGGL(k_ntt_w8r8<true>, dim3(tiles), dim3(R8_NT), 0, st, P);
+    else hipLaunchKernelGGL(k_ntt_w8r8<false>, dim3(tiles), dim3(R8_NT), 0, st, P);
+    return true;
+  }
+  if (P.m == 12 && P.sL == 0) {
+    if (inverse) hipLaunchKernelGGL(k_ntt_n12r8<true>, dim3(tiles), dim3(R8_NT), 0, st, P);
+    else hipLaunchKernelGGL(k_ntt_n12r8<false>, dim3(tiles), dim3(R8_NT), 0, st, P);
+    return true;
+  }
+  return false;
+}
+
 // launch one pass with the register kernel when its shape allows, else false
 template <bool DIF, bool INV>
 static bool launch_ntt4(hipStream_t st, const NttPassArgs& P, unsigned tiles) {
+  if constexpr (DIF) {
+    if (launch_r8(st, P, INV, tiles)) return true;
+  }
   if (P.logC != 4) return false;
   const int skip = P.src ? P.skip : 0;
   if (DIF && skip) return false;

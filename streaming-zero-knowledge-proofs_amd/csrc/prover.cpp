@@ -2402,10 +2402,14 @@ struct sezkp_blocks {
 };
 int32_t sezkp_blocks_decode_jsonl_meta(const uint8_t* data, size_t len, uint64_t lo, uint64_t hi, sezkp_blocks** out,
                                        char* err, size_t err_len) {
+  return sezkp_blocks_decode_jsonl_lines(data, len, lo, hi, 0, out, err, err_len);
+}
+int32_t sezkp_blocks_decode_jsonl_lines(const uint8_t* data, size_t len, uint64_t lo, uint64_t hi, int32_t steps,
+                                        sezkp_blocks** out, char* err, size_t err_len) {
   if (!out || (!data && len) || lo > hi) return SEZKP_E_INVALID;
   std::unique_ptr<sezkp_blocks> b(new sezkp_blocks());
   std::string e;
-  if (!decode_blocks_jsonl_meta(reinterpret_cast<const char*>(data), len, lo, hi, b->s, b->line_off, e)) {
+  if (!decode_blocks_jsonl_meta(reinterpret_cast<const char*>(data), len, lo, hi, b->s, b->line_off, e, steps != 0)) {
     set_err(err, err_len, e);
     return SEZKP_E_DECODE;
   }

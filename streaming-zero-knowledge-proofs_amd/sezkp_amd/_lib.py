@@ -34,7 +34,7 @@ EXPORTS = [
     "sezkp_merkle_build", "sezkp_merkle_paths", "sezkp_manifest_frontier_root", "sezkp_ctx_comm_stats",
     "sezkp_fs_xof", "sezkp_ctx_upload_rows", "sezkp_shard_rows", "sezkp_blocks_decode_jsonl_meta",
     "sezkp_blocks_line_offsets", "sezkp_manifest_leaf_hashes", "sezkp_merkle_root_of_leaves",
-    "sezkp_ctx_create_sharded_solo",
+    "sezkp_ctx_create_sharded_solo", "sezkp_blocks_decode_jsonl_lines",
 ]
 
 
@@ -156,6 +156,8 @@ def _load():
                                    C.POINTER(C.c_uint64)]
     L.sezkp_blocks_decode_jsonl_meta.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint64,
                                                  C.POINTER(C.c_void_p)] + E
+    L.sezkp_blocks_decode_jsonl_lines.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint64, C.c_int32,
+                                                  C.POINTER(C.c_void_p)] + E
     L.sezkp_blocks_line_offsets.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.c_size_t)]
     L.sezkp_manifest_leaf_hashes.argtypes = [C.POINTER(BlockView), C.c_void_p]
     L.sezkp_merkle_root_of_leaves.argtypes = [C.c_char_p, C.c_size_t, C.c_int32, C.c_char_p]

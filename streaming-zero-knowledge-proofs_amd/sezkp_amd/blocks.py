@@ -153,22 +153,30 @@ class BlockSoA:
         return out.raw[:32 * self.n_blocks]
 
     @classmethod
-    def from_jsonl_meta(cls, data, lo: int, hi: int) -> tuple:
+    def from_jsonl_meta(cls, data, lo: int, hi: int, steps: bool = False) -> tuple:
         """The metadata of the JSONL lines starting in bytes [lo, hi) of `data`
         (bytes or a uint8 numpy array / memmap; cut at line ends): every field
-        and step count, no steps (empty step arrays). Returns (BlockSoA, line
-        byte offsets) (sezkp_blocks_decode_jsonl_meta)."""
+        and step count, no steps (empty step arrays); steps=True: the same
+        lines decoded in full. Returns (BlockSoA, line byte offsets)
+        (sezkp_blocks_decode_jsonl_lines)."""
         ptr, n = _addr(data)
         h = C.c_void_p()
         err = C.create_string_buffer(512)
-        rc = lib.sezkp_blocks_decode_jsonl_meta(ptr, n, lo, hi, C.byref(h), err, 512)
+        rc = lib.sezkp_blocks_decode_jsonl_lines(ptr, n, lo, hi, int(steps), C.byref(h), err, 512)
         if rc != 0:
             raise SezkpError(rc, err.value.decode())
         p = C.POINTER(C.c_uint64)()
         cnt = C.c_size_t()
         lib.sezkp_blocks_line_offsets(h, C.byref(p), C.byref(cnt))
         offs = np.ctypeslib.as_array(p, shape=(cnt.value,)).copy() if cnt.value else np.zeros(0, np.uint64)
-        return cls._take(h, meta=True), offs
+        return cls._take(h, meta=not steps), offs
+
+    def meta_only(self) -> "BlockSoA":
+        """These blocks' fields and step counts without the step arrays."""
+        arr = {f: getattr(self, f) for f, _ in VIEW_FIELDS}
+        for f in ("input_mv", "mv", "has_write", "wsym"):
+            arr[f] = arr[f][:0]
+        return BlockSoA(self.tau, **arr)
 
     @classmethod
     def from_jsonl_range(cls, data, lo: int, hi: int) -> "BlockSoA":

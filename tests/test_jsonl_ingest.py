@@ -98,19 +98,21 @@ def _sliced_worker(rank, world, port, path, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sliced_ingest_matches_full_decode(product, tmp_path, world):
+@pytest.mark.parametrize("world,log_t", [(2, 14), (4, 14), (8, 15)])
+def test_sliced_ingest_matches_full_decode(product, tmp_path, world, log_t):
     """Each rank reads 1/P of the JSONL lines' metadata, the metadata and the
     leaf hashes are allgathered (gloo), rank 0 reduces the Frontier root, and
     each rank decodes only the lines over its rows: ragged blocks (333 steps)
-    cross every rank boundary. Every rank's step slice equals the full
-    decode's rows [row0, row0 + nrows), and the root is the file's Frontier root."""
+    cross every rank boundary, and a rank's rows reach into its neighbours'
+    byte ranges (those lines are decoded again). Every rank's
+    step slice equals the full decode's rows [row0, row0 + nrows), and the
+    root is the file's Frontier root."""
     import hashlib
     import socket
     import torch.multiprocessing as mp
     import numpy as np
     from sezkp_amd.blocks import shard_rows
-    blocks = product.synthetic_blocks(1 << 14, 333, 3, 11)
+    blocks = product.synthetic_blocks(1 << log_t, 333, 3, 11)
     path = tmp_path / "b.jsonl"
     path.write_bytes(blocks.to_jsonl())
     full = product.BlockSoA.from_file(str(path))
@@ -162,3 +164,69 @@ def test_jsonl_meta_ranges_cover_every_line_once(product):
         a, b = 3, 9
         sl = BlockSoA.from_jsonl_range(jl, int(offs[a]), int(offs[b]))
         assert np.array_equal(sl.block_id, full.block_id[a:b])
+
+
+def test_jsonl_noncanonical_forms_decode_alike(product):
+    """The decoder's fast paths read only the canonical step encoding
+    (serde's field order, no white space); spaced, reordered and extended
+    forms take the general parser and give the same blocks, in the full and
+    the metadata decode; out-of-range values are errors on both paths."""
+    import json as js
+    from sezkp_amd.blocks import BlockSoA
+    b = product.synthetic_blocks(2000, 61, 3, 9)
+    canon = b.to_jsonl()
+    objs = [js.loads(x) for x in canon.split(b"\n") if x]
+
+    def dump(os_, **kw):
+        return b"".join(js.dumps(o, **kw).encode() + b"\n" for o in os_)
+
+    def remap(fn):
+        out = []
+        for o in objs:
+            o = js.loads(js.dumps(o))
+            o["movement_log"]["steps"] = [fn(s) for s in o["movement_log"]["steps"]]
+            out.append(o)
+        return out
+
+    variants = [
+        dump(objs),  # ", " and ": " separators
+        dump(remap(lambda s: {"input_mv": s["input_mv"],
+                              "tapes": [{"mv": t["mv"], "write": t["write"]} for t in s["tapes"]]}),
+             separators=(",", ":")),
+        dump(remap(lambda s: {"tapes": s["tapes"], "input_mv": s["input_mv"]}), separators=(",", ":")),
+        dump(remap(lambda s: {"input_mv": s["input_mv"], "tapes": [dict(t, x=[1, {"y": "]"}]) for t in s["tapes"]],
+                              "z": "}"}), separators=(",", ":")),
+    ]
+    for v in variants:
+        assert v != canon
+        r = BlockSoA.from_jsonl(v)
+        for f in _fields(product):
+            np.testing.assert_array_equal(getattr(r, f), getattr(b, f))
+        m, _ = BlockSoA.from_jsonl_meta(v, 0, len(v))
+        assert np.array_equal(m.step_start, b.step_start)
+    bad_mv = canon.replace(b'"mv":-1}', b'"mv":200}', 1)
+    bad_w = canon.replace(b'{"write":', b'{"write":70000', 1)
+    with pytest.raises(product.SezkpError, match="mv out of i8 range"):
+        BlockSoA.from_jsonl(bad_mv)
+    with pytest.raises(product.SezkpError):
+        BlockSoA.from_jsonl(bad_w)
+
+
+def test_jsonl_meta_threads_match_one_thread(product, monkeypatch):
+    """The metadata pass cuts its byte range at line ends into one range per
+    host thread: the same blocks and offsets as one thread, and an error
+    names its line."""
+    from sezkp_amd.blocks import BlockSoA
+    b = product.synthetic_blocks(1 << 18, 100, 4, 7)
+    data = b.to_jsonl()
+    outs = []
+    for threads in ("1", "5"):
+        monkeypatch.setenv("SEZKP_HOST_THREADS", threads)
+        outs.append(BlockSoA.from_jsonl_meta(data, len(data) // 7, len(data)))
+    (m1, o1), (m5, o5) = outs
+    assert np.array_equal(o1, o5) and np.array_equal(m1.step_start, m5.step_start)
+    assert np.array_equal(m1.block_id, m5.block_id) and m1.tau == m5.tau == b.tau
+    lines = data.split(b"\n")
+    lines[len(lines) * 3 // 4] = b""
+    with pytest.raises(product.SezkpError, match="empty line"):
+        BlockSoA.from_jsonl_meta(b"\n".join(lines), 0, len(data))
