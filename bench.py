@@ -1068,10 +1068,13 @@ def measure_sharded_predicted(args, torch, single_ms: float) -> dict:
             ctx.prove_view(mroot)  # warmup
             torch.cuda.synchronize()
             wall, coll_ms, model_ms, wire = [], 0.0, 0.0, 0
+            st_sum = {}
             for _ in range(reps):
                 t0 = time.perf_counter()
                 ctx.prove_view(mroot)
                 wall.append((time.perf_counter() - t0) * 1e3)
+                for k, v in ctx.stage_times_ms().items():
+                    st_sum[k] = st_sum.get(k, 0.0) + v / reps
             stats = ctx.comm_stats()
             for c in stats:
                 coll_ms += c["ms"]
@@ -1081,7 +1084,10 @@ def measure_sharded_predicted(args, torch, single_ms: float) -> dict:
             w = statistics.median(wall)
             ranks.append({"rank": r, "solo_wall_ms": w, "solo_collective_ms": coll_ms, "collectives": len(stats),
                           "wire_bytes": wire, "model_collective_ms": model_ms,
-                          "predicted_ms": w - coll_ms + model_ms})
+                          "predicted_ms": w - coll_ms + model_ms,
+                          "stages_ms": {k: round(v, 4) for k, v in st_sum.items() if v > 0},
+                          "collectives_detail": [{"name": c["name"], "bytes": c["bytes"], "ms": round(c["ms"], 4)}
+                                                 for c in stats] if r == 0 else None})
         pm = max(x["predicted_ms"] for x in ranks)
         res["by_gpus"][str(P)] = {"predicted_ms_per_proof": pm, "predicted_value": N / (pm * 1e-3),
                                   "predicted_speedup": single_ms / pm if pm > 0 else None,

@@ -846,15 +846,15 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_w8r8(NttPassArgs P) {
 }
 
 // Narrow DIF pass of 12 stages on 4096 contiguous points (sL = 0),
-// 4096 = 8^4: lane g < 512. nat_out: position p = 4096 tile + e goes to
-// out[bitrev(p)] * out_scale (workgroup order as k_ntt4's nat_out); else the
-// tile is stored in place (or to out) in bit-reversed order through the LDS.
+// 4096 = 8^4: lane g < 512; the natural-order store (nat_out): position
+// p = 4096 tile + e goes to out[bitrev(p)] * out_scale (workgroup order as
+// k_ntt4's nat_out).
 template <bool INV>
 __global__ void __launch_bounds__(R8_NT, 2) k_ntt_n12r8(NttPassArgs P) {
   __shared__ uint64_t sh[4096 + 512];
   const int g = threadIdx.x;
   const NttTables& T = P.tw;
-  const uint64_t tile = P.nat_out ? nat_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t tile = nat_tile(blockIdx.x, gridDim.x);
   const uint64_t p0 = tile << 12;
   uint64_t x[8];
   // stages 11..9 (stride 512), straight from HBM
@@ -892,37 +892,26 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_n12r8(NttPassArgs P) {
 #pragma unroll
   for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(8 * g + d)];
   fft_dif_regs<3, INV>(x);
-  if (P.nat_out) {
-    const int sh_r = 32 - P.nat_logN;
-    const bool scale = P.out_scale > 1;
+  const int sh_r = 32 - P.nat_logN;
+  const bool scale = P.out_scale > 1;
 #pragma unroll
-    for (int q = 0; q < 8; q++)
-      P.out[__brev((uint32_t)(p0 + 8 * g + q)) >> sh_r] = scale ? gl_mul(x[q], P.out_scale) : x[q];
-    return;
-  }
-  __syncthreads();  // every lane has read its points
-#pragma unroll
-  for (int q = 0; q < 8; q++) sh[r8_pad(8 * g + q)] = x[q];
-  __syncthreads();
-  uint64_t* dst = (P.out ? P.out : P.a) + p0;
-#pragma unroll
-  for (int j = 0; j < 8; j++) dst[j * R8_NT + g] = sh[r8_pad(j * R8_NT + g)];
+  for (int q = 0; q < 8; q++)
+    P.out[__brev((uint32_t)(p0 + 8 * g + q)) >> sh_r] = scale ? gl_mul(x[q], P.out_scale) : x[q];
 }
 
-// the radix-8 forms of a DIF pass when its shape has one (wide m = 8 with 16
-// columns, narrow m = 12), else false. SEZKP_NTT_R8=0: the k_ntt4 forms (A/B)
+// the radix-8 forms of the natural-order 2^20 DIF's passes (wide m = 8 with
+// 16 columns, narrow m = 12 with the natural-order store), else false.
+// Measured (round 4, profiles/r04/c2_ab.txt): 2^20 fwd + inv 72.7 -> 70.4 us;
+// the prover's in-place 12-stage INTT pass measured 2 us slower with it, so
+// it keeps k_ntt4's X16 form.
 static bool launch_r8(hipStream_t st, const NttPassArgs& P, bool inverse, unsigned tiles) {
-  static const bool off = [] {
-    const char* e = getenv("SEZKP_NTT_R8");
-    return e && atoi(e) == 0;
-  }();
-  if (off || P.src || P.dp_rlo || P.nat_tr) return false;
+  if (P.src || P.dp_rlo || P.nat_tr) return false;
   if (P.m == 8 && P.logC == 4 && P.sL >= 4 && !P.nat_out) {
     if (inverse) hipLaunchKernelGGL(k_ntt_w8r8<true>, dim3(tiles), dim3(R8_NT), 0, st, P);
     else hipLaunchKernelGGL(k_ntt_w8r8<false>, dim3(tiles), dim3(R8_NT), 0, st, P);
     return true;
   }
-  if (P.m == 12 && P.sL == 0) {
+  if (P.m == 12 && P.sL == 0 && P.nat_out) {
     if (inverse) hipLaunchKernelGGL(k_ntt_n12r8<true>, dim3(tiles), dim3(R8_NT), 0, st, P);
     else hipLaunchKernelGGL(k_ntt_n12r8<false>, dim3(tiles), dim3(R8_NT), 0, st, P);
     return true;
@@ -933,9 +922,6 @@ static bool launch_r8(hipStream_t st, const NttPassArgs& P, bool inverse, unsign
 // launch one pass with the register kernel when its shape allows, else false
 template <bool DIF, bool INV>
 static bool launch_ntt4(hipStream_t st, const NttPassArgs& P, unsigned tiles) {
-  if constexpr (DIF) {
-    if (launch_r8(st, P, INV, tiles)) return true;
-  }
   if (P.logC != 4) return false;
   const int skip = P.src ? P.skip : 0;
   if (DIF && skip) return false;
@@ -1563,8 +1549,9 @@ bool ntt_dif_natural(hipStream_t st, uint64_t* a, uint64_t* scratch, int logN, b
       P.out = a; P.nat_out = 1; P.nat_logN = logN; P.out_scale = scale;
       if (P.m > NTT_MMAX) tiles = (1ULL << logN) >> P.m;
     }
-    const bool ok = inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
-                            : launch_ntt4<true, false>(st, P, (unsigned)tiles);
+    const bool ok = (logN == 20 && launch_r8(st, P, inverse, (unsigned)tiles)) ||
+                    (inverse ? launch_ntt4<true, true>(st, P, (unsigned)tiles)
+                             : launch_ntt4<true, false>(st, P, (unsigned)tiles));
     if (!ok) { *err = hipErrorInvalidValue; return true; }
   }
   *err = hipGetLastError();

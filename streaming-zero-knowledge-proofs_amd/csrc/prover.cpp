@@ -1113,14 +1113,18 @@ FsArgs sezkp_ctx::fs_args(int point, const uint8_t mroot[32]) {
   return a;
 }
 
-// The device transcript is the default. The host's is used for traces below
-// 16 rows (the per-point DEEP), for streams too long for the kernel's LDS,
-// with SEZKP_NO_DEEP_POLY=1 (the per-point DEEP needs z on the host) and with
-// SEZKP_HOST_TRANSCRIPT=1 (A/B, parity tests; read per proof, the tests
-// switch it).
+// The host transcript is the default: the device one (SEZKP_DEVICE_TRANSCRIPT=1,
+// csrc/transcript.hip) measured slower in both views (round 4,
+// profiles/r04/transcript_ab.txt: its three one-workgroup kernels take
+// 40 / 23 / 54 us of serial BLAKE3 chains per proof against ~35 us per host
+// round trip, and its single workgroups wait for a free CU behind the other
+// proofs' trees: in flight 7.51 against 7.98 10^9 elements/s). The device
+// transcript is never used for traces below 16 rows (the per-point DEEP), for
+// streams too long for the kernel's LDS or with SEZKP_NO_DEEP_POLY=1 (the
+// per-point DEEP needs z on the host). Read per proof (the tests switch it).
 bool sezkp_ctx::host_transcript() const {
-  const char* e = getenv("SEZKP_HOST_TRANSCRIPT");
-  return (e && atoi(e) != 0) || !fs_ok || logn < 4 || getenv("SEZKP_NO_DEEP_POLY") != nullptr;
+  const char* e = getenv("SEZKP_DEVICE_TRANSCRIPT");
+  return !(e && atoi(e) != 0) || !fs_ok || logn < 4 || getenv("SEZKP_NO_DEEP_POLY") != nullptr;
 }
 
 size_t sezkp_ctx::prove(const uint8_t mroot[32]) {

@@ -5,8 +5,8 @@ suffix, the core of Blake3Transcript::challenge_bytes,
 crates/sezkp-crypto/src/lib.rs:102-123) against the C oracle's BLAKE3 and the
 reference's committed v0 proofs; the reference's transcript input vector
 (specs/stark-v1/transcript_inputs.json, crates/sezkp-stark/tests/param_vectors.rs);
-and full proofs with the device transcript (default), the host transcript
-(SEZKP_HOST_TRANSCRIPT=1) and the device path's host re-run hook, all equal
+and full proofs with the host transcript (default), the device transcript
+(SEZKP_DEVICE_TRANSCRIPT=1) and the device path's host re-run hook, all equal
 to the oracle's bytes.
 """
 import ctypes as C
@@ -150,7 +150,7 @@ def test_transcript_input_vector(gpu_ok, product):
 
 @pytest.mark.parametrize("T,b,tau,seed", [(16, 16, 1, 1), (64, 8, 2, 2), (4096, 512, 8, 42), (1 << 15, 333, 3, 4)])
 def test_prove_device_vs_host_transcript(gpu_ok, product, oracle, monkeypatch, T, b, tau, seed):
-    """The same proof with the device transcript (default), the host
+    """The same proof with the host transcript (default), the device
     transcript and the device path's host re-run (z outside the DEEP
     polynomial's domain, forced by a test hook): all equal the oracle's."""
     blocks = product.synthetic_blocks(T, b, tau, seed)
@@ -160,12 +160,13 @@ def test_prove_device_vs_host_transcript(gpu_ok, product, oracle, monkeypatch, T
     ctx.upload(blocks)
     # host first, on a fresh workspace: its challenge record must not lean on
     # what an earlier device-transcript proof left in device memory
-    monkeypatch.setenv("SEZKP_HOST_TRANSCRIPT", "1")
     assert ctx.prove(mroot).proof_bytes == want
-    monkeypatch.delenv("SEZKP_HOST_TRANSCRIPT")
+    monkeypatch.setenv("SEZKP_DEVICE_TRANSCRIPT", "1")
     assert ctx.prove(mroot).proof_bytes == want
     monkeypatch.setenv("SEZKP_DEBUG_FS_RARE", "1")
     assert ctx.prove(mroot).proof_bytes == want
     monkeypatch.delenv("SEZKP_DEBUG_FS_RARE")
+    assert ctx.prove(mroot).proof_bytes == want
+    monkeypatch.delenv("SEZKP_DEVICE_TRANSCRIPT")
     assert ctx.prove(mroot).proof_bytes == want
     ctx.close()

@@ -40,7 +40,8 @@ def main():
     print(f"T=2^{log_t}: jsonl {len(jl)/1e6:.0f} MB written in {time.time()-t0:.1f} s", flush=True)
     del jl, blocks
     res = {}
-    for name, extra in (("single", ["--gpus", "1"]), (f"sharded_host_x{P}", ["--gpus", str(P), "--comm", "host"])):
+    for name, extra in (("single", ["--gpus", "1"]), (f"sharded_host_x{P}", ["--gpus", str(P), "--comm", "host"]),
+                        (f"sharded_host_x{P}_full_ingest", ["--gpus", str(P), "--comm", "host", "--full-ingest"])):
         o = f"/tmp/c5_{name}.cbor"
         t1 = time.time()
         r = subprocess.run([sys.executable, "-m", "sezkp_amd.launch", "prove", "--blocks", bpath, "--manifest", mpath,
