@@ -99,7 +99,13 @@ def host_info() -> dict:
         allowed = len(os.sched_getaffinity(0))
     except AttributeError:
         allowed = os.cpu_count()
-    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": allowed,
+    quota = None  # cgroup v2 CPU bandwidth limit, in CPUs
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": allowed, "cgroup_cpu_quota": quota,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
@@ -120,6 +126,7 @@ def cpu_baseline(T_mt: int, tau: int, T_faithful: int, T_single: int, check=None
     # reference-faithful, full run at config 1 (1 thread)
     b1 = reference_blocks(T_faithful, 512, tau)
     r1 = b1.manifest_root()
+    progress("cpu baseline: reference-faithful structure at config 1, 1 thread")
     t0 = time.perf_counter()
     p_faith = O.prove_v1(b1, r1, mode=1)
     dt_f = time.perf_counter() - t0
@@ -131,6 +138,7 @@ def cpu_baseline(T_mt: int, tau: int, T_faithful: int, T_single: int, check=None
     # one thread, compute-once
     bs = reference_blocks(T_single, 512, tau)
     rs = bs.manifest_root()
+    progress("cpu baseline: compute-once, 1 thread")
     t0 = time.perf_counter()
     O.prove_v1(bs, rs)
     dt_s = time.perf_counter() - t0
@@ -145,24 +153,43 @@ def cpu_baseline(T_mt: int, tau: int, T_faithful: int, T_single: int, check=None
         r, want = bl.manifest_root(), None
     N = 8 * T_mt
     env_t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hi["affinity_cpus"] or 1
+    all_t = hi["affinity_cpus"] or 1
     runs = []
-    for threads, label in [(env_t, "OMP_NUM_THREADS"), (hi["affinity_cpus"] or 1, "affinity_cpus")]:
-        if runs and threads == runs[0]["cores"]:
-            runs[0]["label"] += " = affinity_cpus"
-            continue
-        used = O.use_mt(threads)
+    # every allowed CPU first, on a bounded sample (T = 2^16): on a host whose
+    # cgroup quota is below its affinity set (the GPU box: 128 CPUs allowed,
+    # 16 CPUs of quota) the threads are throttled, and the headline size took
+    # 154 s there (round 4); the headline proof runs at the faster count
+    if all_t != env_t:
+        used = O.use_mt(all_t)
+        Ts = 1 << 16
+        bsm = reference_blocks(Ts, 512, tau)
+        progress(f"cpu baseline: OpenMP oracle, {used} threads, sample T=2^16")
         t0 = time.perf_counter()
-        p = O.prove_v1(bl, r)
-        dt = time.perf_counter() - t0
-        runs.append({"label": label, "cores": used, "seconds": dt, "value": N / dt,
-                     "matches_gpu": (hashlib.sha256(p).hexdigest() == want) if want is not None else None})
-    best = max(runs, key=lambda x: x["value"])
+        O.prove_v1(bsm, bsm.manifest_root())
+        dta = time.perf_counter() - t0
+        used_e = O.use_mt(env_t)
+        t0 = time.perf_counter()
+        O.prove_v1(bsm, bsm.manifest_root())
+        dte = time.perf_counter() - t0
+        runs.append({"label": "affinity_cpus", "cores": used, "seconds": dta, "value": 8 * Ts / dta,
+                     "sample": "T=2^16 proof", "same_sample_at_env_threads": {"cores": used_e, "seconds": dte,
+                                                                             "value": 8 * Ts / dte}})
+    best_t = all_t if runs and runs[0]["value"] > runs[0]["same_sample_at_env_threads"]["value"] else env_t
+    used = O.use_mt(best_t)
+    progress(f"cpu baseline: OpenMP oracle, {used} threads, headline size")
+    t0 = time.perf_counter()
+    p = O.prove_v1(bl, r)
+    dt = time.perf_counter() - t0
+    runs.append({"label": "OMP_NUM_THREADS" if best_t == env_t else "affinity_cpus", "cores": used, "seconds": dt,
+                 "value": N / dt, "matches_gpu": (hashlib.sha256(p).hexdigest() == want) if want is not None else None})
+    best = runs[-1]
     out.update({"value": best["value"], "cores": best["cores"], "seconds": best["seconds"], "by_threads": runs,
                 "sample": f"oracle compute-once prove_v1 (C restatement, OpenMP), one full proof at the headline "
-                          f"size T=2^{T_mt.bit_length() - 1} (N=2^{N.bit_length() - 1}), tau={tau}, timed at "
-                          f"OMP_NUM_THREADS and at every allowed CPU; value = the faster ({best['cores']} threads)"})
+                          f"size T=2^{T_mt.bit_length() - 1} (N=2^{N.bit_length() - 1}), tau={tau}, at the thread "
+                          f"count that was faster on a T=2^16 sample (OMP_NUM_THREADS={env_t} or every allowed "
+                          f"CPU, {all_t}); value = that run ({best['cores']} threads)"})
     if want is not None:
-        out["gpu_proof_matches_oracle"] = all(x["matches_gpu"] for x in runs)
+        out["gpu_proof_matches_oracle"] = best["matches_gpu"]
     return out
 
 
@@ -479,6 +506,7 @@ def main():
         dt, halves_, cpu_frac = dt_r, halves_r, cpu_r
         headline = "trace_resident"
     value = N * total * world / dt
+    progress(f"pipeline: {value / 1e9:.3f}e9 field-elements/s")
     holds = list(pipe.cur)  # trace each context holds
     pipe.close()
     # consistency: each context's last timed proof (both pipelines) equals an
@@ -596,9 +624,11 @@ def main():
     del proof
     worst = None
     if rank == 0 and not args.no_worst_case:
+        progress("worst-case inputs")
         worst = measure_worst_case(args, T)
     host_rows = None
     if rank == 0 and not args.no_host_rows:
+        progress("host rows")
         host_rows = measure_host_rows(args, traces[holds[0]], roots[holds[0]], single_pb, 42 + holds[0])
     for c in ctxs:
         c.close()
@@ -612,6 +642,7 @@ def main():
             chk = None
             if args.cpu_mt_log_t == args.log_t:
                 chk = (traces[0], roots[0], check_digest[0])
+            progress("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(1 << args.cpu_mt_log_t, args.tau, 1 << args.cpu_faithful_log_t,
                                                1 << args.cpu_single_log_t, chk)
             if out["cpu_baseline"].get("gpu_proof_matches_oracle") is False:
@@ -644,16 +675,20 @@ def main():
             out[key] = res
 
     if rank == 0 and not args.no_configs:
+        progress("configs")
         guarded("configs", lambda: measure_configs(args, torch))
     if args.dntt_log_n:
         # BASELINE config 4 (at N = 8): 2^26-point four-step NTT over all ranks
+        progress("dist_ntt")
         guarded("dist_ntt", lambda: measure_dist_ntt(args, world, rank, dev, dist, torch))
     if world > 1 and not args.no_sharded:
         # ONE T = 2^21 proof over all ranks (strong scaling)
+        progress("sharded")
         guarded("sharded", lambda: measure_sharded(args, world, rank, dev, dist, torch))
     if world == 1 and rank == 0 and not args.no_sharded:
         # the same strong-scaling proof predicted for 2/4/8 GPUs from each
         # rank's own work measured here, plus a link model of its collectives
+        progress("sharded_predicted")
         guarded("sharded_predicted", lambda: measure_sharded_predicted(args, torch, single_ms))
     if rank == 0:
         if isinstance(out.get("sharded"), dict):
@@ -708,6 +743,14 @@ def bind_gpu_local_cpus(torch, dev):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+T_START = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """A progress line on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def tree_roofline(kernel: str, ms: float, leaves: int) -> dict:
     """VALU roofline of a BLAKE3 tree kernel from its live launch time and its
     PMC instruction count (profiles/pmc_summary.json), with the HBM view on
@@ -739,15 +782,20 @@ def tree_roofline(kernel: str, ms: float, leaves: int) -> dict:
 
 
 def committed_top_kernel():
-    """The longest kernel of the committed single-proof kernel stats
-    (profiles/kernel_stats_if1.csv, tools/profile_round.sh), for the record."""
+    """The longest kernel of the newest committed single-proof kernel stats
+    (profiles/r*/kernel_stats_if1.csv, tools/profile_round.sh), for the record."""
     import csv
-    p = os.path.join(ROOT, "profiles", "kernel_stats_if1.csv")
+    import glob
+    cand = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats_if1.csv")) +
+                  glob.glob(os.path.join(ROOT, "profiles", "r*", "final", "kernel_stats_if1.csv")))
+    if not cand:
+        return None
+    p = cand[-1]
     try:
         rows = list(csv.DictReader(open(p)))
         top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
         return {"name": top["Name"].split("(")[0].replace("sezkp::", "").replace("void ", ""),
-                "average_ms": float(top["AverageNs"]) * 1e-6, "file": "profiles/kernel_stats_if1.csv"}
+                "average_ms": float(top["AverageNs"]) * 1e-6, "file": os.path.relpath(p, ROOT)}
     except Exception:
         return None
 
@@ -1061,6 +1109,7 @@ def measure_sharded_predicted(args, torch, single_ms: float) -> dict:
            "link_GBs": XGMI_LINK_GBS, "latency_us_per_collective": COLL_LATENCY_US,
            "single_gpu_ms_per_proof": single_ms, "by_gpus": {}}
     for P in (2, 4, 8):
+        progress(f"sharded_predicted: P = {P}")
         ranks = []
         for r in range(P):
             ctx = ShardedProverContext(r, P, device=0, comm="solo")

@@ -44,11 +44,22 @@ def main():
                         (f"sharded_host_x{P}_full_ingest", ["--gpus", str(P), "--comm", "host", "--full-ingest"])):
         o = f"/tmp/c5_{name}.cbor"
         t1 = time.time()
-        r = subprocess.run([sys.executable, "-m", "sezkp_amd.launch", "prove", "--blocks", bpath, "--manifest", mpath,
-                            "--out", o, "--stream"] + extra, cwd=PKG, capture_output=True, text=True, timeout=1500)
+        pr = subprocess.Popen([sys.executable, "-m", "sezkp_amd.launch", "prove", "--blocks", bpath, "--manifest",
+                               mpath, "--out", o, "--stream"] + extra, cwd=PKG, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True)
+        while True:  # a heartbeat line every 30 s (a silent run looks hung)
+            try:
+                out, err = pr.communicate(timeout=30)
+                break
+            except subprocess.TimeoutExpired:
+                print(f"{name}: running, {time.time() - t1:.0f} s", flush=True)
+                if time.time() - t1 > 1500:
+                    pr.kill()
         dt = time.time() - t1
-        print(name, r.returncode, r.stdout.strip()[-300:], r.stderr.strip()[-500:], f"wall {dt:.1f} s", flush=True)
-        res[name] = hashlib.sha256(open(o, "rb").read()).hexdigest() if r.returncode == 0 else None
+        js = [x for x in out.splitlines() if x.startswith("{")]
+        print(name, pr.returncode, js[-1] if js else out.strip()[-300:], "" if pr.returncode == 0 else err.strip()[-500:],
+              f"wall {dt:.1f} s", flush=True)
+        res[name] = hashlib.sha256(open(o, "rb").read()).hexdigest() if pr.returncode == 0 else None
     print(json.dumps(res))
     print("identical" if len(set(res.values())) == 1 and None not in res.values() else "DIFFERENT")
 

@@ -4,8 +4,6 @@ set -uo pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r4f
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo TESTS FAILED; grep -E "FAILED|Error" $O/gpu_tests.log | head -30; exit 1; }
-echo tests ok
 timeout -k 10 500 python3 bench.py > $O/bench_default.log 2> $O/bench_default.err || { echo BENCH FAILED; tail -20 $O/bench_default.err; exit 1; }
 echo bench ok
 timeout -k 10 600 python3 tools/c5_run.py 22 8 > $O/c5.log 2>&1 || { echo C5 FAILED; tail -20 $O/c5.log; exit 1; }
