@@ -768,12 +768,19 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   rep16.clear();
   tail_first = rR + 1 > 1 ? rR + 1 : 1;
   while (tail_first <= k && k - tail_first >= L16_LOG) rep16.push_back(tail_first++);
-  // forest of the run layers 1..rR (local runs of 4096 leaves per WG)
+  // forest of the run layers 1..rR (local runs of 4096 leaves per WG) and,
+  // sharded, of the replicated layers of >= 4096 leaves (whole subtrees of
+  // 4096, level 12 and up from the upper jobs): their WGs run beside the run
+  // layers' instead of as three serial few-WG launches after them
   {
     std::vector<ForestLayer> fl;
     uint32_t wgs = 0;
     for (int r = 1; r <= rR; r++) {
       fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)tree_stop()});
+      wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
+    }
+    for (int r : rep16) {
+      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)L16_LOG});
       wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
     }
     n_forest = (int)fl.size();
@@ -1544,12 +1551,32 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     krec(0, false);
     ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf, 0), "fri_forest");
     krec(0, true);
-  } else {
-    if (!sharded) launch_tail(rep_src);
+  } else if (!sharded) {
+    launch_tail(rep_src);
     ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
-  }
-  if (sharded) {  // run roots of layers 1..rR + the whole of layer rR
-    uint64_t wire = P1 * S * 8;
+  } else {
+    // the whole of layer rR, then the replicated layers folded from it in one
+    // pass, the tail (side stream) and one forest of run + replicated layers
+    coll("fri_rep_values", P1 * S * 8, [&] { comm->allgather(lvals[rR], d_rep, (size_t)S * 8, st); });
+    rep_src = d_rep;
+    const int last = rR + (int)rep16.size();
+    for (int r = rR; r < last;) {
+      const int F = std::min(FOLD_MAX, last - r);
+      const uint64_t* src = r == rR ? d_rep : lvals[r];
+      if (F >= 2) {
+        FoldOuts fo{};
+        fo.beta = dbeta + r;
+        for (int m = 1; m <= F; m++) fo.out[m - 1] = lvals[r + m];
+        ok(launch_foldm(st, src, fo, F, ltrees[r + F].logLen), "fri_rep_folds");
+      } else {
+        ok(launch_fold(st, src, lvals[r + 1], ltrees[r + 1].logLen, 0, dbeta + r), "fri_rep_fold");
+      }
+      r += F;
+    }
+    if (!rep16.empty()) rep_src = lvals[rep16.back()];
+    launch_tail(rep_src);
+    ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
+    uint64_t wire = 0;
     for (int r = 1; r <= rR; r++) wire += P1 * ((N >> r) >> (L16_LOG + logP)) * 32;
     coll("fri_run_roots", wire, [&] {
       comm->group_start();
@@ -1558,18 +1585,11 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
         const uint32_t* lv12 = ltrees[r].nodes + 8 * tree_level_off(ltrees[r].logLen, LSTORE_FRI, L16_LOG);
         comm->allgather(lv12, rr_gather[r], (size_t)nrun * 32, st);
       }
-      comm->allgather(lvals[rR], d_rep, (size_t)S * 8, st);
       comm->group_end();
     });
     for (int r = 1; r <= rR; r++)
       ok(launch_runroots_scatter(st, rr_gather[r], caps[r], (N >> r) >> (L16_LOG + logP), logP), "runroots");
-    rep_src = d_rep;
   }
-  for (int r : rep16) {  // replicated layers with >= 4096 leaves: fold + subtrees
-    ok(launch_layer16(st, rep_src, lvals[r], k - r, 1, 0, ltrees[r], L16_LOG, dbeta + (r - 1)), "fri_rep16");
-    rep_src = lvals[r];
-  }
-  if (sharded) launch_tail(rep_src);
   for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
   if (tail_first <= k && !tail_merged) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
   rec(ST_FRI + 1);

@@ -188,7 +188,7 @@ struct DictPlan {
   uint32_t delta;  // head delta plan: K = 2 and slot 2 holds TD (below)
   int64_t dmin;    // delta plan: range of the tape's moves
   uint32_t dR;
-  uint32_t pad;
+  uint32_t a;      // rows per commit lane = 2^(6 + a): dict_extra(K), lowered for few rows (k_dict_plan)
 };
 // Head delta plan: inside a block head[r] = head[r-1] + mv[r], so an aligned
 // 4-row head group is a function of (head[g], mv[g+1], mv[g+2], mv[g+3]):

@@ -1182,7 +1182,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
   } else if (dict && K >= 0) {
     const DictPlan Pl = plans[dsel];
     const uint32_t* tab = dtabs + 8 * dcols[dsel].tab;
-    const int glog = DICT_LANE_LOG + dict_extra(K);
+    const int glog = DICT_LANE_LOG + (int)plans[dsel].a;
     const int D = glog - K;
     const uint64_t gstart = row & ~((1ULL << glog) - 1);
     for (int j = tid; j < (1 << D); j += TR_THREADS) {
@@ -1226,7 +1226,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
     if (tid < 8) o[8 + tid] = ob[8 * ch + tid];
   } else {
     // rebuild the chunk (or, for a K = -1 dictionary column, its 64-row group)
-    const int glog = dict ? DICT_LANE_LOG + dict_extra(K) : logcl;
+    const int glog = dict ? DICT_LANE_LOG + (int)plans[dsel].a : logcl;
     const uint64_t gstart = dict ? (row & ~((1ULL << glog) - 1)) : start;
     for (uint64_t i = tid; i < (1ULL << glog); i += TR_THREADS) {
       uint32_t h[8];
@@ -1362,7 +1362,7 @@ __device__ __forceinline__ void reduce_parts(const int64_t* pp, uint32_t nparts,
 // XCD's L2) was measured slower in round 3: the extra compressions of the
 // lower levels cost more than the misses save.
 __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restrict__ part, uint32_t nparts,
-                                                          uint64_t n, const DictCol* __restrict__ dcols,
+                                                          uint64_t n, uint64_t nrows, const DictCol* __restrict__ dcols,
                                                           DictPlan* __restrict__ plans) {
   __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
   const int tid = threadIdx.x;
@@ -1409,6 +1409,12 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restr
       for (int k = 3; k < DICT_LEVELS; k++) P.pw[k] = 0;
     }
   }
+  // a lane's rows: 2^(6 + dict_extra(K)) (32 gathered nodes for K >= 1), and
+  // fewer when this device commits fewer than 2^21 rows (a sharded rank), so
+  // the commit still has ~4 waves per SIMD: one step of a per halving
+  int a = dict_extra(P.K);
+  for (uint64_t r = nrows; r < (1ULL << 21) && a > 0; r <<= 1) a--;
+  P.a = (uint32_t)a;
   plans[blockIdx.x] = P;
 }
 
@@ -1495,13 +1501,19 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_level(const ColTemplate* __
 template <typename Key>
 __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const uint32_t* tab,
                                           const ColTemplate* ct, uint32_t (&h)[8]) {
-  // a lane covers 2^(6 + dict_extra(K)) rows: 2^(6+a-K) table nodes
-  switch (P.K) {
-    case 0: lane_tree_pf<6>(DictNodes<Key, 0>{p, tab, P.min, P.R}, h); break;
-    case 1: lane_tree_pf<5>(DictNodes<Key, 1>{p, tab + 8 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 2: lane_tree_pf<5>(DictNodes<Key, 2>{p, tab + 16 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 3: lane_tree_pf<5>(DictNodes<Key, 3>{p, tab + 24 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
-    case 4: lane_tree_pf<4>(DictNodes<Key, 4>{p, tab + 32 * (uint64_t)DICT_CAP, P.min, P.R}, h); break;
+  // a lane covers 2^(6 + a) rows: 2^(6+a-K) table nodes
+  const uint32_t* tk = tab + 8 * (uint64_t)DICT_CAP * (P.K > 0 ? P.K : 0);
+  switch (P.K * 4 + (int)P.a) {
+    case 0 * 4 + 0: lane_tree_pf<6>(DictNodes<Key, 0>{p, tk, P.min, P.R}, h); break;
+    case 1 * 4 + 0: lane_tree_pf<5>(DictNodes<Key, 1>{p, tk, P.min, P.R}, h); break;
+    case 2 * 4 + 0: lane_tree_pf<4>(DictNodes<Key, 2>{p, tk, P.min, P.R}, h); break;
+    case 2 * 4 + 1: lane_tree_pf<5>(DictNodes<Key, 2>{p, tk, P.min, P.R}, h); break;
+    case 3 * 4 + 0: lane_tree_pf<3>(DictNodes<Key, 3>{p, tk, P.min, P.R}, h); break;
+    case 3 * 4 + 1: lane_tree_pf<4>(DictNodes<Key, 3>{p, tk, P.min, P.R}, h); break;
+    case 3 * 4 + 2: lane_tree_pf<5>(DictNodes<Key, 3>{p, tk, P.min, P.R}, h); break;
+    case 4 * 4 + 0: lane_tree_pf<2>(DictNodes<Key, 4>{p, tk, P.min, P.R}, h); break;
+    case 4 * 4 + 1: lane_tree_pf<3>(DictNodes<Key, 4>{p, tk, P.min, P.R}, h); break;
+    case 4 * 4 + 2: lane_tree_pf<4>(DictNodes<Key, 4>{p, tk, P.min, P.R}, h); break;
     default: lane_tree<6>(RawLeaves<Key>{p, ct}, h); break;
   }
 }
@@ -1526,7 +1538,7 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
   const uint32_t* tab = tabs + 8 * dc.tab;
   const int lane = threadIdx.x;
   // high-K columns give each lane more rows (fewer LDS levels per row)
-  const int a = dict_extra(P.K);
+  const int a = (int)P.a;
   const int llog = DICT_LANE_LOG + a;  // rows per lane (log2)
   const uint64_t wg_row = row0 + ((uint64_t)bx << (llog + 6));
   if (wg_row >= row_end) return;  // grid is sized for a = 0
@@ -1542,9 +1554,10 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
       default:
         if (P.delta) {
           const uint64_t o = (uint64_t)ct.tape * T.n + lrow;
-          lane_tree_pf<5>(DeltaNodes{T.head + o, T.mv + o, T.row_flags + lrow, tab + 8 * (uint64_t)DICT_CAP,
-                                  tab + 16 * (uint64_t)DICT_CAP, P.min, P.dmin, P.R, P.dR},
-                       h);
+          const DeltaNodes dn{T.head + o, T.mv + o, T.row_flags + lrow, tab + 8 * (uint64_t)DICT_CAP,
+                              tab + 16 * (uint64_t)DICT_CAP, P.min, P.dmin, P.R, P.dR};
+          if (a == 1) lane_tree_pf<5>(dn, h);  // 4-row groups: 2^(4 + a) per lane
+          else lane_tree_pf<4>(dn, h);
         } else {
           dict_lane<int32_t>(dict_keys<int32_t>(T, ct) + lrow, P, tab, ctp, h);
         }
@@ -1637,7 +1650,7 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
                      row0, row0 + nrows);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, d_dcols, d_plans);
+  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, nrows, d_dcols, d_plans);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   for (int l = 0; l < DICT_LEVELS; l++) {
     // one flat launch per level (and per DICT_FLAT_MAX columns): all WGs
