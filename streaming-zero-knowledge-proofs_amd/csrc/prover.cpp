@@ -771,16 +771,18 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   // forest of the run layers 1..rR (local runs of 4096 leaves per WG) and,
   // sharded, of the replicated layers of >= 4096 leaves (whole subtrees of
   // 4096, level 12 and up from the upper jobs): their WGs run beside the run
-  // layers' instead of as three serial few-WG launches after them
+  // layers' instead of as three serial few-WG launches after them, and come
+  // first in the grid (each is one WG's 4096-leaf chain: started last, they
+  // would set the launch's end)
   {
     std::vector<ForestLayer> fl;
     uint32_t wgs = 0;
-    for (int r = 1; r <= rR; r++) {
-      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)tree_stop()});
-      wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
-    }
     for (int r : rep16) {
       fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)L16_LOG});
+      wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
+    }
+    for (int r = 1; r <= rR; r++) {
+      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)tree_stop()});
       wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
     }
     n_forest = (int)fl.size();
