@@ -1277,14 +1277,23 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
                         row_hi - row_lo, d_dlev),
      "col_commit_dict");
   HIP_OR_THROW(hipStreamWaitEvent(st, ev_cols, 0));
+  // test hook: SEZKP_DEBUG_TRIP_GUARD=<rank> sets that rank's guard word, to
+  // check that the failure is collective (tests/test_gpu_sharded.py)
+  static const char* trip = getenv("SEZKP_DEBUG_TRIP_GUARD");
+  if (trip && atoi(trip) == rank) HIP_OR_THROW(hipMemsetAsync(d_err, 0x7f, 1, st));
   if (sharded) {
+    // the chunk roots of every column and every rank's guard word in one
+    // group: sharded ranks see all guard words, so a trip on any rank makes
+    // ALL ranks fail at the first check, before the next collective (no rank
+    // is left blocked in an RCCL call its peers never reach)
     const size_t bytes = (size_t)(ch_hi - ch_lo) * 32;
-    coll("col_chunk_roots", P1 * bytes * ncols, [&] {
+    coll("col_chunk_roots", P1 * (bytes * ncols + 4), [&] {
       comm->group_start();
       for (int c = 0; c < ncols; c++) {
         uint32_t* lvl0 = d_outer + (size_t)c * outer_stride * 8;
         comm->allgather(lvl0 + ch_lo * 8, lvl0, bytes, st);
       }
+      comm->allgather(d_err, d_err + 8, 4, st);
       comm->group_end();
     });
   }
@@ -1292,9 +1301,6 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   TreeDev outer0{d_outer, d_colroots, logChunks, 0};
   ok(launch_tree_upper(st, &outer0, ncols, outer_stride, 8, 0), "col_outer");
   rec(3);
-  // guard words: sharded ranks gather every rank's word, so a trip on any
-  // rank makes ALL ranks fail here, before the next collective (no rank is
-  // left blocked in an RCCL call its peers never reach)
   const int nguard = sharded ? comm->world : 1;
   auto check_guards = [&](const uint32_t* g_h, int ng) {
     for (int r = 0; r < ng; r++) {
@@ -1306,11 +1312,6 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
       if (g) throw Err{SEZKP_E_DEVICE, "column commitment guard tripped" + who + " (code " + std::to_string(g) + ")"};
     }
   };
-  // test hook: SEZKP_DEBUG_TRIP_GUARD=<rank> sets that rank's guard word, to
-  // check that the failure is collective (tests/test_gpu_sharded.py)
-  static const char* trip = getenv("SEZKP_DEBUG_TRIP_GUARD");
-  if (trip && atoi(trip) == rank) HIP_OR_THROW(hipMemsetAsync(d_err, 0x7f, 1, st));
-  if (sharded) coll("guard_words", P1 * 4, [&] { comm->allgather(d_err, d_err + 8, 4, st); });
   // ---- transcript prelude + column roots (prover.rs:67-81) -> alphas,
   // masks, z. Every rank replays the same transcript, so challenges need no
   // broadcast. Device mode: one workgroup derives them on the stream (no host

@@ -79,7 +79,7 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
         assert calls["alltoall"] == 6 and calls["allreduce"] == 2 and calls["allgather"] > 0
         # sezkp_ctx_comm_stats: one entry per collective of the last prove
         st = {c["name"]: c for c in calls["stats"]}
-        assert {"col_chunk_roots", "guard_words", "intt_alltoall1", "intt_alltoall2", "intt_coeffs",
+        assert {"col_chunk_roots", "intt_alltoall1", "intt_alltoall2", "intt_coeffs",
                 "lde_alltoall", "layer0_run_roots", "fri_run_roots", "proof_allreduce"} <= set(st), sorted(st)
         assert all(c["bytes"] > 0 and c["ms"] >= 0 for c in calls["stats"])
 
