@@ -213,10 +213,13 @@ __global__ void __launch_bounds__(MK_THREADS) k_leaf_subtree(const uint64_t* __r
 
 // ------------------------------------------------------------ upper levels
 // Input: stored level `from` (count 2^(logLen-from)); one WG reduces up to
-// 1024 nodes (4 per lane, 2 levels in registers) and stores every level.
-__device__ __forceinline__ void upper_wg(const TreeDev& T, int from, uint64_t wg, uint32_t (*lds)[MK_THREADS]) {
+// 1024 nodes (4 per lane, 2 levels in registers) and stores every level, up
+// to level `to` (0: the root).
+__device__ __forceinline__ void upper_wg(const TreeDev& T, int from, uint64_t wg, uint32_t (*lds)[MK_THREADS],
+                                         int to = 0) {
   const int tid = threadIdx.x;
-  const int cnt_log = T.logLen - from;
+  const int top = (to > 0 && to < T.logLen) ? to : T.logLen;
+  const int cnt_log = top - from;
   const int sub_log = cnt_log < 10 ? cnt_log : 10;
   const int logper = cnt_log < 2 ? cnt_log : 2;
   const int nact = 1 << (sub_log - logper);
@@ -266,7 +269,7 @@ __global__ void __launch_bounds__(MK_THREADS) k_tree_upper(TreeDev T0, uint64_t 
 __global__ void __launch_bounds__(MK_THREADS) k_upper_jobs(const UpperJob* __restrict__ jobs) {
   __shared__ uint32_t lds[8][MK_THREADS];
   const UpperJob J = jobs[blockIdx.x];
-  upper_wg(J.tree, J.from, J.wg, lds);
+  upper_wg(J.tree, J.from, J.wg, lds, J.to);
 }
 
 // ------------------------------------------------- layers of >= 4096 leaves
@@ -287,22 +290,27 @@ __device__ __forceinline__ void subtree_regs(const uint64_t (&v)[16], uint64_t i
   }
 }
 
-// One WG = 4096 leaves, 16 consecutive leaves per lane folded to a level-4
-// node in registers (binary counter: 31 compressions per lane, all lanes
-// busy), then levels 5..12 through LDS. fold == 1 computes the layer from the
-// previous one first (y'_i = in[i] + beta*in[i+len]) and writes it to out.
-// Levels above 12 are left to the upper-level jobs.
+// One WG = 256 << LPL leaves: 2^LPL consecutive leaves per lane folded to a
+// level-LPL node in registers (binary counter; LPL = 4: 31 compressions per
+// lane, all lanes busy), then levels LPL+1 .. 8+LPL through LDS. fold == 1
+// computes the layer from the previous one first (y'_i = in[i] + beta*in[i+len])
+// and writes it to out. Levels above `stop` are left to the upper-level jobs.
+// LPL = 4 (4096-leaf WGs) for large trees; LPL = 2 (1024 leaves) when a
+// launch has too few 4096-leaf WGs to fill the chip (small shards and
+// traces): a WG's 31 dependent compressions per lane then ran at one or two
+// waves per SIMD.
+template <int LPL>
 __device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int logLen,
                                            int fold, uint64_t beta, const TreeDev& T, uint64_t wg,
                                            uint32_t (*lds)[MK_THREADS], int stop) {
   const int tid = threadIdx.x;
   const uint64_t len = 1ULL << logLen;
-  const uint64_t i0 = (wg << L16_LOG) + ((uint64_t)tid << 4);
+  const uint64_t i0 = (wg << (8 + LPL)) + ((uint64_t)tid << LPL);
   uint64_t v[16];
   {
     const ulonglong2* p = reinterpret_cast<const ulonglong2*>(in + i0);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < (1 << LPL) / 2; k++) {
       const ulonglong2 a = p[k];
       v[2 * k] = a.x;
       v[2 * k + 1] = a.y;
@@ -312,7 +320,7 @@ __device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint
     const ulonglong2* q = reinterpret_cast<const ulonglong2*>(in + i0 + len);
     ulonglong2* o = reinterpret_cast<ulonglong2*>(out + i0);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < (1 << LPL) / 2; k++) {
       const ulonglong2 b = q[k];
       v[2 * k] = gl_add(v[2 * k], gl_mul(beta, b.x));
       v[2 * k + 1] = gl_add(v[2 * k + 1], gl_mul(beta, b.y));
@@ -320,18 +328,19 @@ __device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint
     }
   }
   uint32_t h[8];
-  subtree_regs<4, 0>(v, i0, T, h);
+  subtree_regs<LPL, 0>(v, i0, T, h);
   lds_put(lds, tid, h);
   __syncthreads();
-  wg_reduce(lds, MK_THREADS, 4, wg, T, stop);
+  wg_reduce(lds, MK_THREADS, LPL, wg, T, stop);
 }
 
+template <int LPL>
 __global__ void __launch_bounds__(MK_THREADS) k_layer16(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
                                                         int logLen, int fold, uint64_t beta,
                                                         const uint64_t* __restrict__ dbeta, TreeDev T, int stop) {
   __shared__ uint32_t lds[8][MK_THREADS];
   if (dbeta) beta = *dbeta;
-  layer16_wg(in, out, logLen, fold, beta, T, blockIdx.x, lds, stop);
+  layer16_wg<LPL>(in, out, logLen, fold, beta, T, blockIdx.x, lds, stop);
 }
 
 // FRI fold y'_i = y_i + beta * y_{i+len} (prover.rs:200-239), 4 per lane.
@@ -521,6 +530,7 @@ __device__ __forceinline__ void fri_tail_wg(const TailArgs& A, int j, uint64_t* 
 // `ntail` workgroups build the layers of <= 2048 leaves (fri_tail_wg).
 // A launch may cover a sub-range of the layers: `layers` then points at its
 // first one and wg_base is that layer's wg_start (wg_start values are global).
+template <int LPL>
 __global__ void __launch_bounds__(MK_THREADS) k_forest16(const ForestLayer* __restrict__ layers, int nlayers,
                                                          TailArgs A, int ntail, uint64_t* __restrict__ tailbuf,
                                                          uint32_t wg_base) {
@@ -533,7 +543,7 @@ __global__ void __launch_bounds__(MK_THREADS) k_forest16(const ForestLayer* __re
   int l = 0;
   while (l + 1 < nlayers && layers[l + 1].wg_start <= b) l++;
   const ForestLayer F = layers[l];
-  layer16_wg(F.vals, nullptr, F.tree.logLen, 0, 0, F.tree, b - F.wg_start, lds, (int)F.stop);
+  layer16_wg<LPL>(F.vals, nullptr, F.tree.logLen, 0, 0, F.tree, b - F.wg_start, lds, (int)F.stop);
 }
 
 // ------------------------------------------------ sharded layout changes
@@ -711,10 +721,14 @@ hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out
 }
 
 hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
-                          TreeDev tree, int stop, const uint64_t* dbeta) {
-  if (logLen < L16_LOG || stop < tree.lstore || stop > L16_LOG) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_layer16, dim3((unsigned)(1ULL << (logLen - L16_LOG))), dim3(MK_THREADS), 0, st, in, out_vals,
-                     logLen, fold, beta, dbeta, tree, stop);
+                          TreeDev tree, int stop, const uint64_t* dbeta, int wg_log) {
+  if ((wg_log != L16_LOG && wg_log != L16S_LOG) || logLen < wg_log || stop < tree.lstore || stop > wg_log)
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(1ULL << (logLen - wg_log)));
+  if (wg_log == L16_LOG)
+    hipLaunchKernelGGL(k_layer16<4>, grid, dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, dbeta, tree, stop);
+  else
+    hipLaunchKernelGGL(k_layer16<2>, grid, dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, dbeta, tree, stop);
   return hipGetLastError();
 }
 
@@ -740,13 +754,19 @@ hipError_t launch_foldm(hipStream_t st, const uint64_t* in, const FoldOuts& outs
 }
 
 hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs,
-                           const TailArgs* tail, uint64_t* tailbuf, uint32_t wg_base) {
+                           const TailArgs* tail, uint64_t* tailbuf, uint32_t wg_base, int wg_log) {
   if (nlayers <= 0) return tail ? hipErrorInvalidValue : hipSuccess;
   if (tail && (tail->Ls < 0 || tail->Ls >= TAIL_MAX || !tailbuf)) return hipErrorInvalidValue;
   const int ntail = tail ? tail->Ls + 1 : 0;
   const TailArgs none{};
-  hipLaunchKernelGGL(k_forest16, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
-                     tail ? *tail : none, ntail, tailbuf, wg_base);
+  if (wg_log == L16_LOG)
+    hipLaunchKernelGGL(k_forest16<4>, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
+                       tail ? *tail : none, ntail, tailbuf, wg_base);
+  else if (wg_log == L16S_LOG)
+    hipLaunchKernelGGL(k_forest16<2>, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
+                       tail ? *tail : none, ntail, tailbuf, wg_base);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -762,13 +782,15 @@ hipError_t launch_upper_jobs(hipStream_t st, const UpperJob* d_jobs, int njobs) 
   return hipGetLastError();
 }
 
-void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes) {
+void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes, int to) {
+  const int top = (to > 0 && to < T.logLen) ? to : T.logLen;
   int p = 0;
-  while (from < T.logLen) {
-    const int c = T.logLen - from;
+  while (from < top) {
+    const int c = top - from;
     const int step = c < 10 ? c : 10;
     if ((int)passes.size() <= p) passes.resize(p + 1);
-    for (uint64_t w = 0; w < (1ULL << (c - step)); w++) passes[p].push_back(UpperJob{T, from, (uint32_t)w, 0});
+    for (uint64_t w = 0; w < (1ULL << (T.logLen - from - step)); w++)
+      passes[p].push_back(UpperJob{T, from, (uint32_t)w, to, 0});
     from += step;
     p++;
   }

@@ -250,6 +250,10 @@ struct sezkp_ctx {
   // level the run-layer WGs reduce to: the run root (12) when run roots are
   // allgathered, else 6 so the upper jobs build levels 7.. with every lane busy
   int tree_stop() const { return sharded() ? L16_LOG : LSTORE_FRI; }
+  // leaves per WG of the layer-0 tree and the forest: 4096, or 1024 when the
+  // local LDE has at most 2^22 points (too few 4096-leaf WGs to fill the chip)
+  int tree_wg_log = L16_LOG;
+  int wg_stop() const { return std::min(tree_stop(), tree_wg_log); }
   uint64_t M = 0;                       // local LDE length N / P
   int logM = 0;
   int rR = -1;                          // run layers 0..rR (len >= 4096 P), the rest replicated
@@ -270,6 +274,7 @@ struct sezkp_ctx {
   uint32_t forest_wgs = 0;
   UpperJob* d_jobs = nullptr;  // upper-level passes: layer 0, then all fold layers
   std::vector<std::pair<size_t, int>> jobs0, jobsF;
+  std::vector<std::pair<size_t, int>> jobsL0, jobsLR;  // sharded, 1024-leaf WGs: run trees' levels 11..12
   uint32_t* d_req = nullptr;
   uint32_t* h_req = nullptr;
   ProofLayout PL{};             // device proof body (after the column-root header)
@@ -710,6 +715,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   }
   M = N >> logP;
   logM = logN - logP;
+  tree_wg_log = M <= (1ULL << 22) ? L16S_LOG : L16_LOG;
   rR = sharded() ? k - L16_LOG - logP : (k >= L16_LOG ? k - L16_LOG : -1);
   d_lde = dalloc<uint64_t>(M);
   if (sharded()) {
@@ -778,12 +784,12 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
     std::vector<ForestLayer> fl;
     uint32_t wgs = 0;
     for (int r : rep16) {
-      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)L16_LOG});
-      wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
+      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)std::min(L16_LOG, tree_wg_log)});
+      wgs += (uint32_t)(1ULL << (ltrees[r].logLen - tree_wg_log));
     }
     for (int r = 1; r <= rR; r++) {
-      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)tree_stop()});
-      wgs += (uint32_t)(1ULL << (ltrees[r].logLen - L16_LOG));
+      fl.push_back(ForestLayer{lvals[r], ltrees[r], wgs, (uint32_t)wg_stop()});
+      wgs += (uint32_t)(1ULL << (ltrees[r].logLen - tree_wg_log));
     }
     n_forest = (int)fl.size();
     forest_wgs = wgs;
@@ -793,21 +799,35 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   }
   // upper levels (> 12): layer 0's cap, then every other cap / replicated tree
   {
-    std::vector<std::vector<UpperJob>> p0, pF;
+    std::vector<std::vector<UpperJob>> p0, pF, pL0, pLR;
     // run layers start from the level their layer16 WGs stopped at
     const int from = tree_stop();
     if (rR >= 0 && caps[0].logLen > from) plan_upper_jobs(caps[0], from, p0);
+    const int rep_from = std::min(L16_LOG, tree_wg_log);
     for (int r = 1; r <= k; r++) {
       const bool runl = r <= rR;
       if ((runl || std::find(rep16.begin(), rep16.end(), r) != rep16.end()) &&
-          caps[r].logLen > (runl ? from : L16_LOG))
-        plan_upper_jobs(caps[r], runl ? from : L16_LOG, pF);
+          caps[r].logLen > (runl ? from : rep_from))
+        plan_upper_jobs(caps[r], runl ? from : rep_from, pF);
+    }
+    // sharded with 1024-leaf WGs: the run trees' levels 11..12 (the run roots
+    // the caps are gathered from) by upper jobs before each allgather
+    if (sharded() && wg_stop() < L16_LOG && rR >= 0) {
+      plan_upper_jobs(ltrees[0], wg_stop(), pL0, L16_LOG);
+      for (int r = 1; r <= rR; r++) plan_upper_jobs(ltrees[r], wg_stop(), pLR, L16_LOG);
     }
     std::vector<UpperJob> all;
     jobs0.clear();
     jobsF.clear();
-    for (auto& v : p0) { jobs0.push_back({all.size(), (int)v.size()}); all.insert(all.end(), v.begin(), v.end()); }
-    for (auto& v : pF) { jobsF.push_back({all.size(), (int)v.size()}); all.insert(all.end(), v.begin(), v.end()); }
+    jobsL0.clear();
+    jobsLR.clear();
+    auto add = [&](std::vector<std::vector<UpperJob>>& ps, std::vector<std::pair<size_t, int>>& out) {
+      for (auto& v : ps) { out.push_back({all.size(), (int)v.size()}); all.insert(all.end(), v.begin(), v.end()); }
+    };
+    add(p0, jobs0);
+    add(pF, jobsF);
+    add(pL0, jobsL0);
+    add(pLR, jobsLR);
     d_jobs = dalloc<UpperJob>(all.size() + 1);
     if (!all.empty()) up(d_jobs, all.data(), all.size());
   }
@@ -1472,8 +1492,10 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   rec(7);
   // ---- layer-0 tree: local runs, then the cap from allgathered run roots
   if (rR >= 0) {
-    ok(launch_layer16(st, d_lde, nullptr, ltrees[0].logLen, 0, 0, ltrees[0], tree_stop()), "layer0_tree");
+    ok(launch_layer16(st, d_lde, nullptr, ltrees[0].logLen, 0, 0, ltrees[0], wg_stop(), nullptr, tree_wg_log),
+       "layer0_tree");
     rec(ST_L0TREE + 1);
+    for (auto& p : jobsL0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_runroots");
     if (sharded) {
       const uint64_t nrun = M >> L16_LOG;
       const uint32_t* lv12 = ltrees[0].nodes + 8 * tree_level_off(ltrees[0].logLen, LSTORE_FRI, L16_LOG);
@@ -1552,11 +1574,11 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   if (tail_merged) {
     const TailArgs ta = tail_args(rep_src);
     krec(0, false);
-    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf, 0), "fri_forest");
+    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf, 0, tree_wg_log), "fri_forest");
     krec(0, true);
   } else if (!sharded) {
     launch_tail(rep_src);
-    ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
+    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, nullptr, nullptr, 0, tree_wg_log), "fri_forest");
   } else {
     // the whole of layer rR, then the replicated layers folded from it in one
     // pass, the tail (side stream) and one forest of run + replicated layers
@@ -1578,7 +1600,8 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     }
     if (!rep16.empty()) rep_src = lvals[rep16.back()];
     launch_tail(rep_src);
-    ok(launch_forest16(st, d_forest, n_forest, forest_wgs), "fri_forest");
+    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, nullptr, nullptr, 0, tree_wg_log), "fri_forest");
+    for (auto& p : jobsLR) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_runroots");
     uint64_t wire = 0;
     for (int r = 1; r <= rR; r++) wire += P1 * ((N >> r) >> (L16_LOG + logP)) * 32;
     coll("fri_run_roots", wire, [&] {

@@ -370,16 +370,20 @@ struct UpperJob {
   TreeDev tree;
   int from;
   uint32_t wg;
-  uint64_t pad;
+  int to;  // last level to build (0: up to the root)
+  uint32_t pad;
 };
-void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes);
+void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes, int to = 0);
 hipError_t launch_upper_jobs(hipStream_t st, const UpperJob* d_jobs, int njobs);
 
 constexpr int L16_LOG = 12;  // leaves per WG of the 16-leaves-per-lane layer kernel
+constexpr int L16S_LOG = 10; // leaves per WG of its 4-leaves-per-lane form (small trees)
 // stop: highest level the WG reduces to (L16_LOG = its run root; LSTORE_FRI
 // leaves levels 7..12 to the upper jobs, whose lanes are all busy)
+// wg_log: leaves per WG (L16_LOG, or L16S_LOG for trees too small to fill
+// the chip with 4096-leaf WGs); stop <= wg_log
 hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
-                          TreeDev tree, int stop = L16_LOG, const uint64_t* dbeta = nullptr);
+                          TreeDev tree, int stop = L16_LOG, const uint64_t* dbeta = nullptr, int wg_log = L16_LOG);
 // Fold chain kernel (values only) and the one-launch forest of layer trees.
 hipError_t launch_fold(hipStream_t st, const uint64_t* in, uint64_t* out, int logLen, uint64_t beta,
                        const uint64_t* dbeta = nullptr);
@@ -411,7 +415,8 @@ hipError_t launch_fri_tail(hipStream_t st, const TailArgs& a);
 // the forest of layer trees >= 4096 leaves; tail != null: its first workgroups
 // also build the small layers (fri_tail_wg), tailbuf = TAIL_MAX x 4096 u64 scratch
 hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlayers, uint32_t total_wgs,
-                           const TailArgs* tail = nullptr, uint64_t* tailbuf = nullptr, uint32_t wg_base = 0);
+                           const TailArgs* tail = nullptr, uint64_t* tailbuf = nullptr, uint32_t wg_base = 0,
+                           int wg_log = L16_LOG);
 // requests: (layer, index, ordinal in the proof's FRI records) triples
 // d_count != null: the number of requests is read on the device (grid = nreq, the most possible)
 hipError_t launch_fri_paths(hipStream_t st, const FriLayerDev* d_layers, const uint32_t* d_req, int nreq,
