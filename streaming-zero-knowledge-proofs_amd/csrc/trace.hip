@@ -1269,21 +1269,23 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
 
 constexpr int DICT_WG_ROWS = 64 << DICT_LANE_LOG;                    // 4096 rows per 64-lane WG
 constexpr int DICT_RANGE_STEP = TR_THREADS * 16;                     // rows per WG sweep
-constexpr int DICT_RANGE_ROWS = DICT_RANGE_STEP * 8;                  // rows per range WG
 
-// per-(column, 32768 rows) min / max of the raw integers: 8 sweeps of 16 rows
-// per lane (one 16-byte-or-less load each), so the grid stays ~2K workgroups
+// per-(column, part) min / max of the raw integers: `sweeps` (1..8) sweeps of
+// 16 rows per lane (one 16-byte-or-less load each); parts of 32768 rows keep
+// the grid at ~2K workgroups for 2^21 rows, and a device with fewer rows (a
+// sharded rank) takes smaller parts, so every column still has ~64 of them
 __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                            const DictCol* __restrict__ dcols,
                                                            int64_t* __restrict__ part, uint32_t nparts,
-                                                           uint64_t row0, uint64_t row_end) {
+                                                           uint64_t row0, uint64_t row_end, int sweeps) {
   __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
   const ColTemplate ct = tmpl[dcols[blockIdx.y].col];
   const int tid = threadIdx.x;
   int64_t lo = INT64_MAX, hi = INT64_MIN;
   if (ct.kind == 6) {  // head: the per-block ranges of k_expand over the blocks meeting this part
-    const uint64_t p0 = row0 + (uint64_t)blockIdx.x * DICT_RANGE_ROWS;
-    const uint64_t p1 = p0 + DICT_RANGE_ROWS < row_end ? p0 + DICT_RANGE_ROWS : row_end;
+    const uint64_t prow = (uint64_t)sweeps * DICT_RANGE_STEP;
+    const uint64_t p0 = row0 + (uint64_t)blockIdx.x * prow;
+    const uint64_t p1 = p0 + prow < row_end ? p0 + prow : row_end;
     const int64_t* hr = T.head_rng + 2 * ((uint64_t)ct.tape * T.nblk);
     for (uint32_t b = T.row_blk[p0] + tid; b <= T.row_blk[p1 - 1]; b += TR_THREADS) {
       lo = hr[2 * b] < lo ? hr[2 * b] : lo;
@@ -1291,8 +1293,8 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const Col
     }
   } else {  // narrow keys: 32-bit min / max
     int32_t l32 = INT32_MAX, h32 = INT32_MIN;
-    for (int sw = 0; sw < DICT_RANGE_ROWS / DICT_RANGE_STEP; sw++) {
-      const uint64_t r0 = row0 + (uint64_t)blockIdx.x * DICT_RANGE_ROWS + (uint64_t)sw * DICT_RANGE_STEP +
+    for (int sw = 0; sw < sweeps; sw++) {
+      const uint64_t r0 = row0 + (uint64_t)blockIdx.x * ((uint64_t)sweeps * DICT_RANGE_STEP) + (uint64_t)sw * DICT_RANGE_STEP +
                           (uint64_t)tid * 16;
       if (r0 >= row_end) break;
       int64_t k[16];
@@ -1645,9 +1647,12 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
   if (ndict == 0) return hipSuccess;
   if (T.n < (1ULL << COL_CHUNK_LOG2)) return hipErrorInvalidValue;
   if (row0 + nrows > T.n || (nrows != T.n && (row0 % DICT_WG_ROWS || nrows % DICT_WG_ROWS))) return hipErrorInvalidValue;
-  const uint32_t nparts = (uint32_t)((nrows + DICT_RANGE_ROWS - 1) / DICT_RANGE_ROWS);
+  // parts of 1..8 sweeps: ~64 per column (the partial buffer holds n / 4096)
+  const int sweeps = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, nrows / (64ull * DICT_RANGE_STEP)));
+  const uint64_t prow = (uint64_t)sweeps * DICT_RANGE_STEP;
+  const uint32_t nparts = (uint32_t)((nrows + prow - 1) / prow);
   hipLaunchKernelGGL(k_dict_range, dim3(nparts, ndict), dim3(TR_THREADS), 0, st, T, d_tmpl, d_dcols, d_part, nparts,
-                     row0, row0 + nrows);
+                     row0, row0 + nrows, sweeps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, nrows, d_dcols, d_plans);

@@ -1,0 +1,9 @@
+set -uo pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r4i
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo TESTS FAILED; grep -E "FAILED|Error" $O/gpu_tests.log | head -30; exit 1; }
+echo tests ok
+timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/solo8 -o run -- python3 tools/solo_trace.py 8 0 21 > $O/solo8.log 2>&1 || exit 1
+timeout -k 10 400 python3 bench.py --no-cpu-baseline --no-worst-case --no-host-rows > $O/bench.log 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+echo done
