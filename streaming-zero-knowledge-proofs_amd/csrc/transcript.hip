@@ -60,19 +60,31 @@ constexpr int ROT1 = 0x39, ROT2 = 0x4E, ROT3 = 0x93;  // lane i <- lane i + 1 / 
   a = a + b + (y); d = fs_rotr(d ^ a, 8);      \
   c = c + d;       b = fs_rotr(b ^ c, 7);
 
-// One BLAKE3 compression on a quad. m: the quad's 16 message words (LDS).
-// In: h0 = cv[li], h1 = cv[4 + li]. Out: words li, 4 + li, 8 + li, 12 + li
-// of the 16-word output (the first two are the next chaining value).
-__device__ __forceinline__ void b3q(const uint32_t* m, int li, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                    uint32_t& h3, uint64_t ctr, uint32_t blen, uint32_t flags) {
+// One BLAKE3 compression on a quad. m: the quad's 16 message words (LDS);
+// midx: this lane's FS_MIDX row, loaded once per kernel. In: h0 = cv[li],
+// h1 = cv[4 + li]. Out: words li, 4 + li, 8 + li, 12 + li of the 16-word
+// output (the first two are the next chaining value). All 28 message words
+// of the lane are read from LDS before the first round, so the rounds are a
+// pure ALU / DPP chain.
+__device__ __forceinline__ void b3q(const uint32_t* m, int li, const uint32_t (&midx)[7], uint32_t& h0,
+                                    uint32_t& h1, uint32_t& h2, uint32_t& h3, uint64_t ctr, uint32_t blen,
+                                    uint32_t flags) {
   const uint32_t IVQ[4] = {B3_IV0, B3_IV1, B3_IV2, B3_IV3};
   uint32_t a = h0, b = h1, c = IVQ[li];
   uint32_t d = li == 0 ? (uint32_t)ctr : li == 1 ? (uint32_t)(ctr >> 32) : li == 2 ? blen : flags;
   const uint32_t cv0 = h0, cv1 = h1;
+  uint32_t mw[28];
 #pragma unroll
   for (int r = 0; r < 7; r++) {
-    const uint32_t mi = FS_MIDX[r][li];
-    const uint32_t cx = m[mi & 0xff], cy = m[(mi >> 8) & 0xff], dx = m[(mi >> 16) & 0xff], dy = m[mi >> 24];
+    const uint32_t mi = midx[r];
+    mw[4 * r] = m[mi & 0xff];
+    mw[4 * r + 1] = m[(mi >> 8) & 0xff];
+    mw[4 * r + 2] = m[(mi >> 16) & 0xff];
+    mw[4 * r + 3] = m[mi >> 24];
+  }
+#pragma unroll
+  for (int r = 0; r < 7; r++) {
+    const uint32_t cx = mw[4 * r], cy = mw[4 * r + 1], dx = mw[4 * r + 2], dy = mw[4 * r + 3];
     FS_G(a, b, c, d, cx, cy)
     b = qperm<ROT1>(b);
     c = qperm<ROT2>(c);
@@ -275,6 +287,9 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   __shared__ RootNode rn[FS_MAX_CHAL];
   const int tid = threadIdx.x, li = tid & 3, quad = tid >> 2;
   uint32_t* m = qm[quad];
+  uint32_t midx[7];
+#pragma unroll
+  for (int r = 0; r < 7; r++) midx[r] = FS_MIDX[r][li];
 
   // ---- phase 0: the stream template into LDS, the roots filled in
   {
@@ -318,7 +333,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
         for (int w = 0; w < 4; w++) m[4 * li + w] = sw[4 * li + w];
         qsync();
         const uint32_t fl = ((b & 15) == 0 ? FS_CHUNK_START : 0) | ((b & 15) == 15 ? FS_CHUNK_END : 0);
-        b3q(m, li, h0, h1, h2, h3, c, 64, fl);
+        b3q(m, li, midx, h0, h1, h2, h3, c, 64, fl);
         qsync();
         if ((b & 15) == 15) {
           A.ccv[8 * c + li] = h0;
@@ -362,7 +377,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
         break;
       }
       const bool last_in_chunk = o + 64 == cend;
-      b3q(m, li, h0, h1, h2, h3, c, 64, st | (last_in_chunk ? FS_CHUNK_END : 0));
+      b3q(m, li, midx, h0, h1, h2, h3, c, 64, st | (last_in_chunk ? FS_CHUNK_END : 0));
       qsync();
       o += 64;
       if (last_in_chunk) {  // chunk c complete (only chunk J can be: the suffix is < 1 KB)
@@ -389,7 +404,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
     } else {
       // its chaining value (non-root)
       uint32_t n0 = h0, n1 = h1, x2, x3;
-      b3q(m, li, n0, n1, x2, x3, c, blen, flags);
+      b3q(m, li, midx, n0, n1, x2, x3, c, blen, flags);
       qsync();
       // stack of merged subtrees over chunks 0..C-2 (push_chunk_cv)
       uint32_t(*stk)[8] = qstack[quad];
@@ -412,7 +427,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
           m[12 + li] = c1;
           qsync();
           uint32_t p0 = IV8[li], p1 = IV8[4 + li], y2, y3;
-          b3q(m, li, p0, p1, y2, y3, 0, 64, FS_PARENT);
+          b3q(m, li, midx, p0, p1, y2, y3, 0, 64, FS_PARENT);
           qsync();
           c0 = p0;
           c1 = p1;
@@ -432,7 +447,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
         qsync();
         if (i == 0) break;  // the root node: cv = IV, block m, PARENT
         uint32_t p0 = IV8[li], p1 = IV8[4 + li], y2, y3;
-        b3q(m, li, p0, p1, y2, y3, 0, 64, FS_PARENT);
+        b3q(m, li, midx, p0, p1, y2, y3, 0, 64, FS_PARENT);
         qsync();
         n0 = p0;
         n1 = p1;
@@ -460,7 +475,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
         for (int w = 0; w < 4; w++) m[4 * li + w] = R.block[4 * li + w];
         qsync();
         uint32_t h0 = R.cv[li], h1 = R.cv[4 + li], h2, h3;
-        b3q(m, li, h0, h1, h2, h3, t, R.blen, R.flags | FS_ROOT);
+        b3q(m, li, midx, h0, h1, h2, h3, t, R.blen, R.flags | FS_ROOT);
         qsync();
         const uint32_t words[4] = {h0, h1, h2, h3};
 #pragma unroll

@@ -6,4 +6,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 echo tests ok
 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/solo8 -o run -- python3 tools/solo_trace.py 8 0 21 > $O/solo8.log 2>&1 || exit 1
 timeout -k 10 400 python3 bench.py --no-cpu-baseline --no-worst-case --no-host-rows > $O/bench.log 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+SEZKP_DEVICE_TRANSCRIPT=1 timeout -k 10 200 python3 bench.py --inflight 1 --steps 10 --no-cpu-baseline --no-configs --no-worst-case --no-host-rows --no-sharded --dntt-log-n 0 > $O/bench_devtr.log 2> $O/bench_devtr.err || { tail -5 $O/bench_devtr.err; exit 1; }
 echo done
