@@ -983,7 +983,11 @@ void sezkp_ctx::take_staged() {
     T.blk_winlen = t.bw;
     T.blk_offin = t.bi;
     T.blk_offout = t.bo;
-    HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
+    // A/B (round 4): a device-side wait on a copy still in flight holds the
+    // hardware queue this stream shares with other contexts' streams
+    static const bool host_wait = getenv("SEZKP_STAGE_HOST_WAIT") != nullptr;
+    if (host_wait) HIP_OR_THROW(hipEventSynchronize(t.ready));
+    else HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
   }
 }
 
