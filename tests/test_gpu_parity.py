@@ -331,11 +331,12 @@ def test_prove_full_size_config3(gpu_ok, product, oracle):
     assert view.readonly and bytes(view) == art.proof_bytes
 
 
-def test_prove_headline_size_matches_openmp_oracle(gpu_ok, product):
+def test_prove_headline_size_matches_openmp_oracle(gpu_ok, product, monkeypatch):
     """The bench workload itself: `sezkp-cli simulate --t 2097152 --b 512
     --tau 8` blocks (T = 2^21, N = 2^24). The GPU proof equals the OpenMP build
-    of the C oracle byte for byte; the oracle runs in a child process on 16
-    threads (~10 s), so the other tests keep the single-thread build."""
+    of the C oracle byte for byte, with the host transcript (default) and with
+    the device transcript; the oracle runs in a child process on 16 threads
+    (~10 s), so the other tests keep the single-thread build."""
     import sys
     T = 1 << 21
     code = ("import sys; sys.path[:0]=[%r,%r]\n"
@@ -348,10 +349,12 @@ def test_prove_headline_size_matches_openmp_oracle(gpu_ok, product):
     ctx = product.ProverContext(0)
     ctx.upload(blocks)
     got = hashlib.sha256(ctx.prove(blocks.manifest_root()).proof_bytes).hexdigest()
+    monkeypatch.setenv("SEZKP_DEVICE_TRANSCRIPT", "1")
+    got_dev = hashlib.sha256(ctx.prove(blocks.manifest_root()).proof_bytes).hexdigest()
     ctx.close()
     out, err = child.communicate(timeout=150)
     assert child.returncode == 0, err[-1500:]
-    assert got == out.strip()
+    assert got == out.strip() and got_dev == got
 
 
 def test_prove_config5_size_one_gpu_matches_openmp_oracle(gpu_ok, product):
