@@ -296,9 +296,8 @@ __device__ __forceinline__ void subtree_regs(const uint64_t (&v)[16], uint64_t i
 // computes the layer from the previous one first (y'_i = in[i] + beta*in[i+len])
 // and writes it to out. Levels above `stop` are left to the upper-level jobs.
 // LPL = 4 (4096-leaf WGs) for large trees; LPL = 2 (1024 leaves) when a
-// launch has too few 4096-leaf WGs to fill the chip (small shards and
-// traces): a WG's 31 dependent compressions per lane then ran at one or two
-// waves per SIMD.
+// launch has 512 or fewer 4096-leaf WGs (small shards and traces): a WG's 31
+// dependent compressions per lane then ran at one or two waves per SIMD.
 template <int LPL>
 __device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int logLen,
                                            int fold, uint64_t beta, const TreeDev& T, uint64_t wg,

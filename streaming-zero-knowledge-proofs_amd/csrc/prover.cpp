@@ -251,7 +251,10 @@ struct sezkp_ctx {
   // allgathered, else 6 so the upper jobs build levels 7.. with every lane busy
   int tree_stop() const { return sharded() ? L16_LOG : LSTORE_FRI; }
   // leaves per WG of the layer-0 tree and the forest: 4096, or 1024 when the
-  // local LDE has at most 2^22 points (too few 4096-leaf WGs to fill the chip)
+  // local LDE has at most 2^21 points (512 or fewer 4096-leaf WGs). Measured
+  // (round 4, tools/r4i.sh): config 3 (N = 2^21) in flight 0.499 -> 0.479 ms per
+  // proof, a P = 8 rank's trees even; at 2^22 points (a P = 4 rank) the
+  // 4096-leaf WGs were faster (layer-0 tree 0.186 against 0.208 ms)
   int tree_wg_log = L16_LOG;
   int wg_stop() const { return std::min(tree_stop(), tree_wg_log); }
   uint64_t M = 0;                       // local LDE length N / P
@@ -715,7 +718,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   }
   M = N >> logP;
   logM = logN - logP;
-  tree_wg_log = M <= (1ULL << 22) ? L16S_LOG : L16_LOG;
+  tree_wg_log = M <= (1ULL << 21) ? L16S_LOG : L16_LOG;
   rR = sharded() ? k - L16_LOG - logP : (k >= L16_LOG ? k - L16_LOG : -1);
   d_lde = dalloc<uint64_t>(M);
   if (sharded()) {
@@ -983,11 +986,11 @@ void sezkp_ctx::take_staged() {
     T.blk_winlen = t.bw;
     T.blk_offin = t.bi;
     T.blk_offout = t.bo;
-    // A/B (round 4): a device-side wait on a copy still in flight holds the
-    // hardware queue this stream shares with other contexts' streams
-    static const bool host_wait = getenv("SEZKP_STAGE_HOST_WAIT") != nullptr;
-    if (host_wait) HIP_OR_THROW(hipEventSynchronize(t.ready));
-    else HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
+    // (a host-side wait here instead, so no device-side wait on a copy in
+    // flight holds a hardware queue other contexts' streams share, measured
+    // within noise in round 4: host -> proof 7.90 / 7.98 10^9, mean of two
+    // alternating runs each, profiles/r04/stage_wait_ab.txt)
+    HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
   }
 }
 
