@@ -1748,6 +1748,15 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   mark("sync4");
   if (htrace) {
     for (auto& m : hmarks) fprintf(stderr, "%s %.1f ", m.first, m.second);
+    if (!host_tr) {  // device transcript: us per kernel phase (fill, chain, tails, xof, derive) of each point
+      uint64_t t[3][6];
+      HIP_OR_THROW(hipMemcpy(t, d_chal->fs_t, sizeof t, hipMemcpyDeviceToHost));
+      for (int p = 0; p < 3; p++) {
+        fprintf(stderr, "fs%d", p + 1);
+        for (int i = 1; i < 6; i++) fprintf(stderr, " %.1f", (double)(t[p][i] - t[p][i - 1]) / 100.0);
+        fprintf(stderr, " ");
+      }
+    }
     fprintf(stderr, "\n");
   }
   for (int s = 0; s < ST_NSTAGE; s++) {

@@ -243,6 +243,7 @@ struct DevChal {
   uint64_t rows[FS_NQ], frows[FS_NQ];    // derive_queries mod n / mod N (prover.rs:248, 297)
   uint32_t counts[2];               // FRI path / opening requests this rank owns
   uint32_t pad[2];
+  uint64_t fs_t[3][6];              // device transcript: s_memrealtime at each kernel phase (SEZKP_HOST_TRACE prints)
 };
 
 // Device transcript (transcript.hip): the stream S (template from the host,

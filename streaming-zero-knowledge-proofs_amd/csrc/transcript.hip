@@ -290,6 +290,12 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   uint32_t midx[7];
 #pragma unroll
   for (int r = 0; r < 7; r++) midx[r] = FS_MIDX[r][li];
+  // phase timestamps (100 MHz realtime clock) for SEZKP_HOST_TRACE
+  uint64_t* tmark = (A.point >= 1 && A.point <= 3) ? A.ch->fs_t[A.point - 1] : nullptr;
+  auto stamp = [&](int i) {
+    if (tmark && tid == 0) tmark[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   // ---- phase 0: the stream template into LDS, the roots filled in
   {
@@ -309,6 +315,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
     S[f.s_off + byte] = (uint8_t)(w >> (8 * (byte & 3)));
   }
   __syncthreads();
+  stamp(1);
 
   // ---- phase 1: chaining values of blocks [B0, B1), one chunk per quad
   if (A.B1 > A.B0) {
@@ -348,6 +355,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   }
   __syncthreads();
 
+  stamp(2);
   // ---- phase 2: per challenge, the root node of S[0..pos) || suffix
   if (quad < (int)A.nchal) {
     const FsChal ch = A.chal[quad];
@@ -462,6 +470,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   }
   __syncthreads();
 
+  stamp(3);
   // ---- phase 3: XOF output blocks, one quad per (challenge, block)
   {
     uint32_t item = 0;
@@ -489,6 +498,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   }
   __syncthreads();
 
+  stamp(4);
   // ---- phase 4: derived values
   DevChal* D = A.ch;
   if (A.point == 1) {
@@ -512,6 +522,8 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   } else if (A.point == 3) {
     fs_queries(A, D, tid);
   }
+  __syncthreads();
+  stamp(5);
 }
 
 // DEEP-polynomial constants from z (DeepPoly, sezkp_internal.h): z^n, K1 =
