@@ -193,11 +193,7 @@ __device__ __forceinline__ uint32_t wg_scan(uint32_t v, uint32_t* sm, uint32_t& 
 __device__ void fs_queries(const FsArgs& A, DevChal* D, int tid) {
   __shared__ uint64_t s_row[FS_NQ], s_pos[FS_NQ];
   __shared__ uint32_t s_sum[FS_THREADS / 64];
-  constexpr uint32_t DICT_LDS = 512;
-  __shared__ uint32_t s_dict[DICT_LDS];  // column -> dictionary index (the first 512 columns)
   const FsQueryArgs& Q = A.q;
-  const uint32_t ncols = 3 + 7 * Q.tau;
-  for (uint32_t c = tid; c < ncols && c < DICT_LDS; c += FS_THREADS) s_dict[c] = Q.dict_of[c];
   const uint64_t n = 1ULL << A.logn, N = 1ULL << A.logN;
   const int k = A.logN;
   if (tid < FS_NQ) {
@@ -255,7 +251,7 @@ __device__ void fs_queries(const FsArgs& A, DevChal* D, int tid) {
     rq[1] = (uint32_t)row;
     rq[2] = (uint32_t)(row >> 32);
     rq[3] = j;
-    rq[4] = c < DICT_LDS ? s_dict[c] : Q.dict_of[c];
+    rq[4] = Q.dict_of[c];
   }
   if (tid == 0) D->counts[1] = total;
   if (Q.rank != 0) return;  // sharded: one writer per byte (the image is byte-summed)
@@ -289,8 +285,6 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   __shared__ uint32_t qm[FS_QUADS][16];
   __shared__ uint32_t qstack[FS_MAX_CHAL][10][8];
   __shared__ RootNode rn[FS_MAX_CHAL];
-  __shared__ FsChal s_chal[FS_MAX_CHAL];
-  __shared__ uint32_t s_ccv[FS_S_MAX / 1024 + 2][8];  // chunk chaining values
   const int tid = threadIdx.x, li = tid & 3, quad = tid >> 2;
   uint32_t* m = qm[quad];
   uint32_t midx[7];
@@ -303,49 +297,22 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   };
   stamp(0);
 
-  // ---- phase 0: the stream template into LDS, the roots filled in. Every
-  // global read of the phase is issued before the first wait: the fill
-  // bytes (descriptor -> root word) into registers, the template, the
-  // challenge table and the chunk CVs of earlier points; one latency, not
-  // a chain of them
+  // ---- phase 0: the stream template into LDS, the roots filled in
   {
-    constexpr int FMAX = 16;  // fill bytes per thread held in registers (60 roots: 8)
-    const uint32_t nfb = A.nfill * 32;
-    uint32_t fo[FMAX], fv[FMAX];
-#pragma unroll
-    for (int k = 0; k < FMAX; k++) {
-      const uint32_t i = tid + (uint32_t)k * FS_THREADS;
-      fo[k] = ~0u;
-      if (i < nfb) {
-        const FsFill f = A.fills[i >> 5];
-        const uint32_t byte = i & 31;
-        uint32_t w;
-        if (f.src == FS_SRC_MROOT) w = A.mroot[byte >> 2];
-        else if (f.src < FS_SRC_FRI) w = A.colroots[8 * (f.src - FS_SRC_COL) + (byte >> 2)];
-        else w = A.friroots[8 * (f.src - FS_SRC_FRI) + (byte >> 2)];
-        fo[k] = f.s_off + byte;
-        fv[k] = (w >> (8 * (byte & 3))) & 0xff;
-      }
-    }
     const uint32_t nw = (A.s_bytes + 15) / 16;
     const uint4* src = reinterpret_cast<const uint4*>(A.S);
     uint4* dst = reinterpret_cast<uint4*>(S);
     for (uint32_t i = tid; i < nw; i += FS_THREADS) dst[i] = src[i];
-    if (tid < (int)A.nchal) s_chal[tid] = A.chal[tid];
-    for (uint32_t i = tid; i < 8 * (A.B0 >> 4); i += FS_THREADS) s_ccv[i >> 3][i & 7] = A.ccv[i];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FMAX; k++)
-      if (fo[k] != ~0u) S[fo[k]] = (uint8_t)fv[k];
-    for (uint32_t i = tid + FMAX * FS_THREADS; i < nfb; i += FS_THREADS) {  // more than FMAX per thread
-      const FsFill f = A.fills[i >> 5];
-      const uint32_t byte = i & 31;
-      uint32_t w;
-      if (f.src == FS_SRC_MROOT) w = A.mroot[byte >> 2];
-      else if (f.src < FS_SRC_FRI) w = A.colroots[8 * (f.src - FS_SRC_COL) + (byte >> 2)];
-      else w = A.friroots[8 * (f.src - FS_SRC_FRI) + (byte >> 2)];
-      S[f.s_off + byte] = (uint8_t)(w >> (8 * (byte & 3)));
-    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < A.nfill * 32; i += FS_THREADS) {
+    const FsFill f = A.fills[i >> 5];
+    const uint32_t byte = i & 31;
+    uint32_t w;
+    if (f.src == FS_SRC_MROOT) w = A.mroot[byte >> 2];
+    else if (f.src < FS_SRC_FRI) w = A.colroots[8 * (f.src - FS_SRC_COL) + (byte >> 2)];
+    else w = A.friroots[8 * (f.src - FS_SRC_FRI) + (byte >> 2)];
+    S[f.s_off + byte] = (uint8_t)(w >> (8 * (byte & 3)));
   }
   __syncthreads();
   stamp(1);
@@ -378,8 +345,6 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
         if ((b & 15) == 15) {
           A.ccv[8 * c + li] = h0;
           A.ccv[8 * c + 4 + li] = h1;
-          s_ccv[c][li] = h0;
-          s_ccv[c][4 + li] = h1;
         }
       }
       if (b1 & 15) {  // the state in front of the next (not yet known) block
@@ -393,7 +358,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   stamp(2);
   // ---- phase 2: per challenge, the root node of S[0..pos) || suffix
   if (quad < (int)A.nchal) {
-    const FsChal ch = s_chal[quad];
+    const FsChal ch = A.chal[quad];
     const uint32_t L = ch.pos + ch.sfx_len;
     const uint32_t J = ch.pos >> 10, bi = (ch.pos >> 6) & 15;
     const uint32_t IV8[8] = {B3_IV0, B3_IV1, B3_IV2, B3_IV3, B3_IV4, B3_IV5, B3_IV6, B3_IV7};
@@ -455,8 +420,8 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
       for (uint32_t j = 0; j + 1 < C; j++) {
         uint32_t c0, c1;
         if (j < J || !crossed) {
-          c0 = s_ccv[j][li];
-          c1 = s_ccv[j][4 + li];
+          c0 = A.ccv[8 * j + li];
+          c1 = A.ccv[8 * j + 4 + li];
         } else {
           c0 = tail_cv0;
           c1 = tail_cv1;
@@ -510,7 +475,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
   {
     uint32_t item = 0;
     for (uint32_t i = 0; i < A.nchal; i++) {
-      const FsChal ch = s_chal[i];
+      const FsChal ch = A.chal[i];
       const uint32_t nb = (ch.out_len + 63) / 64;
       for (uint32_t t = 0; t < nb; t++, item++) {
         if ((int)(item % FS_QUADS) != quad) continue;
