@@ -178,6 +178,7 @@ struct sezkp_ctx {
     uint8_t* raw = nullptr;     // step arrays as the view holds them (row-major), before k_trace_image
     uint64_t* h_tab = nullptr;  // pinned staging of bw | bi | bo
     hipEvent_t ready = nullptr;
+    bool image_pending = false;  // staged: raw copied (copy stream), k_trace_image not yet run
   };
   TraceSlot slot[2];
   int active = 0;
@@ -466,7 +467,10 @@ struct sezkp_ctx {
   void stage(const sezkp_block_view& v);
   void alloc_slot(TraceSlot& t);
   // block tables + step arrays of `v` into slot t, async on stream s
-  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, uint64_t row0, uint64_t nrows);
+  void write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, uint64_t row0, uint64_t nrows,
+                   bool staged_copy = false);
+  void launch_image(TraceSlot& t, hipStream_t s, uint64_t row0, uint64_t nrows);
+  void wait_copy_stream();
   void check_shape_same(const sezkp_block_view& v) const;
   void take_staged();
   // proves into the pinned staging buffer; returns its size (bytes at h_proof)
@@ -900,13 +904,40 @@ void sezkp_ctx::alloc_slot(TraceSlot& t) {
   if (!t.ready) HIP_OR_THROW(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
 }
 
+// The copy stream holds only SDMA copies: no kernel and no event marker, so
+// no packet waiting on a copy in flight sits in a hardware queue that other
+// contexts' streams share (9 streams on the device's 4 queues at 3 contexts).
+// Its copies finish long before the next proof of the context starts; this
+// host-side poll is the completion check.
+void sezkp_ctx::wait_copy_stream() {
+  if (!stc) return;
+  for (;;) {
+    const hipError_t q = hipStreamQuery(stc);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) HIP_OR_THROW(q);
+    std::this_thread::yield();
+  }
+}
+
+// the row-major step arrays in t.raw -> the tape-major image, on `s`
+void sezkp_ctx::launch_image(TraceSlot& t, hipStream_t s, uint64_t row0, uint64_t nrows) {
+  const size_t cells = (size_t)tau * n;
+  HIP_OR_THROW(launch_trace_image(s, reinterpret_cast<int8_t*>(t.raw + 2 * cells), t.raw + 3 * cells,
+                                  reinterpret_cast<uint16_t*>(t.raw), n, tau, t.mv, t.wf, t.ws, row0, row0 + nrows));
+  HIP_OR_THROW(hipEventRecord(t.ready, s));
+  t.image_pending = false;
+}
+
 // Per-block tables on the host (window lengths, head offsets: tau * n_blocks
 // values), then every array over PCIe asynchronously on `s` and the row-major
-// step arrays transposed to the tape-major image on the device.
-void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, uint64_t row0, uint64_t nrows) {
+// step arrays transposed to the tape-major image on the device (staged_copy:
+// the transposition is left to take_staged(), on the prover stream).
+void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t s, uint64_t row0, uint64_t nrows,
+                            bool staged_copy) {
   const size_t cells = (size_t)tau * n, nt = (size_t)tau * nblk;
-  // the previous copy out of h_tab (an earlier stage into this slot, and its
-  // transposition of `raw` on the same stream) must be done
+  // the previous copy out of h_tab (an earlier stage into this slot) and the
+  // transposition of `raw` must be done
+  wait_copy_stream();
   HIP_OR_THROW(hipEventSynchronize(t.ready));
   for (uint32_t k = 0; k < nblk; k++)
     for (uint32_t r = 0; r < tau; r++) {
@@ -933,14 +964,13 @@ void sezkp_ctx::write_trace(TraceSlot& t, const sezkp_block_view& v, hipStream_t
   int8_t* raw_mv = reinterpret_cast<int8_t*>(t.raw + 2 * cells);
   uint8_t* raw_hw = t.raw + 3 * cells;
   const size_t c0 = (size_t)row0 * tau, nc = (size_t)nrows * tau;
-  (void)cells;
   cp(raw_ws + c0, v.wsym, nc * 2);
   cp(raw_mv + c0, v.mv, nc);
   cp(raw_hw + c0, v.has_write, nc);
   cp(t.imv + row0, v.input_mv, nrows);
   cp(t.bw, t.h_tab, 3 * nt * 8);
-  HIP_OR_THROW(launch_trace_image(s, raw_mv, raw_hw, raw_ws, n, tau, t.mv, t.wf, t.ws, row0, row0 + nrows));
-  HIP_OR_THROW(hipEventRecord(t.ready, s));
+  if (staged_copy) t.image_pending = true;
+  else launch_image(t, s, row0, nrows);
 }
 
 void sezkp_ctx::check_shape_same(const sezkp_block_view& v) const {
@@ -965,7 +995,7 @@ void sezkp_ctx::stage(const sezkp_block_view& v) {
   TraceSlot& t = slot[1 - active];
   if (!t.imv) alloc_slot(t);  // first stage on this workspace: the spare image
   staged = false;             // (re)filling the spare slot
-  write_trace(t, v, stc, 0, n);
+  write_trace(t, v, stc, 0, n, true);
   staged = true;
 }
 
@@ -986,11 +1016,15 @@ void sezkp_ctx::take_staged() {
     T.blk_winlen = t.bw;
     T.blk_offin = t.bi;
     T.blk_offout = t.bo;
-    // (a host-side wait here instead, so no device-side wait on a copy in
-    // flight holds a hardware queue other contexts' streams share, measured
-    // within noise in round 4: host -> proof 7.90 / 7.98 10^9, mean of two
-    // alternating runs each, profiles/r04/stage_wait_ab.txt)
-    HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
+    // the copies are done (host-side check, nothing queued on the copy
+    // stream's hardware queue), then the transposition runs on the prover
+    // stream ahead of this proof's kernels
+    if (t.image_pending) {
+      wait_copy_stream();
+      launch_image(t, st, 0, n);
+    } else {
+      HIP_OR_THROW(hipStreamWaitEvent(st, t.ready, 0));
+    }
   }
 }
 
