@@ -81,9 +81,15 @@ def load_profile(kernel: str) -> dict:
     (tools/profile_round.sh -> profiles/pmc_summary.json)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
-        return json.load(open(p)).get(kernel, {})
+        allp = json.load(open(p))
     except Exception:
         return {}
+    if kernel in allp:
+        return allp[kernel]
+    # keyed per template instance (k_forest16<4>, k_forest16<2>): the instance
+    # with the most instructions per launch is the one the headline shape runs
+    inst = [v for k, v in allp.items() if k.split("<")[0] == kernel]
+    return max(inst, key=lambda v: v.get("valu_instr_per_launch") or 0) if inst else {}
 
 
 def host_info() -> dict:
