@@ -540,13 +540,15 @@ def main():
     for _ in range(nsp):
         proof = ctx.prove_view(roots[holds[0]])
         for k, v in ctx.stage_times_ms().items():
-            stage_sum[k] = stage_sum.get(k, 0.0) + v
+            if k.startswith("host_"):
+                stage_sum[k] = stage_sum.get(k, 0.0) + v
     barrier()
     dt1 = time.perf_counter() - t1
     single_ms = dt1 / nsp * 1e3
-    # the same proofs again with event pairs around single launches (the
-    # forest, the transcript points): live per-kernel times for the roofline,
-    # kept out of the latency figure above
+    # the same proofs again with timed events around every stage and around
+    # single launches (the forest, the transcript points): the device stage
+    # split and the live per-kernel times of the rooflines, kept out of the
+    # latency figure above (the events lengthen a proof by ~45 us)
     os.environ["SEZKP_KERNEL_EVENTS"] = "1"
     ksum = {}
     for _ in range(nsp):
@@ -554,6 +556,8 @@ def main():
         for k, v in ctx.stage_times_ms().items():
             if k.startswith(("k_", "fs_")) or k == "layer0_tree":
                 ksum[k] = ksum.get(k, 0.0) + v
+            if not k.startswith(("host_", "k_", "fs_")):
+                stage_sum[k] = stage_sum.get(k, 0.0) + v
     os.environ.pop("SEZKP_KERNEL_EVENTS", None)
     kern_ms = {k: v / nsp for k, v in ksum.items()}
     proof_len = len(proof)
@@ -833,7 +837,7 @@ def roofline_ntt(args, torch, stages, N, T):
     pass (the first pass reads only the n coefficients); traffic and VALU
     instructions per proof from the per-template PMC summary (the first pass is
     the NARROW instance, the others the wide one)."""
-    t_lde = stages.get("lde_ntt", float("nan")) * 1e-3
+    t_lde = (stages.get("lde_ntt") or float("nan")) * 1e-3  # nan, not 0, when the stage was not timed
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     allp = json.load(open(p)) if os.path.exists(p) else {}
     from sezkp_amd._lib import lib
@@ -1128,9 +1132,15 @@ def measure_sharded_predicted(args, torch, single_ms: float) -> dict:
                 t0 = time.perf_counter()
                 ctx.prove_view(mroot)
                 wall.append((time.perf_counter() - t0) * 1e3)
-                for k, v in ctx.stage_times_ms().items():
-                    st_sum[k] = st_sum.get(k, 0.0) + v / reps
             stats = ctx.comm_stats()
+            # the stage split from two more proofs with timed stage events
+            # (kept out of the wall times: the events lengthen a proof)
+            os.environ["SEZKP_STAGE_EVENTS"] = "1"
+            for _ in range(2):
+                ctx.prove_view(mroot)
+                for k, v in ctx.stage_times_ms().items():
+                    st_sum[k] = st_sum.get(k, 0.0) + v / 2
+            os.environ.pop("SEZKP_STAGE_EVENTS", None)
             for c in stats:
                 coll_ms += c["ms"]
                 wire += c["bytes"]
@@ -1176,14 +1186,21 @@ def measure_sharded(args, world, rank, local, dist, torch):
     coll_sum = {}
     for _ in range(args.sharded_steps):
         view = ctx.prove_view(mroot)
-        for k, v in ctx.stage_times_ms().items():
-            stage_sum[k] = stage_sum.get(k, 0.0) + v
         for c in ctx.comm_stats():
             a = coll_sum.setdefault(c["name"], {"bytes": c["bytes"], "ms": 0.0})
             a["ms"] += c["ms"]
     dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # rank 0's stage split from a few more proofs with timed stage events (every
+    # rank runs them: the proof is collective), outside the timed window
+    n_st = min(3, args.sharded_steps)
+    os.environ["SEZKP_STAGE_EVENTS"] = "1"
+    for _ in range(n_st):
+        ctx.prove_view(mroot)
+        for k, v in ctx.stage_times_ms().items():
+            stage_sum[k] = stage_sum.get(k, 0.0) + v
+    os.environ.pop("SEZKP_STAGE_EVENTS", None)
     t = torch.tensor([dt], dtype=torch.float64, device=RED_DEV)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
@@ -1202,7 +1219,7 @@ def measure_sharded(args, world, rank, local, dist, torch):
                                      f"all-to-all, allgathered Merkle caps, byte-sum proof assembly"
                                      + (" (REHEARSAL: all ranks on GPU 0)" if REHEARSE else "")},
            "ranks_agree": len(set(ds)) == 1, "matches_single_gpu_proof": ds[0] == single, "proof_bytes": plen,
-           "stages_ms_rank0": {k: v / args.sharded_steps for k, v in stage_sum.items()},
+           "stages_ms_rank0": {k: v / n_st for k, v in stage_sum.items()},
            "collectives_rank0": {k: {"bytes_sent": v["bytes"], "ms": v["ms"] / args.sharded_steps,
                                      "GBs": v["bytes"] / (v["ms"] / args.sharded_steps) / 1e6 if v["ms"] > 0 else None}
                                  for k, v in coll_sum.items()},

@@ -131,9 +131,11 @@ int32_t sezkp_host_unregister(void* p);
 int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags,
                                const uint8_t** data, size_t* len, char* err, size_t err_len);
 /* Per-stage device times (ms) of the last prove, measured with HIP events on
- * the context's stream. Order: expand, col_commit, col_outer, compose, intt,
- * lde_ntt, deep, layer0_tree, layer0_upper, fri_fold_trees, col_openings,
- * fri_paths, total, then host wall / sync-wait / final-wait / serialize,
+ * the context's stream when SEZKP_STAGE_EVENTS=1 (or SEZKP_KERNEL_EVENTS=1) is
+ * set, else 0 (timed events lengthen a proof). Order: expand, col_commit,
+ * col_outer, compose, intt, lde_ntt, deep, layer0_tree, layer0_upper,
+ * fri_fold_trees, col_openings, fri_paths, total, then host wall / sync-wait /
+ * final-wait / serialize (always measured),
  * then single launches timed only when SEZKP_KERNEL_EVENTS=1 is set (else 0):
  * the FRI forest (k_forest16) and the three device transcript points.
  * Returns the number of values written. */

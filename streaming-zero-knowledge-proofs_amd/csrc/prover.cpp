@@ -1263,9 +1263,18 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   };
   HIP_OR_THROW(hipSetDevice(device));
   const int k = logN;
-  auto rec = [&](int s) { HIP_OR_THROW(hipEventRecord(ev[s], st)); };
   const char* kev_env = getenv("SEZKP_KERNEL_EVENTS");
   const bool kprobe = kev_env && atoi(kev_env) != 0;
+  // Per-stage timed events only on request (SEZKP_STAGE_EVENTS=1, or with the
+  // kernel events): each timed event record costs the stream ~3.5 us, so the
+  // 13 of a proof added ~45 us to one proof at a time (round 4,
+  // profiles/r04/stage_events_ab.txt); without them the device stage times
+  // read 0
+  const char* sev_env = getenv("SEZKP_STAGE_EVENTS");
+  const bool stage_ev = kprobe || (sev_env && atoi(sev_env) != 0);
+  auto rec = [&](int s) {
+    if (stage_ev) HIP_OR_THROW(hipEventRecord(ev[s], st));
+  };
   bool kdone[4] = {false, false, false, false};
   auto krec = [&](int i, bool end) {
     if (!kprobe) return;
@@ -1793,13 +1802,16 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     }
     fprintf(stderr, "\n");
   }
-  for (int s = 0; s < ST_NSTAGE; s++) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, ev[s], ev[s + 1]) == hipSuccess) stage_ms[s] = ms;
+  for (int s = 0; s <= ST_NSTAGE; s++) stage_ms[s] = 0;
+  if (stage_ev) {
+    for (int s = 0; s < ST_NSTAGE; s++) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, ev[s], ev[s + 1]) == hipSuccess) stage_ms[s] = ms;
+    }
+    float tot = 0;
+    (void)hipEventElapsedTime(&tot, ev[0], ev[ST_NSTAGE]);
+    stage_ms[ST_NSTAGE] = tot;
   }
-  float tot = 0;
-  (void)hipEventElapsedTime(&tot, ev[0], ev[ST_NSTAGE]);
-  stage_ms[ST_NSTAGE] = tot;
   for (int i = 0; i < 4; i++) {
     float ms = 0;
     kernel_ms[i] = kdone[i] && hipEventElapsedTime(&ms, kev[2 * i], kev[2 * i + 1]) == hipSuccess ? ms : 0.0;

@@ -14,6 +14,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "streaming-zero-knowledge-proofs_amd")
 ORACLE = os.path.join(ROOT, "oracle")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def free_port() -> int:
+    """A TCP port for a multi-process test's rendezvous, drawn outside Linux's
+    ephemeral range (32768-60999): a port found by binding port 0 comes from
+    that range and can go to another connection (an earlier test's gloo pairs)
+    before the store listens on it (EADDRINUSE, seen once on the GPU box)."""
+    import random
+    import socket
+    rng = random.SystemRandom()
+    for _ in range(500):
+        p = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+        except OSError:
+            continue
+        finally:
+            s.close()
+        return p
+    raise RuntimeError("no free TCP port in 20000-32000")
 for p in (PKG, ORACLE):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -7,23 +7,18 @@ transport differs from RCCL. Layouts (sezkp_stark.h): rank g's input is
 x[g + P j]; its output is X[g Q + q + M k1] at k1 Q + q (M = n/P, Q = M/P).
 """
 import os
-import socket
 import sys
 
 import numpy as np
 import pytest
 
-from conftest import ORACLE, PKG
+from conftest import ORACLE, PKG, free_port
 
 pytestmark = pytest.mark.gpu
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 def expected_local(X: np.ndarray, rank: int, world: int) -> np.ndarray:

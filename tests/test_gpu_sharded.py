@@ -7,22 +7,17 @@ oracle's proof bytes.
 """
 import hashlib
 import os
-import socket
 import sys
 
 import pytest
 
-from conftest import ORACLE, PKG
+from conftest import ORACLE, PKG, free_port
 
 pytestmark = pytest.mark.gpu
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 def _worker(rank, world, port, T, b, tau, seed, q):
@@ -454,17 +449,13 @@ def test_sharded_sliced_upload_matches_full(gpu_ok, product, oracle, tmp_path, w
     cross every rank boundary. Every rank's proof equals the oracle's proof of
     the whole trace (bound to the file's Frontier root), and no rank holds
     the whole trace (row slices of about n / P)."""
-    import socket
     T, b, tau, seed = 1 << 15, 333, 3, 17
     blocks = product.synthetic_blocks(T, b, tau, seed)
     path = tmp_path / "b.jsonl"
     path.write_bytes(blocks.to_jsonl())
     root = blocks.manifest_frontier_root()
     want = hashlib.sha256(oracle.prove_v1(blocks, root)).hexdigest()
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = free_port()
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, free_port
 
 FIX = [("tests/golden/ref_blocks.cbor", "tests/golden/ref_manifest.cbor"),
        ("tests/golden/riscv_blocks.cbor", "tests/golden/riscv_manifest.cbor")]
@@ -108,7 +108,6 @@ def test_sliced_ingest_matches_full_decode(product, tmp_path, world, log_t):
     step slice equals the full decode's rows [row0, row0 + nrows), and the
     root is the file's Frontier root."""
     import hashlib
-    import socket
     import torch.multiprocessing as mp
     import numpy as np
     from sezkp_amd.blocks import shard_rows
@@ -116,10 +115,7 @@ def test_sliced_ingest_matches_full_decode(product, tmp_path, world, log_t):
     path = tmp_path / "b.jsonl"
     path.write_bytes(blocks.to_jsonl())
     full = product.BlockSoA.from_file(str(path))
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_sliced_worker, args=(r, world, port, str(path), q)) for r in range(world)]

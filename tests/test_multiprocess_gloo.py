@@ -2,21 +2,16 @@
 host collectives behind ShardedProverContext(comm="host") and models of the
 sharded layouts and of the four-step distributed NTT."""
 import os
-import socket
 import sys
 
 import pytest
 import torch.multiprocessing as mp
 
-from conftest import ORACLE, PKG
+from conftest import ORACLE, PKG, free_port
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 # ------------------------------------------------- sharded prover (CPU side)

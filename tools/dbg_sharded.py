@@ -4,6 +4,8 @@ RCCL (--comm rccl; needs P GPUs): every rank's proof must equal the oracle's.
 
     python tools/dbg_sharded.py --world 2 --log-t 13 --tau 2
 """
+import os as _os
+_os.environ.setdefault("SEZKP_STAGE_EVENTS", "1")  # device stage times (timed events)
 import argparse
 import hashlib
 import os

@@ -3,6 +3,8 @@
 per-rank cost model of bench.py's sharded_predicted), T = 2^log_t: stage times
 of a few proofs; run under `rocprofv3 --kernel-trace` for its kernel timeline.
 Usage: tools/solo_trace.py [P] [rank] [log_t]"""
+import os as _os
+_os.environ.setdefault("SEZKP_STAGE_EVENTS", "1")  # device stage times (timed events)
 import json
 import os
 import sys

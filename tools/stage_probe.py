@@ -3,6 +3,8 @@ context, `reps` proofs one at a time, the mean of sezkp_ctx_stage_times per
 stage. Run it twice under an environment switch for an A/B, or under
 `rocprofv3 --kernel-trace --stats` for per-kernel durations:
   python3 tools/stage_probe.py [log_t] [reps]"""
+import os as _os
+_os.environ.setdefault("SEZKP_STAGE_EVENTS", "1")  # device stage times (timed events)
 import json
 import os
 import sys
