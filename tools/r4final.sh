@@ -2,7 +2,7 @@
 # (kernel stats + PMC passes), config-5 sliced ingest at P = 8
 set -uo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r4final3
+O=gpurun_out/r4final4
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo TESTS FAILED; grep -E "FAILED|Error" $O/gpu_tests.log | head -30; exit 1; }
 echo tests ok
