@@ -331,6 +331,27 @@ def test_prove_full_size_config3(gpu_ok, product, oracle):
     assert view.readonly and bytes(view) == art.proof_bytes
 
 
+def test_stage_events_opt_in_same_bytes(gpu_ok, product, oracle, monkeypatch):
+    """Per-stage timed events are recorded only on request
+    (SEZKP_STAGE_EVENTS=1): without them the device stage times read 0 and the
+    host times are still measured; the proof bytes are the same either way."""
+    blocks = product.synthetic_blocks(1 << 12, 100, 3, 21)
+    mroot = blocks.manifest_root()
+    want = oracle.prove_v1(blocks, mroot)
+    ctx = product.ProverContext(0)
+    ctx.upload(blocks)
+    monkeypatch.delenv("SEZKP_STAGE_EVENTS", raising=False)
+    monkeypatch.delenv("SEZKP_KERNEL_EVENTS", raising=False)
+    assert ctx.prove(mroot).proof_bytes == want
+    st = ctx.stage_times_ms()
+    assert st["total"] == 0 and st["lde_ntt"] == 0 and st["host_wall"] > 0
+    monkeypatch.setenv("SEZKP_STAGE_EVENTS", "1")
+    assert ctx.prove(mroot).proof_bytes == want
+    st = ctx.stage_times_ms()
+    assert st["total"] > 0 and st["lde_ntt"] > 0 and st["total"] >= st["lde_ntt"]
+    ctx.close()
+
+
 def test_prove_headline_size_matches_openmp_oracle(gpu_ok, product, monkeypatch):
     """The bench workload itself: `sezkp-cli simulate --t 2097152 --b 512
     --tau 8` blocks (T = 2^21, N = 2^24). The GPU proof equals the OpenMP build
