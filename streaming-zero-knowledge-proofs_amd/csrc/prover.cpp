@@ -1391,12 +1391,15 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   const uint64_t shift_inv = hgl_inv(3);
   uint64_t z = 0, zn = 0;
   if (host_tr) {
-    HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32, hipMemcpyDeviceToHost, st));
-    HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * ncols, sharded ? d_err + 8 : d_err, 4 * nguard, hipMemcpyDeviceToHost, st));
+    // one copy: the column roots and the guard words stored right behind them
+    // (d_err = d_colroots + 8 ncols; sharded, every rank's word at d_err + 8)
+    const size_t gofs = sharded ? 8 : 0;
+    HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32 + 4 * (gofs + nguard), hipMemcpyDeviceToHost,
+                                st));
     sync();
     mark("sync1");
     const uint32_t* colroots_h = h_small;
-    check_guards(h_small + 8 * ncols, nguard);
+    check_guards(h_small + 8 * ncols + gofs, nguard);
     std::vector<uint8_t> colroots((const uint8_t*)colroots_h, (const uint8_t*)colroots_h + (size_t)ncols * 32);
     for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
 
