@@ -110,8 +110,9 @@ int32_t sezkp_ctx_prove(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_
  * block count and block boundaries; the values may all differ). The block
  * tables and step arrays go over PCIe on the context's copy stream into a
  * second (spare) trace image and the call returns at once; the next prove on
- * this context switches to it, its kernels waiting for the copy on the
- * device. Allowed while a proof is in flight on the context (that is the
+ * this context switches to it: that call checks on the host that the copies
+ * are done (they normally are) and transposes the step arrays on its own
+ * stream, so the copy stream never holds a packet that waits on a copy. Allowed while a proof is in flight on the context (that is the
  * point: the upload of proof i+1 overlaps proof i). The view's arrays must
  * stay valid and unchanged until the proof that consumes them has completed
  * (sezkp_ctx_prove / sezkp_ctx_prove_borrow returned, or sezkp_ctx_wait for
