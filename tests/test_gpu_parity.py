@@ -613,6 +613,31 @@ def test_staged_uploads_pipeline_bit_exact(gpu_ok, product, oracle):
         t.unpin()
 
 
+def test_stage_then_prove_at_once_bit_exact(gpu_ok, product, oracle):
+    """The prove call right after a pinned stage() finds the copies still in
+    flight: it waits for them on the host (the copy stream holds only copies)
+    and transposes the step arrays on its own stream. A stage() that replaces
+    a staged trace whose copies are still running waits for them too."""
+    T, b, tau = 1 << 18, 512, 8
+    tr = [product.synthetic_blocks(T, b, tau, s) for s in (61, 62)]
+    for t in tr:
+        t.pin()
+    roots = [t.manifest_root() for t in tr]
+    want = [oracle.prove_v1(t, r) for t, r in zip(tr, roots)]
+    c = product.ProverContext(0)
+    c.upload(tr[0])
+    assert bytes(c.prove_view(roots[0])) == want[0]
+    for i in (1, 0, 1):
+        c.stage(tr[i])
+        assert bytes(c.prove_view(roots[i])) == want[i]
+    c.stage(tr[0])
+    c.stage(tr[1])  # replaces the staged trace 0 while its copies may still run
+    assert bytes(c.prove_view(roots[1])) == want[1]
+    c.close()
+    for t in tr:
+        t.unpin()
+
+
 def test_stage_after_prove_async_feeds_the_next_proof(gpu_ok, product, oracle):
     """prove_async(i) then stage(i + 1) at once: proof i must read trace i even
     when its worker starts late. SEZKP_TEST_WORKER_DELAY_US holds the worker
