@@ -418,6 +418,8 @@ def main():
     ap.add_argument("--dntt-log-n", type=int, default=26,
                     help="distributed four-step NTT sub-measurement size (BASELINE config 4: 2^26); 0 = skip")
     ap.add_argument("--dntt-steps", type=int, default=20)
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="file that receives the full measurement record (the stdout line keeps the summary)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -668,7 +670,7 @@ def main():
         def _bail():
             if rank == 0:
                 out[key] = {"error": f"watchdog: no result within {args.sharded_timeout:.0f} s"}
-                print(json.dumps(out), flush=True)
+                emit(out, args.detail)
             os._exit(3)
         # the other ranks wait longer: rank 0 enters late (it alone runs the
         # configs) and must print the main line before any rank's exit makes
@@ -709,9 +711,111 @@ def main():
             head["sharded_ms_per_proof"] = sh.get("ms_per_proof")
             head["sharded_speedup_vs_1gpu_proof"] = (single_ms / sh["ms_per_proof"]) if sh.get("ms_per_proof") else None
             out = {**head, **{k: v for k, v in out.items() if k not in head}}
-        print(json.dumps(out), flush=True)
+        emit(out, args.detail)
     if dist:
         dist.destroy_process_group()
+
+
+LINE_MAX_BYTES = 8192  # the driver read round 3's 10.3 KB line but not round 4's 25.7 KB one
+
+
+def _pick(d, keys, nd=None):
+    """The subset `keys` of dict `d` (missing keys dropped), floats rounded to
+    `nd` significant digits when given."""
+    if not isinstance(d, dict):
+        return d
+    out = {}
+    for k in keys:
+        if k in d:
+            v = d[k]
+            if nd is not None and isinstance(v, float):
+                v = float(f"{v:.{nd}g}")
+            out[k] = v
+    return out
+
+
+def compact_line(out: dict, detail_path) -> dict:
+    """The stdout line: BASELINE's fields, the dominant kernel's roofline (with
+    its HBM view), the CPU baseline and one-number summaries of every other
+    measurement. Everything else stays in the detail file the line names."""
+    line = _pick(out, ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                       "scaling", "vs_baseline", "dtype", "data", "ms_per_proof", "proofs_consistent", "error",
+                       "sharded_value", "sharded_ms_per_proof", "sharded_speedup_vs_1gpu_proof"))
+    cfg = out.get("config")
+    if isinstance(cfg, dict):
+        line["config"] = _pick(cfg, ("workload", "value_is", "T", "N", "tau", "b", "proof_bytes",
+                                     "proofs_in_flight_per_gpu", "upload_bytes_per_proof", "parallelism"))
+    roof = out.get("roofline")
+    if isinstance(roof, dict):
+        r = _pick(roof, ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "mean_launch_ms",
+                         "frac_mix", "measured_on"), 5)
+        if isinstance(roof.get("hbm"), dict):
+            r["hbm"] = _pick(roof["hbm"], ("alg_bytes_per_launch", "achieved_alg_GBs", "frac_alg",
+                                           "traffic_bytes_per_launch", "frac_traffic"), 5)
+        top = roof.get("committed_stats_top_kernel")
+        if isinstance(top, dict):
+            r["rocprof"] = _pick(top, ("name", "average_ms", "file"), 5)
+        line["roofline"] = r
+    cb = out.get("cpu_baseline")
+    if isinstance(cb, dict):
+        c = _pick(cb, ("value", "unit", "cores", "kind", "seconds", "sample", "gpu_proof_matches_oracle", "error"), 5)
+        if isinstance(cb.get("reference_faithful"), dict):
+            c["reference_faithful"] = _pick(cb["reference_faithful"], ("value", "cores", "seconds", "sample"), 4)
+        line["cpu_baseline"] = c
+    for k in ("trace_resident", "single_proof"):
+        if isinstance(out.get(k), dict):
+            line[k] = _pick(out[k], ("value", "ms_per_proof"), 5)
+    rn = out.get("roofline_ntt")
+    if isinstance(rn, dict):
+        line["roofline_ntt"] = _pick(rn, ("bound", "achieved", "peak", "unit", "frac", "traffic", "ms"), 4)
+    cf = out.get("configs")
+    if isinstance(cf, dict):
+        s = {}
+        for k, keys in (("c2_ntt_2e20", ("ms_fwd_plus_inv", "roundtrip_ok")),
+                        ("ntt_2e24", ("ms_per_transform", "roundtrip_ok")),
+                        ("ntt_2e26", ("ms_per_transform", "roundtrip_ok")),
+                        ("c3_prove_2e18", ("single_proof_ms", "inflight3_ms_per_proof", "matches_oracle")),
+                        ("error", None)):
+            if k in cf:
+                s[k] = cf[k] if keys is None else _pick(cf[k], keys + ("error",), 4)
+        line["configs"] = s
+    dn = out.get("dist_ntt")
+    if isinstance(dn, dict):
+        line["dist_ntt"] = _pick(dn, ("value", "ms_per_transform", "roundtrip_ok", "frac_hbm_alg", "error"), 4)
+    sp = out.get("sharded_predicted")
+    if isinstance(sp, dict):
+        s = {str(P): _pick(v, ("predicted_ms_per_proof", "predicted_speedup"), 4)
+             for P, v in (sp.get("by_gpus") or {}).items()}
+        if "error" in sp:
+            s["error"] = sp["error"]
+        line["sharded_predicted"] = s
+    sh = out.get("sharded")
+    if isinstance(sh, dict):
+        line["sharded"] = _pick(sh, ("value", "ms_per_proof", "ranks_agree", "matches_single_gpu_proof", "error"), 5)
+    wc = out.get("worst_case")
+    if isinstance(wc, dict):
+        line["worst_case"] = {k: _pick(v, ("single_proof_ms", "inflight3_ms_per_proof"), 4) for k, v in wc.items() if isinstance(v, dict)}
+    line["detail"] = detail_path
+    return line
+
+
+def emit(out: dict, detail_path) -> None:
+    """Write the full record to `detail_path`, print the compact line (rank 0)."""
+    try:
+        d = os.path.dirname(detail_path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        with open(detail_path, "w") as f:
+            json.dump(out, f, indent=1)
+    except OSError as e:
+        detail_path = f"not written: {e}"
+    s = json.dumps(compact_line(out, detail_path))
+    if len(s) > LINE_MAX_BYTES:  # never lose the headline to the line length
+        s = json.dumps(_pick(compact_line(out, detail_path),
+                             ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
+                              "cpu_baseline", "error", "detail")))
+    print(s, flush=True)
 
 
 def bind_gpu_local_cpus(torch, dev):

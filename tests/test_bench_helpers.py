@@ -53,3 +53,38 @@ def test_halves():
     h = b.halves([1.0, 2.0, 3.0, 4.0], 0.0)
     assert math.isclose(h["first_half"], 1000.0) and math.isclose(h["second_half"], 1000.0)
     assert b.halves([1.0], 0.0) is None
+
+
+def test_stdout_line_is_bounded_and_parseable():
+    """the driver could not read round 4's 25.7 KB line. The
+    formatter applied to that round's full record must give a json.loads-clean
+    line of at most 8 KB that keeps BASELINE's fields, the roofline and the CPU
+    baseline (the rest goes to the detail file)."""
+    b = _bench()
+    full = json.load(open(os.path.join(ROOT, "profiles", "r04", "final", "bench_default.json")))
+    assert len(json.dumps(full)) > 20000
+    s = json.dumps(b.compact_line(full, "gpurun_out/bench_detail.json"))
+    assert len(s) <= b.LINE_MAX_BYTES
+    line = json.loads(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+              "roofline", "cpu_baseline", "trace_resident", "single_proof", "configs", "dist_ntt",
+              "sharded_predicted", "detail"):
+        assert k in line, k
+    assert line["value"] == full["value"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "hbm"):
+        assert k in line["roofline"], k
+    for k in ("value", "cores", "kind", "sample", "gpu_proof_matches_oracle"):
+        assert k in line["cpu_baseline"], k
+    assert set(line["sharded_predicted"]) == {"2", "4", "8"}
+
+
+def test_emit_writes_detail_and_bounds_line(tmp_path, capsys):
+    b = _bench()
+    full = json.load(open(os.path.join(ROOT, "profiles", "r04", "final", "bench_default.json")))
+    full["sharded"] = {"value": 1.0, "stages_ms_rank0": {"x" * 40 + str(i): 1.0 for i in range(2000)}}
+    det = tmp_path / "d" / "detail.json"
+    b.emit(full, str(det))
+    printed = capsys.readouterr().out.strip().splitlines()
+    assert len(printed) == 1 and len(printed[0]) <= b.LINE_MAX_BYTES
+    assert json.loads(printed[0])["detail"] == str(det)
+    assert json.load(open(det))["sharded"]["value"] == 1.0
