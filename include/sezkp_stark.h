@@ -146,7 +146,12 @@ int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max)
  * flight per context; keep several contexts (one per trace, same device) in
  * flight to overlap one proof's VALU-bound trees with another's memory- and
  * latency-bound stages. Other calls on a context with a proof in flight fail
- * with SEZKP_E_INVALID; destroy waits for it. */
+ * with SEZKP_E_INVALID; destroy waits for it. When a staged trace is
+ * pending, this call (like sezkp_ctx_prove) first waits on the host until that
+ * trace's copies have finished (a hipStreamQuery poll of the copy stream: no
+ * event packet sits in a shared hardware queue) and only then returns; in a
+ * pipeline the copies finish long before, but a prove issued right after a
+ * stage() of a 67 MB trace blocks for the rest of that upload (a few ms). */
 int32_t sezkp_ctx_prove_async(sezkp_ctx* ctx, const uint8_t manifest_root[32], uint32_t flags, char* err,
                               size_t err_len);
 int32_t sezkp_ctx_wait(sezkp_ctx* ctx, const uint8_t** data, size_t* len, char* err, size_t err_len);

@@ -2,11 +2,15 @@
 //   prove  --backend stark --blocks B --manifest M --out P [--stream] [--assume-committed]
 //   verify --backend stark --blocks B --manifest M --proof P [--assume-committed]
 //   commit --blocks B(.cbor|.json|.jsonl|.ndjson) --out M
+//   verify-commit --blocks B --manifest M
+//   export-jsonl --input B(.cbor|.json|.jsonl|.ndjson) --output B.jsonl
 // Semantics follow crates/sezkp-cli/src/main.rs:429-578 (manifest precheck,
 // .json/.cbor block files only for prove/verify, write_proof_auto by extension)
 // and crates/sezkp-merkle/src/lib.rs:259-337 (commit / precheck).
 #include <stdio.h>
 #include <string.h>
+
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <fstream>
@@ -95,7 +99,7 @@ std::string pretty_artifact(const Artifact& a) {
 }
 
 struct Args {
-  std::string cmd, backend = "stark", blocks, manifest, out, proof;
+  std::string cmd, backend = "stark", blocks, manifest, out, proof, input;
   bool stream = false, assume = false;
   std::string t = "32", b = "4", tau = "2";  // simulate defaults (main.rs:87-100)
 };
@@ -245,6 +249,61 @@ int cmd_commit(const Args& a) {
   return 0;
 }
 
+// `verify-commit` (main.rs:377-398): the precheck of prove/verify on its own
+int cmd_verify_commit(const Args& a) {
+  BlockStore bs;
+  if (precheck(a, bs)) return 1;
+  printf("OK: %s matches manifest %s\n", a.blocks.c_str(), a.manifest.c_str());
+  return 0;
+}
+
+// mkdir -p of the output's parent directory (main.rs:299-307)
+bool ensure_parent_dir(const std::string& path, std::string& err) {
+  const size_t s = path.find_last_of('/');
+  if (s == std::string::npos || s == 0) return true;
+  const std::string dir = path.substr(0, s);
+  for (size_t i = 1; i <= dir.size(); i++) {
+    if (i < dir.size() && dir[i] != '/') continue;
+    const std::string part = dir.substr(0, i);
+    struct stat st;
+    if (stat(part.c_str(), &st) == 0) {
+      if (!S_ISDIR(st.st_mode)) { err = "creating parent directory " + dir + ": not a directory"; return false; }
+    } else if (mkdir(part.c_str(), 0777) != 0) {
+      err = "creating parent directory " + dir;
+      return false;
+    }
+  }
+  return true;
+}
+
+// `export-jsonl` (main.rs:400-424): any blocks file (stream_block_summaries_auto,
+// io.rs:111-139: .jsonl/.ndjson, .json, .cbor) -> one serde_json object per line
+// (the layout of write_block_summaries_jsonl, io_jsonl.rs:93-106)
+int cmd_export_jsonl(const Args& a) {
+  if (a.input.empty() || a.out.empty()) { fprintf(stderr, "Error: export-jsonl needs --input and --output\n"); return 2; }
+  const std::string e = ext_lower(a.input);
+  if (e != "jsonl" && e != "ndjson" && e != "json" && e != "cbor") {
+    fprintf(stderr, "Error: open input stream: %s\n",
+            e.empty() ? "path has no extension (expected .json, .cbor, .jsonl, or .ndjson)"
+                      : ("unsupported blocks extension: " + e + " (supported: .json, .cbor, .jsonl, .ndjson)").c_str());
+    return 1;
+  }
+  std::string err;
+  BlockStore bs;
+  if (!load_blocks_any(a.input, bs, err)) { fprintf(stderr, "Error: open input stream: %s\n", err.c_str()); return 1; }
+  sezkp_buf buf{};
+  const int32_t rc = sezkp_blocks_encode_jsonl(&bs.view, &buf);
+  if (rc != SEZKP_OK) { fprintf(stderr, "Error: serialize block as JSON line (%d)\n", rc); return 1; }
+  std::vector<uint8_t> out(buf.data, buf.data + buf.len);
+  sezkp_buf_free(&buf);
+  if (!ensure_parent_dir(a.out, err) || !write_file(a.out, out, err)) {
+    fprintf(stderr, "Error: %s\n", err.c_str());
+    return 1;
+  }
+  printf("Exported %u blocks \xe2\x86\x92 %s\n", bs.view.n_blocks, a.out.c_str());
+  return 0;
+}
+
 // `simulate` (main.rs:317-350): generate_trace + partition_trace, written as
 // CBOR (.cbor) or NDJSON (.jsonl/.ndjson) by extension
 int cmd_simulate(const Args& a) {
@@ -291,6 +350,8 @@ void usage() {
           "usage: sezkp-cli prove  --backend stark --blocks B --manifest M --out P [--stream] [--assume-committed]\n"
           "       sezkp-cli verify --backend stark --blocks B --manifest M --proof P [--assume-committed]\n"
           "       sezkp-cli commit --blocks B --out M\n"
+          "       sezkp-cli verify-commit --blocks B --manifest M\n"
+          "       sezkp-cli export-jsonl --input B --output B.jsonl\n"
           "       sezkp-cli simulate --t T --b STEPS_PER_BLOCK --tau TAU --out-blocks B(.cbor|.jsonl)\n");
 }
 
@@ -311,7 +372,8 @@ int main(int argc, char** argv) {
     else if (s == "--manifest") val(a.manifest);
     else if (s == "--out" || s == "-o") val(a.out);
     else if (s == "--proof") val(a.proof);
-    else if (s == "--out-blocks") val(a.out);
+    else if (s == "--out-blocks" || s == "--output") val(a.out);
+    else if (s == "--input") val(a.input);
     else if (s == "--t") val(a.t);
     else if (s == "--b") val(a.b);
     else if (s == "--tau") val(a.tau);
@@ -322,6 +384,8 @@ int main(int argc, char** argv) {
   for (auto& c : a.backend) c = (char)tolower((unsigned char)c);
   if (a.cmd == "commit") return cmd_commit(a);
   if (a.cmd == "simulate") return cmd_simulate(a);
+  if (a.cmd == "verify-commit") return cmd_verify_commit(a);
+  if (a.cmd == "export-jsonl") return cmd_export_jsonl(a);
   if (a.backend != "stark") {
     fprintf(stderr, "Error: only --backend stark is implemented by the MI355X build\n");
     return 2;

@@ -80,6 +80,7 @@ class StarkV1:
     def _prove(blocks: BlockSoA, manifest_root: bytes, streaming: bool) -> ProofArtifact:
         if len(manifest_root) != 32:
             raise SezkpError(-1, "manifest_root must be 32 bytes")
+        blocks.check_shape()
         pb, mb = Buf(), Buf()
         err = C.create_string_buffer(1024)
         rc = lib.sezkp_stark_v1_prove(C.byref(blocks.view()), bytes(manifest_root),
@@ -96,6 +97,7 @@ class StarkV1:
             raise SezkpError(-5, "backend kind mismatch: expected STARK")
         if bytes(artifact.manifest_root) != bytes(manifest_root):
             raise SezkpError(-5, "manifest root mismatch")
+        blocks.check_shape()
         err = C.create_string_buffer(1024)
         rc = lib.sezkp_stark_v1_verify(artifact.proof_bytes, len(artifact.proof_bytes), C.byref(blocks.view()),
                                        bytes(manifest_root), err, 1024)
@@ -114,6 +116,7 @@ class ProverContext:
         self.rank, self.world = 0, 1
 
     def upload(self, blocks: BlockSoA) -> None:
+        blocks.check_shape()
         err = C.create_string_buffer(1024)
         check(lib.sezkp_ctx_upload(self._h, C.byref(blocks.view()), err, 1024), err)
         self.tau = blocks.tau
@@ -121,6 +124,11 @@ class ProverContext:
     def upload_rows(self, blocks: BlockSoA, row0: int, nrows: int) -> None:
         """Upload from a view whose step arrays hold only rows [row0, row0 +
         nrows) (a sharded rank's slice, sezkp_ctx_upload_rows)."""
+        if row0 < 0 or nrows < 0:
+            raise SezkpError(-1, "row0 and nrows must be non-negative")
+        blocks.check_shape(nrows)
+        if blocks.step_start[-1] < row0 + nrows:
+            raise SezkpError(-1, "rows [row0, row0 + nrows) exceed the trace")
         err = C.create_string_buffer(1024)
         check(lib.sezkp_ctx_upload_rows(self._h, C.byref(blocks.view()), row0, nrows, err, 1024), err)
         self.tau = blocks.tau
@@ -130,6 +138,7 @@ class ProverContext:
         async H2D into the spare trace image, allowed while a proof is in
         flight; the next prove uses it (sezkp_ctx_stage). `blocks` must stay
         alive and unchanged until that prove has started."""
+        blocks.check_shape()
         err = C.create_string_buffer(1024)
         check(lib.sezkp_ctx_stage(self._h, C.byref(blocks.view()), err, 1024), err)
         self._staged = blocks  # keep the arrays alive

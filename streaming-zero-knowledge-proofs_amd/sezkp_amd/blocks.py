@@ -43,6 +43,25 @@ class BlockSoA:
     def n_rows(self) -> int:
         return int((self.step_hi - self.step_lo + 1).sum()) if self.n_blocks else 0
 
+    def check_shape(self, nrows: int | None = None) -> None:
+        """Raise SezkpError unless the arrays have the sizes the C ABI reads
+        (sezkp_block_view carries no lengths): per-block fields n_blocks,
+        per-(block, tape) fields n_blocks * tau, step_start n_blocks + 1, and
+        step arrays of `nrows` rows (default: every row, step_start[-1])."""
+        nb, tau = self.n_blocks, self.tau
+        want = {f: nb for f, _ in VIEW_FIELDS}
+        for f in ("win_left", "win_right", "off_in", "off_out"):
+            want[f] = nb * tau
+        want["step_start"] = nb + 1
+        if self.step_start.size == nb + 1:
+            S = int(self.step_start[-1]) if nrows is None else int(nrows)
+            want.update(input_mv=S, mv=S * tau, has_write=S * tau, wsym=S * tau)
+        for f, _ in VIEW_FIELDS:
+            if getattr(self, f).size != want[f]:
+                raise SezkpError(-1, f"blocks.{f} holds {getattr(self, f).size} values, expected {want[f]}"
+                                 + (" (a metadata-only or sliced view: use upload_rows with its row range)"
+                                    if f in ("input_mv", "mv", "has_write", "wsym") else ""))
+
     def view(self) -> BlockView:
         v = BlockView()
         v.n_blocks = self.n_blocks

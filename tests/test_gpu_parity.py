@@ -309,6 +309,16 @@ def test_prove_rejects_head_outside_i32(gpu_ok, product):
     blocks = product.partition(imv, mv, hw, ws, T)
     with pytest.raises(product.SezkpError, match="i32 range"):
         product.StarkV1.prove(blocks, bytes(32))
+    # the guard is data-dependent, so a refused trace must not
+    # poison the context: a good trace of the same shape staged next proves
+    ctx = product.ProverContext(0)
+    ctx.upload(blocks)
+    with pytest.raises(product.SezkpError, match="i32 range"):
+        ctx.prove(bytes(32))
+    good = product.partition(imv, np.ones((T, 1), np.int8), hw, ws, T)
+    ctx.stage(good)
+    assert len(ctx.prove(bytes(32)).proof_bytes) > 0
+    ctx.close()
     # the same trace in blocks of 2^24 rows (head <= 2^24 * 127 < 2^31) is accepted
     blocks = product.partition(imv, mv, hw, ws, 1 << 24)
     ctx = product.ProverContext(0)

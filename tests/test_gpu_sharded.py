@@ -441,15 +441,17 @@ def _sliced_worker(rank, world, port, path, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_sharded_sliced_upload_matches_full(gpu_ok, product, oracle, tmp_path, world):
+@pytest.mark.parametrize("world,tau", [(2, 3), (4, 3), (8, 3), (2, 8), (8, 8)])
+def test_sharded_sliced_upload_matches_full(gpu_ok, product, oracle, tmp_path, world, tau):
     """each rank ingests only its slice of a JSONL file (the
     metadata of 1/P of the lines, then the lines over its own rows plus the
     halo) and uploads it with sezkp_ctx_upload_rows. Ragged 333-step blocks
     cross every rank boundary. Every rank's proof equals the oracle's proof of
     the whole trace (bound to the file's Frontier root), and no rank holds
-    the whole trace (row slices of about n / P)."""
-    T, b, tau, seed = 1 << 15, 333, 3, 17
+    the whole trace (row slices of about n / P). tau = 8 takes the 8-tape
+    transposition kernel with slice starts that are not multiples of 8
+    (ADVICE r04)."""
+    T, b, seed = 1 << 15, 333, 17
     blocks = product.synthetic_blocks(T, b, tau, seed)
     path = tmp_path / "b.jsonl"
     path.write_bytes(blocks.to_jsonl())
@@ -474,3 +476,43 @@ def test_sharded_sliced_upload_matches_full(gpu_ok, product, oracle, tmp_path, w
     with pytest.raises(product.SezkpError, match="needs rows"):
         c.upload_rows(full.with_steps(product.BlockSoA.from_jsonl_range(path.read_bytes(), 0, 0)), 0, 0)
     c.close()
+
+
+def test_config5_cli_jsonl_launcher_p8_matches_openmp_oracle(gpu_ok, product, tmp_path):
+    """BASELINE config 5 end to end at full size: the
+    CLI writes T = 2^22, tau = 8 blocks (`simulate`, the reference generator),
+    `export-jsonl` turns them into blocks.jsonl (829 MB), `commit` writes the
+    manifest (Frontier root), and `python -m sezkp_amd.launch prove --gpus 8
+    --comm host` proves from the JSONL file in per-rank slices (8 ranks sharing
+    this GPU through host collectives). The artifact equals the one built from
+    the OpenMP oracle's proof of the same blocks, and the JSONL decodes back to
+    CBOR blocks byte-identical to the CLI's blocks.cbor."""
+    import subprocess
+    import cbor_min
+    from conftest import ROOT
+    cli = os.path.join(PKG, "bin", "sezkp-cli")
+    T, b, tau = 1 << 22, 512, 8
+    cb, jl, man, out = (tmp_path / n for n in ("blocks.cbor", "blocks.jsonl", "manifest.cbor", "proof.cbor"))
+    for args in (["simulate", "--t", str(T), "--b", str(b), "--tau", str(tau), "--out-blocks", str(cb)],
+                 ["export-jsonl", "--input", str(cb), "--output", str(jl)],
+                 ["commit", "--blocks", str(jl), "--out", str(man)]):
+        r = subprocess.run([cli] + args, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, (args[0], r.stderr[-1500:])
+    assert product.BlockSoA.from_jsonl(jl.read_bytes()).to_cbor() == cb.read_bytes()
+    code = ("import sys, hashlib; sys.path[:0]=[%r,%r]\n"
+            "import oracle_ctypes as O, sezkp_amd as S\n"
+            "O.use_mt(16)\n"
+            "bl=S.BlockSoA.from_cbor(open(%r,'rb').read()); r=bl.manifest_frontier_root()\n"
+            "sys.stdout.write(r.hex()+' '+O.prove_v1(bl, r).hex())\n" % (PKG, os.path.join(ROOT, "oracle"), str(cb)))
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    cmd = [sys.executable, "-u", "-m", "sezkp_amd.launch", "prove", "--blocks", str(jl), "--manifest", str(man),
+           "--out", str(out), "--gpus", "8", "--comm", "host"]
+    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    o_out, o_err = child.communicate(timeout=600)
+    assert child.returncode == 0, o_err[-1500:]
+    root_hex, proof_hex = o_out.split()
+    root = bytes.fromhex(root_hex)
+    want = cbor_min.proof_artifact_cbor("stark", root, bytes.fromhex(proof_hex),
+                                        {"proto": "stark-v1", "domain_n": 8 * T, "tau": tau})
+    assert out.read_bytes() == want

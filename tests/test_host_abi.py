@@ -139,6 +139,52 @@ def test_cli_rejects_jsonl_for_stark_and_mismatched_manifest(tmp_path):
     assert r.returncode != 0 and "root mismatch" in r.stderr
 
 
+def test_cli_export_jsonl_round_trips_reference_blocks(tmp_path, product):
+    """`sezkp-cli export-jsonl` (main.rs:400-424): the reference's blocks.cbor
+    -> JSONL, one serde_json object per line; the lines decode back to blocks
+    whose CBOR encoding is byte-identical to the reference's file, and a JSONL
+    input exports to itself. The JSON text itself is parity unpinned (the
+    reference commits no JSONL fixture): it is the layout of `simulate`'s
+    .jsonl output, the encoder of write_block_summaries_jsonl."""
+    cli = os.path.join(PKG, "bin", "sezkp-cli")
+    for b, m in (("ref_blocks.cbor", "ref_manifest.cbor"), ("riscv_blocks.cbor", "riscv_manifest.cbor")):
+        src = os.path.join(GOLDEN, b)
+        out = tmp_path / "sub" / "dir" / "blocks.jsonl"  # the parent directories are created
+        r = subprocess.run([cli, "export-jsonl", "--input", src, "--output", str(out)], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        data = out.read_bytes()
+        back = product.BlockSoA.from_jsonl(data)
+        ref = open(src, "rb").read()
+        assert back.to_cbor() == ref
+        assert r.stdout.startswith(f"Exported {back.n_blocks} blocks")
+        assert data.count(b"\n") == back.n_blocks and data.endswith(b"}\n")
+        again = tmp_path / "again.ndjson"
+        subprocess.run([cli, "export-jsonl", "--input", str(out), "--output", str(again)], check=True,
+                       capture_output=True)
+        assert again.read_bytes() == data
+        # the exported file passes verify-commit against the reference manifest
+        # when its Frontier root equals the batch root (power-of-two leaf count)
+        if back.n_blocks & (back.n_blocks - 1) == 0:
+            r = subprocess.run([cli, "verify-commit", "--blocks", str(out), "--manifest", os.path.join(GOLDEN, m)],
+                               capture_output=True, text=True)
+            assert r.returncode == 0 and r.stdout.startswith("OK:"), r.stderr
+    r = subprocess.run([cli, "export-jsonl", "--input", str(tmp_path / "x.txt"), "--output", str(tmp_path / "y.jsonl")],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "unsupported blocks extension: txt" in r.stderr
+
+
+def test_cli_verify_commit(tmp_path):
+    """`sezkp-cli verify-commit` (main.rs:377-398): OK on the reference's own
+    blocks/manifest pair, a root mismatch on the other fixture's manifest."""
+    cli = os.path.join(PKG, "bin", "sezkp-cli")
+    r = subprocess.run([cli, "verify-commit", "--blocks", os.path.join(GOLDEN, "ref_blocks.cbor"), "--manifest",
+                        os.path.join(GOLDEN, "ref_manifest.cbor")], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("OK:"), r.stderr
+    r = subprocess.run([cli, "verify-commit", "--blocks", os.path.join(GOLDEN, "riscv_blocks.cbor"), "--manifest",
+                        os.path.join(GOLDEN, "ref_manifest.cbor")], capture_output=True, text=True)
+    assert r.returncode != 0 and "root mismatch" in r.stderr
+
+
 def test_kernel_abi_rejects_null_pointers_before_any_launch(product):
     """Every kernel-level entry point checks its device pointers before it
     touches HIP, so these return SEZKP_E_INVALID on a machine without a GPU."""
@@ -154,3 +200,29 @@ def test_kernel_abi_rejects_null_pointers_before_any_launch(product):
     out = C.c_void_p()
     assert lib.sezkp_blocks_decode_cbor(None, 10, C.byref(out), buf, 64) == E
     assert lib.sezkp_blocks_decode_jsonl(b"{}", 2, None, buf, 64) == E
+
+
+def test_block_shapes_checked_before_the_c_abi(product):
+    """partial views (meta_only, concat_meta, with_steps)
+    and wrong row counts must be refused on the host, since sezkp_block_view
+    carries no lengths and the C side would read past the numpy buffers."""
+    b = product.synthetic_blocks(4096, 512, 8, 42)
+    b.check_shape()
+    n = int(b.step_start[-1])
+    meta = b.meta_only()
+    with pytest.raises(product.SezkpError, match="input_mv"):
+        meta.check_shape()
+    meta.check_shape(0)  # metadata-only view: zero rows is consistent
+    with pytest.raises(product.SezkpError):
+        b.check_shape(n - 8)  # upload_rows with more rows in the arrays than nrows
+    sl = product.BlockSoA(b.tau, **{f: getattr(b, f) for f, _ in product._lib.VIEW_FIELDS})
+    sl.mv = sl.mv[: 8 * (n - 1)]
+    with pytest.raises(product.SezkpError, match="mv"):
+        sl.check_shape()
+    bad = product.BlockSoA(b.tau, **{f: getattr(b, f) for f, _ in product._lib.VIEW_FIELDS})
+    bad.off_in = bad.off_in[:-1]
+    with pytest.raises(product.SezkpError, match="off_in"):
+        bad.check_shape()
+    # the prove entry point refuses it too (no device needed: it fails first)
+    with pytest.raises(product.SezkpError):
+        product.StarkV1.prove(meta, b.manifest_root())
