@@ -582,6 +582,20 @@ __global__ void __launch_bounds__(256) k_runroots_scatter(const uint32_t* __rest
   store_level(cap, L16_LOG, (k1 << logP) + d, h);
 }
 
+// the same for every FRI run layer in one launch (a thread per cap node;
+// the layers' node ranges are consecutive in the grid)
+__global__ void __launch_bounds__(256) k_runroots_scatter_multi(const RunRootsBatch B) {
+  uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  int j = 0;
+  while (j < B.n && o >= (B.nrun[j] << B.logP)) o -= B.nrun[j++] << B.logP;
+  if (j >= B.n) return;
+  const uint64_t nrun = B.nrun[j];
+  const uint64_t d = o / nrun, k1 = o % nrun;
+  uint32_t h[8];
+  node_load(B.gathered[j] + 8 * o, h);
+  store_level(B.cap[j], L16_LOG, (k1 << B.logP) + d, h);
+}
+
 // ---------------------------------------------------------- path extraction
 // One 64-lane workgroup per (layer, index): recompute the 64-leaf group that
 // holds the index (levels < lstore), then read stored siblings above.
@@ -689,6 +703,14 @@ hipError_t launch_runroots_scatter(hipStream_t st, const uint32_t* gathered, Tre
   const uint64_t total = nrun_per_rank << logP;
   hipLaunchKernelGGL(k_runroots_scatter, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, gathered, cap,
                      nrun_per_rank, logP);
+  return hipGetLastError();
+}
+
+hipError_t launch_runroots_scatter_multi(hipStream_t st, const RunRootsBatch& B) {
+  if (B.n <= 0 || B.n > RR_BATCH_MAX) return hipErrorInvalidValue;
+  uint64_t total = 0;
+  for (int j = 0; j < B.n; j++) total += B.nrun[j] << B.logP;
+  hipLaunchKernelGGL(k_runroots_scatter_multi, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, B);
   return hipGetLastError();
 }
 

@@ -1670,8 +1670,16 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
       }
       comm->group_end();
     });
-    for (int r = 1; r <= rR; r++)
-      ok(launch_runroots_scatter(st, rr_gather[r], caps[r], (N >> r) >> (L16_LOG + logP), logP), "runroots");
+    for (int r0 = 1; r0 <= rR; r0 += RR_BATCH_MAX) {  // one launch for all run layers (rR <= 32)
+      RunRootsBatch B{};
+      B.logP = logP;
+      for (int r = r0; r <= rR && B.n < RR_BATCH_MAX; r++, B.n++) {
+        B.gathered[B.n] = rr_gather[r];
+        B.cap[B.n] = caps[r];
+        B.nrun[B.n] = (N >> r) >> (L16_LOG + logP);
+      }
+      ok(launch_runroots_scatter_multi(st, B), "runroots");
+    }
   }
   for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
   if (tail_first <= k && !tail_merged) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
@@ -1763,25 +1771,27 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   mark("req_copy");
   const uint32_t* req = host_tr ? d_req : d_req_dev;
   const uint32_t* cnt = host_tr ? nullptr : d_chal->counts;
-  // openings first: their section of the proof (~70% of it) goes back over
-  // PCIe on the side stream while the FRI path kernel runs
+  // the openings and the FRI paths write disjoint sections of the proof image
+  // and are both latency-bound small grids: the openings run on the side
+  // stream beside the path kernel, and (single device) their section (~70% of
+  // the proof) goes back over PCIe from there while the paths still run
   mark("col_open");
-  ok(launch_col_open(st, T, d_tmpl, d_outer, outer_stride, logChunks, req + 3 * max_fri_req, (int)no, PL, d_tabs,
+  HIP_OR_THROW(hipEventRecord(ev_fold, st));
+  HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+  ok(launch_col_open(st2, T, d_tmpl, d_outer, outer_stride, logChunks, req + 3 * max_fri_req, (int)no, PL, d_tabs,
                      d_dlev, d_dplans, d_dtabs, d_dcols, cnt ? cnt + 1 : nullptr),
      "col_open");
   rec(ST_OPEN + 1);
   mark("col_open_issued");
-  if (!sharded) {
-    HIP_OR_THROW(hipEventRecord(ev_fold, st));
-    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
-    HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.fr_off, hipMemcpyDeviceToHost, st2));
-    HIP_OR_THROW(hipEventRecord(ev_tail, st2));
-  }
+  if (!sharded) HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.fr_off, hipMemcpyDeviceToHost, st2));
+  HIP_OR_THROW(hipEventRecord(ev_tail, st2));
   mark("open_d2h_issued");
   ok(launch_fri_paths(st, d_layers, req, (int)nf, PL, cnt), "fri_paths");
   mark("fri_paths_issued");
-  if (sharded)
+  if (sharded) {
+    HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));  // the openings are part of the byte-sum
     coll("proof_allreduce", 2 * P1 * PL.total / (uint64_t)world, [&] { comm->allreduce_sum_u8(PL.base, PL.total, st); });
+  }
   rec(ST_PATHS + 1);
   const uint64_t d2h_from = sharded ? 0 : PL.fr_off;
   HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes + d2h_from, (const uint8_t*)PL.base + d2h_from,

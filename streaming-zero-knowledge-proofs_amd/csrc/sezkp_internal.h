@@ -347,6 +347,14 @@ hipError_t launch_merkle_paths(hipStream_t st, const uint32_t* nodes, const Merk
 hipError_t launch_cyc_pack(hipStream_t st, const uint64_t* cyc, uint64_t* send, uint64_t M, int logP);
 hipError_t launch_cyc_unpack(hipStream_t st, const uint64_t* recv, uint64_t* local, uint64_t M, int logP);
 // gathered[d][k1] (run roots of rank d) -> level-12 node k1*P + d of `cap`
+constexpr int RR_BATCH_MAX = 40;
+struct RunRootsBatch {
+  const uint32_t* gathered[RR_BATCH_MAX];
+  TreeDev cap[RR_BATCH_MAX];
+  uint64_t nrun[RR_BATCH_MAX];  // runs per rank
+  int n, logP;
+};
+hipError_t launch_runroots_scatter_multi(hipStream_t st, const RunRootsBatch& B);
 hipError_t launch_runroots_scatter(hipStream_t st, const uint32_t* gathered, TreeDev cap, uint64_t nrun_per_rank,
                                    int logP);
 // dbeta != null: the fold challenge is read from device memory instead of `beta`

@@ -53,6 +53,9 @@ class BlockSoA:
         for f in ("win_left", "win_right", "off_in", "off_out"):
             want[f] = nb * tau
         want["step_start"] = nb + 1
+        ss = self.step_start
+        if ss.size and (ss[0] != 0 or (ss.size > 1 and bool((ss[1:] < ss[:-1]).any()))):
+            raise SezkpError(-1, "blocks.step_start must start at 0 and never decrease")
         if self.step_start.size == nb + 1:
             S = int(self.step_start[-1]) if nrows is None else int(nrows)
             want.update(input_mv=S, mv=S * tau, has_write=S * tau, wsym=S * tau)

@@ -226,3 +226,10 @@ def test_block_shapes_checked_before_the_c_abi(product):
     # the prove entry point refuses it too (no device needed: it fails first)
     with pytest.raises(product.SezkpError):
         product.StarkV1.prove(meta, b.manifest_root())
+
+
+def test_block_step_start_checked_on_host(product):
+    b = product.synthetic_blocks(64, 32, 2)
+    b.step_start[:] += 32
+    with pytest.raises(product.SezkpError, match="step_start"):
+        b.check_shape()
