@@ -123,20 +123,67 @@ __device__ inline uint64_t gl_inv(uint64_t a) {
 __device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, n);
 }
-#define B3_G(a, b, c, d, x, y)          \
-  a = a + b + (x); d = rotr32(d ^ a, 16); \
-  c = c + d;       b = rotr32(b ^ c, 12); \
-  a = a + b + (y); d = rotr32(d ^ a, 8);  \
-  c = c + d;       b = rotr32(b ^ c, 7);
-#include "b3_schedule.inc"
+
+// BLAKE3 message permutation schedule (sigma_r = PERM^r)
+__device__ constexpr uint8_t B3_SIGMA[7][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
+    {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},  {10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6},
+    {12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4},  {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
+    {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
+
+// Empty asm over the 16 state words: a scheduling barrier. The four G
+// functions of a half-round then issue step by step (4 add3, 4 xor, 4
+// alignbit, 4 add, ...) instead of the compiler's interleave of half-rate
+// (add3, alignbit) and full-rate (xor, add) instructions: on gfx950 a mix
+// issues as if every instruction were half rate, runs of one kind do not
+// (tools/valu_mix.hip; tools/b3_sched.hip: 57.3 -> 61.1 G parent
+// compressions/s at 8 waves per SIMD, 57.0 -> 58.9 at 4).
+#define B3_FENCE(v)                                                                                         \
+  asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),   \
+               "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]),     \
+               "+v"(v[14]), "+v"(v[15]))
+
+// one half-round: G on the columns (diag = 0) or the diagonals, message words
+// m[s[2g]], m[s[2g+1]] for G g. FENCE = 0 leaves round 0 to the compiler, so
+// constant IV / message words still fold there (leaf hashes).
+template <bool DIAG, bool FENCE>
+__device__ __forceinline__ void b3_half_round(uint32_t (&v)[16], const uint32_t (&m)[16], const uint8_t* s) {
+#define B3_STEP(EXPR)                              \
+  _Pragma("unroll") for (int g = 0; g < 4; g++) {  \
+    const int A = g, B = 4 + (DIAG ? (g + 1) & 3 : g), C = 8 + (DIAG ? (g + 2) & 3 : g), \
+              D = 12 + (DIAG ? (g + 3) & 3 : g);   \
+    (void)A; (void)B; (void)C; (void)D;            \
+    EXPR;                                          \
+  }                                                \
+  if (FENCE) B3_FENCE(v);
+  B3_STEP(v[A] = v[A] + v[B] + m[s[2 * g]])
+  B3_STEP(v[D] = v[D] ^ v[A])
+  B3_STEP(v[D] = rotr32(v[D], 16))
+  B3_STEP(v[C] = v[C] + v[D])
+  B3_STEP(v[B] = v[B] ^ v[C])
+  B3_STEP(v[B] = rotr32(v[B], 12))
+  B3_STEP(v[A] = v[A] + v[B] + m[s[2 * g + 1]])
+  B3_STEP(v[D] = v[D] ^ v[A])
+  B3_STEP(v[D] = rotr32(v[D], 8))
+  B3_STEP(v[C] = v[C] + v[D])
+  B3_STEP(v[B] = v[B] ^ v[C])
+  B3_STEP(v[B] = rotr32(v[B], 7))
+#undef B3_STEP
+}
 
 // One-block root hash: out = first 32 bytes of BLAKE3(message of block_len bytes).
 __device__ __forceinline__ void b3_hash_block(const uint32_t (&m)[16], uint32_t block_len, uint32_t (&out)[8]) {
-  uint32_t v0 = B3_IV0, v1 = B3_IV1, v2 = B3_IV2, v3 = B3_IV3, v4 = B3_IV4, v5 = B3_IV5, v6 = B3_IV6, v7 = B3_IV7;
-  uint32_t v8 = B3_IV0, v9 = B3_IV1, v10 = B3_IV2, v11 = B3_IV3, v12 = 0, v13 = 0, v14 = block_len, v15 = B3_ROOT_FLAGS;
-  B3_ROUNDS(m)
-  out[0] = v0 ^ v8; out[1] = v1 ^ v9; out[2] = v2 ^ v10; out[3] = v3 ^ v11;
-  out[4] = v4 ^ v12; out[5] = v5 ^ v13; out[6] = v6 ^ v14; out[7] = v7 ^ v15;
+  uint32_t v[16] = {B3_IV0, B3_IV1, B3_IV2, B3_IV3, B3_IV4, B3_IV5, B3_IV6, B3_IV7,
+                    B3_IV0, B3_IV1, B3_IV2, B3_IV3, 0,      0,      block_len, B3_ROOT_FLAGS};
+  b3_half_round<false, false>(v, m, B3_SIGMA[0]);
+  b3_half_round<true, false>(v, m, B3_SIGMA[0] + 8);
+#pragma unroll
+  for (int r = 1; r < 7; r++) {
+    b3_half_round<false, true>(v, m, B3_SIGMA[r]);
+    b3_half_round<true, true>(v, m, B3_SIGMA[r] + 8);
+  }
+#pragma unroll
+  for (int w = 0; w < 8; w++) out[w] = v[w] ^ v[8 + w];
 }
 // leaf = BLAKE3(8 LE bytes of v)  (merkle.rs:150-160, fri_stream.rs:37-41)
 __device__ __forceinline__ void b3_leaf_u64(uint64_t v, uint32_t (&out)[8]) {

@@ -58,7 +58,8 @@ __device__ __forceinline__ uint64_t dp_load(const NttPassArgs& P, const NttTable
     const uint32_t rk = P.log_src ? (__brev((uint32_t)k) >> (32 - P.log_src)) : 0;  // = e
     uint64_t qv = gl_mul(gl_mul(P.src[src_slot(P, k, rk)], P.inv_n), pow3(T, rk));
     if (P.coset_e) qv = gl_mul(qv, tw_pow(T, ((uint64_t)rk * P.coset_e) & ((1ULL << T.K) - 1), false));  // (w_N^g)^e
-    v = gl_add(v, qv);
+    // q_e = d_e - f(z) z^(n-1-e) / (1 - z^n): minus kappa r^e (DeepPoly)
+    v = gl_sub(gl_add(v, qv), gl_mul(P.dp_rhk[e >> 12], P.dp_rlo[e & 4095]));
   }
   return v;
 }
@@ -1139,14 +1140,14 @@ __global__ void __launch_bounds__(256) k_bintt_dft_twiddle(uint64_t* __restrict_
 }
 
 // ------------------------------------------- DEEP quotient (base domain)
-// See DeepPoly (sezkp_internal.h). k_inv_base: inv_j = 1 / (w_n^j - z) for
-// the base points j in [row0, row0 + nrows) (16 per lane, one Montgomery
-// batch per 4096) and the per-WG partial sums of C_j w_n^j inv_j; WG b of the
-// range writes partial[b] (sharded ranks each own a block of rows and then
-// allgather their partials, so every rank reduces the same sum).
+// See DeepPoly (sezkp_internal.h). k_inv_base: C_j <- D_j = C_j / (w_n^j - z)
+// for the base points j in [row0, row0 + nrows) (16 per lane, one Montgomery
+// batch per 4096) and the per-WG partial sums of D_j w_n^j; WG b of the range
+// writes partial[b] (sharded ranks each own a block of rows and allgather
+// their partials with the INTT coefficients, so every rank reduces the same sum).
 constexpr int DQ_PER = 16;
-__global__ void __launch_bounds__(NTT_THREADS) k_inv_base(const uint64_t* __restrict__ C, uint64_t* __restrict__ inv,
-                                                          uint64_t* __restrict__ partial, int logn,
+__global__ void __launch_bounds__(NTT_THREADS) k_inv_base(uint64_t* __restrict__ C, uint64_t* __restrict__ partial,
+                                                          int logn,
                                                           const DevChal* __restrict__ ch, NttTables T, uint64_t row0,
                                                           uint64_t nrows) {
   const uint64_t z = ch->z;
@@ -1202,9 +1203,10 @@ __global__ void __launch_bounds__(NTT_THREADS) k_inv_base(const uint64_t* __rest
     for (int j = DQ_PER - 1; j >= 0; j--) {
       const uint64_t ij = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
       if (j) inv_run = gl_mul(inv_run, d[j]);
-      inv[i0 + j] = ij;
       const uint64_t xj = gl_add(d[j], z);  // w_n^(i0 + j)
-      acc = gl_add(acc, gl_mul(gl_mul(C[i0 + j], xj), ij));
+      const uint64_t Dj = gl_mul(C[i0 + j], ij);
+      C[i0 + j] = Dj;
+      acc = gl_add(acc, gl_mul(Dj, xj));
     }
   }
 #pragma unroll
@@ -1260,15 +1262,14 @@ hipError_t launch_scale_pow_bitrev(hipStream_t st, uint64_t* a, int logn, uint64
   return hipGetLastError();
 }
 
-// Every WG reduces the partials (f(z) = K1 S, c' = f(z) K2), then grid-
-// strides: C_j <- (C_j - f(z)) inv_j (= q(w^j), j in [row0, row0 + nrows)),
-// rlo[t] = r^t, rhi[t] = c' r^(4096 t).
-__global__ void __launch_bounds__(NTT_THREADS) k_q_tables(uint64_t* __restrict__ C, const uint64_t* __restrict__ inv,
-                                                          const uint64_t* __restrict__ partial, uint32_t nparts,
-                                                          uint64_t row0, uint64_t nrows,
+// Every WG reduces the partials (S; f(z) = K1 S, c' = f(z) K2, kappa = K3 S),
+// then grid-strides over the tables: rlo[t] = r^t, rhi[t] = c' r^(4096 t),
+// rhk[t] = kappa r^(4096 t).
+__global__ void __launch_bounds__(NTT_THREADS) k_q_tables(const uint64_t* __restrict__ partial, uint32_t nparts,
                                                           const DevChal* __restrict__ ch, uint64_t* __restrict__ rlo,
-                                                          uint64_t* __restrict__ rhi, uint32_t nhi) {
-  const uint64_t K1 = ch->K1, K2 = ch->K2, r = ch->rho, r4096 = ch->rho4096;
+                                                          uint64_t* __restrict__ rhi, uint32_t nhi,
+                                                          uint64_t* __restrict__ rhk, uint32_t nhk) {
+  const uint64_t K1 = ch->K1, K2 = ch->K2, K3 = ch->K3, r = ch->rho, r4096 = ch->rho4096;
   __shared__ uint64_t wsum[NTT_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint64_t acc = 0;
@@ -1280,43 +1281,34 @@ __global__ void __launch_bounds__(NTT_THREADS) k_q_tables(uint64_t* __restrict__
   uint64_t S = wsum[0];
 #pragma unroll
   for (int w = 1; w < NTT_THREADS / 64; w++) S = gl_add(S, wsum[w]);
-  const uint64_t fz = gl_mul(K1, S), cp = gl_mul(fz, K2);
+  const uint64_t fz = gl_mul(K1, S), cp = gl_mul(fz, K2), kappa = gl_mul(K3, S);
   const uint64_t g0 = (uint64_t)blockIdx.x * NTT_THREADS + tid, gs = (uint64_t)gridDim.x * NTT_THREADS;
-  for (uint64_t j = row0 + g0; j < row0 + nrows; j += gs) C[j] = gl_mul(gl_sub(C[j], fz), inv[j]);
   for (uint64_t t = g0; t < 4096; t += gs) rlo[t] = gl_pow_dev(r, t);
   for (uint64_t t = g0; t < nhi; t += gs) rhi[t] = gl_mul(cp, gl_pow_dev(r4096, t));
+  for (uint64_t t = g0; t < nhk; t += gs) rhk[t] = gl_mul(kappa, gl_pow_dev(r4096, t));
 }
 
-hipError_t launch_inv_base(hipStream_t st, const uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
-                           const DevChal* ch, const NttTables& T, uint64_t row0, uint64_t nrows) {
+hipError_t launch_inv_base(hipStream_t st, uint64_t* C, uint64_t* partial, int logn, const DevChal* ch,
+                           const NttTables& T, uint64_t row0, uint64_t nrows) {
   const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
   if (logn < 4 || nrows % DQ_PER || row0 % per || row0 + nrows > (1ULL << logn)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_inv_base, dim3((unsigned)((nrows + per - 1) / per)), dim3(NTT_THREADS), 0, st, C, inv_scratch,
+  hipLaunchKernelGGL(k_inv_base, dim3((unsigned)((nrows + per - 1) / per)), dim3(NTT_THREADS), 0, st, C,
                      partial + row0 / per, logn, ch, T, row0, nrows);
   return hipGetLastError();
 }
 
-hipError_t launch_q_tables(hipStream_t st, uint64_t* C, const uint64_t* inv_scratch, const uint64_t* partial, int logn,
-                           int logN, const DevChal* ch, uint64_t* rlo, uint64_t* rhi, uint64_t row0, uint64_t nrows) {
+hipError_t launch_q_tables(hipStream_t st, const uint64_t* partial, int logn, int logN, const DevChal* ch,
+                           uint64_t* rlo, uint64_t* rhi, uint64_t* rhk) {
   if (logn < 4 || logN < logn || logN > 32) return hipErrorInvalidValue;
   const uint64_t n = 1ULL << logn;
   const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
   const uint32_t nparts = (uint32_t)((n + per - 1) / per);
   const uint32_t nhi = logN > 12 ? (1u << (logN - 12)) : 1u;
-  const uint64_t work = std::max<uint64_t>(nrows, std::max<uint64_t>(4096, nhi));
+  const uint32_t nhk = logn > 12 ? (1u << (logn - 12)) : 1u;
+  const uint64_t work = std::max<uint64_t>(4096, nhi);
   const unsigned grid = (unsigned)std::min<uint64_t>(1024, (work + NTT_THREADS - 1) / NTT_THREADS);
-  hipLaunchKernelGGL(k_q_tables, dim3(grid), dim3(NTT_THREADS), 0, st, C, inv_scratch, partial, nparts, row0, nrows, ch,
-                     rlo, rhi, nhi);
+  hipLaunchKernelGGL(k_q_tables, dim3(grid), dim3(NTT_THREADS), 0, st, partial, nparts, ch, rlo, rhi, nhi, rhk, nhk);
   return hipGetLastError();
-}
-
-hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
-                                int logN, const DevChal* ch, uint64_t* rlo, uint64_t* rhi, const NttTables& T) {
-  if (logn < 4 || logN < logn || logN > 32) return hipErrorInvalidValue;
-  const uint64_t n = 1ULL << logn;
-  hipError_t e = launch_inv_base(st, C, inv_scratch, partial, logn, ch, T, 0, n);
-  if (e != hipSuccess) return e;
-  return launch_q_tables(st, C, inv_scratch, partial, logn, logN, ch, rlo, rhi, 0, n);
 }
 
 // ------------------------------------------------------------------ host side
@@ -1420,7 +1412,7 @@ hipError_t ntt_dit(hipStream_t st, uint64_t* a, int logN, bool inverse, const Nt
     P.log_src = log_src; P.inv_n = inv_n; P.coset_e = (i == 0) ? coset_e : 0;
     P.src_logP = (i == 0) ? src_logP : 0;
     P.skip = (i == 0 && src && !dpoly) ? (logN - log_src) : 0;
-    if (i == 0 && dpoly) { P.dp_rlo = dpoly->rlo; P.dp_rhi = dpoly->rhi; P.dp_logN = logN; }
+    if (i == 0 && dpoly) { P.dp_rlo = dpoly->rlo; P.dp_rhi = dpoly->rhi; P.dp_rhk = dpoly->rhk; P.dp_logN = logN; }
     int logC = logN - P.m; if (logC > 4) logC = 4; P.logC = logC;
     uint64_t tiles = (1ULL << logN) >> (P.m + logC);
     if (P.m > NTT_MMAX) {  // X16 tile: 2^m contiguous points

@@ -221,7 +221,7 @@ struct sezkp_ctx {
   uint64_t outer_stride = 0;
   uint32_t* d_colroots = nullptr;
   uint64_t* d_base = nullptr;
-  uint64_t *d_dq_part = nullptr, *d_dq_rlo = nullptr, *d_dq_rhi = nullptr;  // DEEP quotient (DeepPoly)
+  uint64_t *d_dq_part = nullptr, *d_dq_rlo = nullptr, *d_dq_rhi = nullptr, *d_dq_rhk = nullptr;  // DeepPoly
   uint64_t* d_lde = nullptr;
   uint64_t* d_fri = nullptr;
   uint32_t* d_roots = nullptr;
@@ -719,6 +719,7 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
     d_dq_part = dalloc<uint64_t>(n / 4096 + 1);
     d_dq_rlo = dalloc<uint64_t>(4096);
     d_dq_rhi = dalloc<uint64_t>(Ml > 4096 ? Ml >> 12 : 1);
+    d_dq_rhk = dalloc<uint64_t>(n > 4096 ? n >> 12 : 1);
   }
   M = N >> logP;
   logM = logN - logP;
@@ -1466,7 +1467,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   // are [g n/P, (g+1) n/P) (n >= 4096 P). SEZKP_REPLICATED_INTT=1 gathers the
   // n values and runs the n-point INTT on every rank instead.
   const bool dist_intt = sharded && world > 1 && !getenv("SEZKP_REPLICATED_INTT");
-  DeepPoly dpoly{d_dq_rlo, d_dq_rhi};
+  DeepPoly dpoly{d_dq_rlo, d_dq_rhi, d_dq_rhk};
   if (dq && host_tr) {
     const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
     const uint64_t zN = hgl_pow(zn, N / n);
@@ -1489,6 +1490,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     h_chal->K2 = K2;
     h_chal->rho = rho;
     h_chal->rho4096 = hgl_pow(rho, 4096);
+    h_chal->K3 = hgl_mul(hgl_mul(zn, hgl_inv(z)), hgl_inv(n % GL_P_HOST));  // z^(n-1) / n: kappa = K3 S
   }
   if (host_tr)  // alphas, masks and the DEEP constants for the kernels below
     HIP_OR_THROW(hipMemcpyAsync(d_chal, h_chal, offsetof(DevChal, beta), hipMemcpyHostToDevice, st));
@@ -1497,20 +1499,17 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     coll("base_values", P1 * (row_hi - row_lo) * 8,
          [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
   rec(4);
+  const uint64_t dq_per = 4096;  // base rows per partial sum (k_inv_base WG)
   if (dq) {
-    // inverses + partial sums need z only; the q tables wait for the DEEP
-    // constants of the side-stream kernel (device transcript)
-    const uint64_t nrows = row_hi - row_lo, per = 4096;
-    ok(launch_inv_base(st, d_base, d_lde, d_dq_part, logn, d_chal, tw, row_lo, nrows), "inv_base");
-    if (sharded)
-      coll("fz_partials", P1 * (nrows / per) * 8,
-           [&] { comm->allgather(d_dq_part + row_lo / per, d_dq_part, (size_t)(nrows / per) * 8, st); });
-    if (!host_tr) HIP_OR_THROW(hipStreamWaitEvent(st, ev_deep, 0));
-    ok(launch_q_tables(st, d_base, d_lde, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, row_lo, nrows),
-       "q_tables");
-    if (sharded && !dist_intt)
-      coll("q_values", P1 * nrows * 8, [&] { comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st); });
+    // D_j = C_j / (w^j - z) in place + the partial sums of f(z): z only
+    // (DeepPoly); the INTT runs on D, f(z) is needed by the tables only
+    ok(launch_inv_base(st, d_base, d_dq_part, logn, d_chal, tw, row_lo, row_hi - row_lo), "inv_base");
   }
+  // sharded: this rank's partial sums of f(z) travel with the INTT exchange
+  // that gathers every rank's values (one collective)
+  auto gather_fz = [&](uint64_t nrows) {
+    if (dq) comm->allgather(d_dq_part + row_lo / dq_per, d_dq_part, (size_t)(nrows / dq_per) * 8, st);
+  };
   if (dist_intt) {
     const uint64_t m = n >> logP, Q = m >> logP;
     if (row_lo != (uint64_t)rank * m || row_hi - row_lo != m) throw Err{SEZKP_E_INVALID, "sharded INTT: row split"};
@@ -1520,9 +1519,27 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     ok(bintt_dft_twiddle(st, d_lde, world, Q, (uint32_t)rank, logn, tw), "intt_dft");
     coll("intt_alltoall2", P1 * Q * 8, [&] { comm->alltoall(d_lde, blk, Q * 8, st); });  // blk[j] = y_rank[j]
     ok(ntt_dif(st, blk, logn - logP, true, tw), "intt_local");  // slot p: n a_(rank + P bitrev(p))
-    coll("intt_coeffs", P1 * m * 8, [&] { comm->allgather(blk, d_base, m * 8, st); });
+    coll("intt_coeffs", P1 * (m * 8 + (dq ? m / dq_per * 8 : 0)), [&] {
+      comm->group_start();
+      comm->allgather(blk, d_base, m * 8, st);
+      gather_fz(m);
+      comm->group_end();
+    });
   } else {
+    if (sharded && dq) {
+      const uint64_t nrows = row_hi - row_lo;
+      coll("d_values", P1 * (nrows * 8 + nrows / dq_per * 8), [&] {
+        comm->group_start();
+        comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st);
+        gather_fz(nrows);
+        comm->group_end();
+      });
+    }
     ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
+  }
+  if (dq) {  // the DEEP constants of the side-stream kernel (device transcript)
+    if (!host_tr) HIP_OR_THROW(hipStreamWaitEvent(st, ev_deep, 0));
+    ok(launch_q_tables(st, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk), "q_tables");
   }
   rec(5);
   // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on

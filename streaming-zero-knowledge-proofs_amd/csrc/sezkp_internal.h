@@ -40,6 +40,7 @@ struct NttPassArgs {
   // h_e = [e < n] src[p >> 3] n^-1 3^e + rhi[e >> 12] rlo[e & 4095], e = bitrev(p)
   const uint64_t* dp_rlo;
   const uint64_t* dp_rhi;
+  const uint64_t* dp_rhk;
   int dp_logN;
   // out-of-place DIF store (null = in place); nat_out: the last (narrow) DIF
   // pass writes position p to out[bitrev_{nat_logN}(p)] * out_scale, i.e. the
@@ -58,28 +59,33 @@ struct DeepFuse {
   int logN, logP;
   uint32_t g;
 };
-// DEEP as a polynomial (single-device path): y_i / (x_i - z) = H(x_i) with
-// H = q + c S, q = (f - f(z)) / (X - z), S = sum_k z^(N-1-k) X^k and
-// c = f(z) / (3^N - z^N) (x_i^N = 3^N on the coset), so the LDE of H's
-// coefficients h_k = q_k 3^k + c' r^k (r = 3/z, c' = c z^(N-1)) IS the DEEP
-// layer: no per-point inversion. q comes from the base domain, where
-// q(w^j) = (C_j - f(z)) / (w^j - z) needs one batch inversion over n points
-// and f(z) is the barycentric sum  (1 - z^n)/n * sum_j C_j w^j / (w^j - z).
+// DEEP as a polynomial: y_i / (x_i - z) = H(x_i) with H = q + c S,
+// q = (f - f(z)) / (X - z), S = sum_k z^(N-1-k) X^k and c = f(z) / (3^N - z^N)
+// (x_i^N = 3^N on the coset), so the LDE of H's coefficients
+// h_k = q_k 3^k + c' r^k (r = 3/z, c' = c z^(N-1)) IS the DEEP layer: no
+// per-point inversion. f(z) is the barycentric sum (1 - z^n)/n *
+// sum_j C_j w^j / (w^j - z). The INTT does not wait for f(z): on the base
+// domain q(w^j) = D_j - f(z) / (w^j - z) with D_j = C_j / (w^j - z), and the
+// interpolant of 1 / (w^j - z) has the coefficients z^(n-1-k) / (1 - z^n), so
+// q_k = d_k - f(z) z^(n-1-k) / (1 - z^n), and q_k 3^k = d_k 3^k - kappa r^k
+// with kappa = f(z) z^(n-1) / (1 - z^n) = K3 S. The INTT runs on D and the
+// LDE's first pass subtracts kappa r^k for k < n; f(z) (the partial sums) is
+// needed only there, so sharded ranks gather it with the INTT coefficients.
 struct DeepPoly {
   const uint64_t* rlo;  // 4096 entries: r^t
   const uint64_t* rhi;  // N >> 12 entries: c' r^(4096 t)
+  const uint64_t* rhk;  // max(1, n >> 12) entries: kappa r^(4096 t)
 };
-// z, K1 = (1 - z^n) / n, K2 = c' / f(z), r (rho) and r^4096 from ch (device memory)
-hipError_t launch_deep_quotient(hipStream_t st, uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
-                                int logN, const DevChal* ch, uint64_t* rlo, uint64_t* rhi, const NttTables& T);
-// the two halves of launch_deep_quotient over a block of base rows [row0,
-// row0 + nrows) (row0 a multiple of 4096): inverses + this block's partial
-// sums (at partial[row0 / 4096 ...]), then q(w^j) of the block once every
-// partial of the n rows is in `partial` (sharded ranks allgather them between)
-hipError_t launch_inv_base(hipStream_t st, const uint64_t* C, uint64_t* inv_scratch, uint64_t* partial, int logn,
-                           const DevChal* ch, const NttTables& T, uint64_t row0, uint64_t nrows);
-hipError_t launch_q_tables(hipStream_t st, uint64_t* C, const uint64_t* inv_scratch, const uint64_t* partial, int logn,
-                           int logN, const DevChal* ch, uint64_t* rlo, uint64_t* rhi, uint64_t row0, uint64_t nrows);
+// over a block of base rows [row0, row0 + nrows) (row0 a multiple of 4096):
+// C_j <- D_j = C_j / (w^j - z) in place (one Montgomery batch inversion per
+// 4096) and this block's partial sums of C_j w^j / (w^j - z) at
+// partial[row0 / 4096 ...] (z from ch)
+hipError_t launch_inv_base(hipStream_t st, uint64_t* C, uint64_t* partial, int logn, const DevChal* ch,
+                           const NttTables& T, uint64_t row0, uint64_t nrows);
+// once every partial of the n rows is in `partial`: f(z) = K1 S, the DeepPoly
+// tables rlo / rhi / rhk (K1, K2, K3, rho, rho^4096 from ch)
+hipError_t launch_q_tables(hipStream_t st, const uint64_t* partial, int logn, int logN, const DevChal* ch,
+                           uint64_t* rlo, uint64_t* rhi, uint64_t* rhk);
 
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
 // natural order in and out through `scratch` (n words): the first pass reads a
@@ -239,6 +245,7 @@ struct DevChal {
   uint64_t alpha[8];                // derive_alphas (params.rs:82-92); reuse of prover.rs:86-98 in the kernels
   uint64_t mask[4];                 // derive_mask_coeffs (masking.rs:56-79)
   uint64_t z, zn, K1, K2, rho, rho4096;  // OOD point (nudged) and the DEEP-polynomial constants
+  uint64_t K3;                      // z^(n-1) / n: f(z) K3' = K3 S (DeepPoly, the q correction)
   uint64_t beta[FS_MAX_BETAS];      // derive_betas_for_fri (params.rs:109-119)
   uint64_t rows[FS_NQ], frows[FS_NQ];    // derive_queries mod n / mod N (prover.rs:248, 297)
   uint32_t counts[2];               // FRI path / opening requests this rank owns

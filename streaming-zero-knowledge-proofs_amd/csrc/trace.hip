@@ -1270,6 +1270,84 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
 constexpr int DICT_WG_ROWS = 64 << DICT_LANE_LOG;                    // 4096 rows per 64-lane WG
 constexpr int DICT_RANGE_STEP = TR_THREADS * 16;                     // rows per WG sweep
 
+// WG-wide min / max of one column's partial ranges (result valid on tid 0)
+__device__ __forceinline__ void reduce_parts(const int64_t* pp, uint32_t nparts, int64_t& lo, int64_t& hi,
+                                             int64_t* slo, int64_t* shi) {
+  const int tid = threadIdx.x;
+  lo = INT64_MAX;
+  hi = INT64_MIN;
+  for (uint32_t i = tid; i < nparts; i += TR_THREADS) {
+    lo = pp[2 * i] < lo ? pp[2 * i] : lo;
+    hi = pp[2 * i + 1] > hi ? pp[2 * i + 1] : hi;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if ((tid & 63) == 0) { slo[tid >> 6] = lo; shi[tid >> 6] = hi; }
+  __syncthreads();
+  for (int w = 0; w < TR_THREADS / 64; w++) {
+    lo = slo[w] < lo ? slo[w] : lo;
+    hi = shi[w] > hi ? shi[w] : hi;
+  }
+  __syncthreads();
+}
+
+// Table level K by cost: table entries + n / 2^K gathered nodes (one hash
+// each). Pricing gathers from tables of > 1 MB higher (they miss the reading
+// XCD's L2) was measured slower in round 3: the extra compressions of the
+// lower levels cost more than the misses save. (lo, hi): the column's range;
+// (mlo, mhi): its tape's move range (head columns, has_mv), for the delta plan.
+__device__ __forceinline__ DictPlan make_plan(int64_t lo, int64_t hi, bool has_mv, int64_t mlo, int64_t mhi,
+                                              uint64_t n, uint64_t nrows) {
+  DictPlan P{};
+  P.min = lo;
+  P.K = -1;
+  const uint64_t R = hi >= lo ? (uint64_t)hi - (uint64_t)lo + 1 : 1;
+  if (R <= DICT_CAP) {
+    P.R = (uint32_t)R;
+    uint64_t best = 2 * n, tabcost = 0, sz = R;  // K = -1: n leaves + n parents
+    bool open = true;
+    // unrolled: constant pw[] indices keep P in registers (a runtime index put
+    // it in scratch memory, and the kernel took ~23 us for 33 tiny workgroups)
+#pragma unroll
+    for (int k = 0; k < DICT_LEVELS; k++) {
+      open = open && (1ULL << k) <= n && sz <= DICT_CAP;
+      if (open) {
+        P.pw[k] = (uint32_t)sz;
+        tabcost += sz;
+        const uint64_t cost = tabcost + (n >> k);
+        if (cost < best) { best = cost; P.K = k; }
+        sz = sz * sz;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DICT_LEVELS; k++)
+      if (k > P.K) P.pw[k] = 0;
+    // head delta plan (see DictPlan): 4-row groups from (head, 3 moves)
+    const uint64_t dR = mhi >= mlo ? (uint64_t)mhi - (uint64_t)mlo + 1 : 0;
+    if (has_mv && P.K <= 1 && n >= 4 && dR && R * R <= DICT_CAP && dR <= 256 && R * dR * dR * dR <= DICT_CAP) {
+      P.K = 2;
+      P.delta = 1;
+      P.dmin = mlo;
+      P.dR = (uint32_t)dR;
+      P.pw[0] = (uint32_t)R;
+      P.pw[1] = (uint32_t)(R * R);
+      P.pw[2] = (uint32_t)(R * dR * dR * dR);
+      for (int k = 3; k < DICT_LEVELS; k++) P.pw[k] = 0;
+    }
+  }
+  // a lane's rows: 2^(6 + dict_extra(K)) (32 gathered nodes for K >= 1), and
+  // fewer when this device commits fewer than 2^21 rows (a sharded rank), so
+  // the commit still has ~4 waves per SIMD: one step of a per halving
+  int a = dict_extra(P.K);
+  for (uint64_t r = nrows; r < (1ULL << 21) && a > 0; r <<= 1) a--;
+  P.a = (uint32_t)a;
+  return P;
+}
+
 // per-(column, part) min / max of the raw integers: `sweeps` (1..8) sweeps of
 // 16 rows per lane (one 16-byte-or-less load each); parts of 32768 rows keep
 // the grid at ~2K workgroups for 2^21 rows, and a device with fewer rows (a
@@ -1333,91 +1411,20 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const Col
   }
 }
 
-// one WG per dictionary column: reduce the partial ranges and choose K
-// WG-wide min / max of one column's partial ranges (result valid on tid 0)
-__device__ __forceinline__ void reduce_parts(const int64_t* pp, uint32_t nparts, int64_t& lo, int64_t& hi,
-                                             int64_t* slo, int64_t* shi) {
-  const int tid = threadIdx.x;
-  lo = INT64_MAX;
-  hi = INT64_MIN;
-  for (uint32_t i = tid; i < nparts; i += TR_THREADS) {
-    lo = pp[2 * i] < lo ? pp[2 * i] : lo;
-    hi = pp[2 * i + 1] > hi ? pp[2 * i + 1] : hi;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const int64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
-    lo = a < lo ? a : lo;
-    hi = b > hi ? b : hi;
-  }
-  if ((tid & 63) == 0) { slo[tid >> 6] = lo; shi[tid >> 6] = hi; }
-  __syncthreads();
-  for (int w = 0; w < TR_THREADS / 64; w++) {
-    lo = slo[w] < lo ? slo[w] : lo;
-    hi = shi[w] > hi ? shi[w] : hi;
-  }
-  __syncthreads();
-}
-
-// Table level K by cost: table entries + n / 2^K gathered nodes (one hash
-// each). Pricing gathers from tables of > 1 MB higher (they miss the reading
-// XCD's L2) was measured slower in round 3: the extra compressions of the
-// lower levels cost more than the misses save.
+// one WG per dictionary column: reduce the partial ranges (and, for a head
+// column, its tape's move ranges) and choose the plan. (Folding this into
+// k_dict_range's last workgroup through agent-scope completion counters was
+// measured 100 us slower per proof in round 5: the release / acquire cache
+// maintenance of ~2000 workgroups disturbs the L2s the commit then gathers from.)
 __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restrict__ part, uint32_t nparts,
                                                           uint64_t n, uint64_t nrows, const DictCol* __restrict__ dcols,
                                                           DictPlan* __restrict__ plans) {
   __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
-  const int tid = threadIdx.x;
   int64_t lo, hi, mlo = 0, mhi = -1;
   reduce_parts(part + 2 * (uint64_t)blockIdx.x * nparts, nparts, lo, hi, slo, shi);
   const uint32_t mvc = dcols[blockIdx.x].mv;
   if (mvc != NO_DICT) reduce_parts(part + 2 * (uint64_t)mvc * nparts, nparts, mlo, mhi, slo, shi);
-  if (tid != 0) return;
-  DictPlan P{};
-  P.min = lo;
-  P.K = -1;
-  const uint64_t R = hi >= lo ? (uint64_t)hi - (uint64_t)lo + 1 : 1;
-  if (R <= DICT_CAP) {
-    P.R = (uint32_t)R;
-    uint64_t best = 2 * n, tabcost = 0, sz = R;  // K = -1: n leaves + n parents
-    bool open = true;
-    // unrolled: constant pw[] indices keep P in registers (a runtime index put
-    // it in scratch memory, and the kernel took ~23 us for 33 tiny workgroups)
-#pragma unroll
-    for (int k = 0; k < DICT_LEVELS; k++) {
-      open = open && (1ULL << k) <= n && sz <= DICT_CAP;
-      if (open) {
-        P.pw[k] = (uint32_t)sz;
-        tabcost += sz;
-        const uint64_t cost = tabcost + (n >> k);
-        if (cost < best) { best = cost; P.K = k; }
-        sz = sz * sz;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < DICT_LEVELS; k++)
-      if (k > P.K) P.pw[k] = 0;
-    // head delta plan (see DictPlan): 4-row groups from (head, 3 moves)
-    const uint64_t dR = mhi >= mlo ? (uint64_t)mhi - (uint64_t)mlo + 1 : 0;
-    if (mvc != NO_DICT && P.K <= 1 && n >= 4 && dR && R * R <= DICT_CAP && dR <= 256 &&
-        R * dR * dR * dR <= DICT_CAP) {
-      P.K = 2;
-      P.delta = 1;
-      P.dmin = mlo;
-      P.dR = (uint32_t)dR;
-      P.pw[0] = (uint32_t)R;
-      P.pw[1] = (uint32_t)(R * R);
-      P.pw[2] = (uint32_t)(R * dR * dR * dR);
-      for (int k = 3; k < DICT_LEVELS; k++) P.pw[k] = 0;
-    }
-  }
-  // a lane's rows: 2^(6 + dict_extra(K)) (32 gathered nodes for K >= 1), and
-  // fewer when this device commits fewer than 2^21 rows (a sharded rank), so
-  // the commit still has ~4 waves per SIMD: one step of a per halving
-  int a = dict_extra(P.K);
-  for (uint64_t r = nrows; r < (1ULL << 21) && a > 0; r <<= 1) a--;
-  P.a = (uint32_t)a;
-  plans[blockIdx.x] = P;
+  if (threadIdx.x == 0) plans[blockIdx.x] = make_plan(lo, hi, mvc != NO_DICT, mlo, mhi, n, nrows);
 }
 
 // entry e of table level `lvl` of one dictionary column

@@ -527,7 +527,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_fs_point(FsArgs A) {
 }
 
 // DEEP-polynomial constants from z (DeepPoly, sezkp_internal.h): z^n, K1 =
-// (1 - z^n) / n, K2 = z^(N-1) / (3^N - z^N) * G, rho = (3 / z) w_N^rank,
+// (1 - z^n) / n, K2 = z^(N-1) / (3^N - z^N) * G, K3 = z^(n-1) / n, rho = (3 / z) w_N^rank,
 // rho^4096 and the status flag for a z the polynomial form cannot use. One
 // serial chain of ~130 products: it runs on the side stream beside the
 // composition kernel, which needs only the alphas and masks.
@@ -554,6 +554,7 @@ __global__ void __launch_bounds__(64) k_fs_deep(FsArgs A) {
   D->K2 = gl_mul(K2, G);
   D->rho = rho;
   D->rho4096 = gl_pow2k_dev(rho, 12);
+  D->K3 = gl_mul(gl_mul(zn, inv_z), A.inv_n);  // z^(n-1) / n
   // the polynomial form needs z off the base domain and z != 0: otherwise
   // the host proves again with its own transcript (per-point DEEP)
   A.status[1] = (z == 0 || zn == 1 || Dd == 0) ? 1u : 0u;
