@@ -548,7 +548,7 @@ def main():
     dt1 = time.perf_counter() - t1
     single_ms = dt1 / nsp * 1e3
     # the same proofs again with timed events around every stage and around
-    # single launches (the forest, the transcript points): the device stage
+    # the forest launch: the device stage
     # split and the live per-kernel times of the rooflines, kept out of the
     # latency figure above (the events lengthen a proof by ~45 us)
     os.environ["SEZKP_KERNEL_EVENTS"] = "1"
@@ -556,9 +556,9 @@ def main():
     for _ in range(nsp):
         ctx.prove_view(roots[holds[0]])
         for k, v in ctx.stage_times_ms().items():
-            if k.startswith(("k_", "fs_")) or k == "layer0_tree":
+            if k.startswith("k_") or k == "layer0_tree":
                 ksum[k] = ksum.get(k, 0.0) + v
-            if not k.startswith(("host_", "k_", "fs_")):
+            if not k.startswith(("host_", "k_")):
                 stage_sum[k] = stage_sum.get(k, 0.0) + v
     os.environ.pop("SEZKP_KERNEL_EVENTS", None)
     kern_ms = {k: v / nsp for k, v in ksum.items()}
@@ -621,7 +621,6 @@ def main():
             "upload": {"bytes": up_bytes, "stage_plus_prove_ms": t_up_prove * 1e3,
                        "note": "one staged upload (pinned host -> HBM image over PCIe) then its proof, alone"},
             "roofline": roof, "roofline_trees": trees, "stages_ms": stages,
-            "transcript_ms": {k: kern_ms.get(k) for k in ("fs_point1", "fs_point2", "fs_point3")},
         }
         out["roofline_ntt"] = roofline_ntt(args, torch, stages, N, T)
         whole = {"alg_bytes_per_proof": alg_bytes(T, args.tau)["total"]}

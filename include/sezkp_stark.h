@@ -137,8 +137,8 @@ int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], 
  * col_outer, compose, intt, lde_ntt, deep, layer0_tree, layer0_upper,
  * fri_fold_trees, col_openings, fri_paths, total, then host wall / sync-wait /
  * final-wait / serialize (always measured),
- * then single launches timed only when SEZKP_KERNEL_EVENTS=1 is set (else 0):
- * the FRI forest (k_forest16) and the three device transcript points.
+ * then the FRI forest launch (k_forest16), timed only when
+ * SEZKP_KERNEL_EVENTS=1 is set (else 0).
  * Returns the number of values written. */
 int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max);
 /* Asynchronous proving: the context's worker thread runs the proof; wait
@@ -336,15 +336,14 @@ int32_t sezkp_manifest_decode(const uint8_t* data, size_t len, int32_t is_json, 
 /* BLAKE3 hash with extendable output (host). */
 void sezkp_blake3(const uint8_t* data, size_t len, uint8_t* out, size_t out_len);
 
-/* Fiat-Shamir transcript challenges on the device (replaces the host side of
- * Blake3Transcript::challenge_bytes, crates/sezkp-crypto/src/lib.rs:102-123,
- * for a batch): out_i = BLAKE3-XOF(stream[0..pos[i]) || suffix_i, out_len[i])
- * with suffix_i the next sfx_len[i] bytes of `suffixes` (a transcript passes
- * "challenge" || u32 LE len || label). Outputs are concatenated in `out`
- * (sum of out_len bytes). The prover runs the same kernel with the stream
- * template of its schedule; this entry point is its known-answer interface.
- * Limits: stream_len + the suffix bytes <= 40960, nchal <= 16, every
- * out_len a multiple of 8. Host buffers; synchronous on `stream`. */
+/* Fiat-Shamir transcript challenges, the core of
+ * Blake3Transcript::challenge_bytes (crates/sezkp-crypto/src/lib.rs:102-123)
+ * for a batch, on the host with the prover's BLAKE3:
+ * out_i = BLAKE3-XOF(stream[0..pos[i]) || suffix_i, out_len[i]) with suffix_i
+ * the next sfx_len[i] bytes of `suffixes` (a transcript passes "challenge" ||
+ * u32 LE len || label). Outputs are concatenated in `out` (sum of out_len
+ * bytes). The known-answer interface of the prover's transcript. `stream` is
+ * ignored (kept from ABI 3, when this ran a device kernel). */
 int32_t sezkp_fs_xof(const uint8_t* stream_bytes, size_t stream_len, const uint32_t* pos, const uint8_t* suffixes,
                      const uint32_t* sfx_len, const uint32_t* out_len, uint32_t nchal, uint8_t* out, void* stream);
 

@@ -124,12 +124,13 @@ __device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, n);
 }
 
-// BLAKE3 message permutation schedule (sigma_r = PERM^r)
-__device__ constexpr uint8_t B3_SIGMA[7][16] = {
-    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
-    {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},  {10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6},
-    {12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4},  {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
-    {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
+// BLAKE3 message schedule: word i of round r is sigma_r(i), sigma_r = PERM^r
+// (a compile-time function, so every message index below is a constant)
+__host__ __device__ constexpr int b3_sigma(int r, int i) {
+  constexpr int PERM[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+  for (int k = 0; k < r; k++) i = PERM[i];
+  return i;
+}
 
 // Empty asm over the 16 state words: a scheduling barrier. The four G
 // functions of a half-round then issue step by step (4 add3, 4 xor, 4
@@ -143,26 +144,27 @@ __device__ constexpr uint8_t B3_SIGMA[7][16] = {
                "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]),     \
                "+v"(v[14]), "+v"(v[15]))
 
-// one half-round: G on the columns (diag = 0) or the diagonals, message words
-// m[s[2g]], m[s[2g+1]] for G g. FENCE = 0 leaves round 0 to the compiler, so
-// constant IV / message words still fold there (leaf hashes).
-template <bool DIAG, bool FENCE>
-__device__ __forceinline__ void b3_half_round(uint32_t (&v)[16], const uint32_t (&m)[16], const uint8_t* s) {
-#define B3_STEP(EXPR)                              \
-  _Pragma("unroll") for (int g = 0; g < 4; g++) {  \
+// one half-round of round R: G on the columns (DIAG = 0) or the diagonals,
+// message words sigma_R(2g + 8 DIAG), sigma_R(2g + 1 + 8 DIAG) for G g.
+// FENCE = 0 leaves round 0 to the compiler, so constant IV / message words
+// still fold there (leaf hashes).
+template <int R, bool DIAG, bool FENCE>
+__device__ __forceinline__ void b3_half_round(uint32_t (&v)[16], const uint32_t (&m)[16]) {
+#define B3_STEP(EXPR)                                                                     \
+  _Pragma("unroll") for (int g = 0; g < 4; g++) {                                         \
     const int A = g, B = 4 + (DIAG ? (g + 1) & 3 : g), C = 8 + (DIAG ? (g + 2) & 3 : g), \
-              D = 12 + (DIAG ? (g + 3) & 3 : g);   \
-    (void)A; (void)B; (void)C; (void)D;            \
-    EXPR;                                          \
-  }                                                \
+              D = 12 + (DIAG ? (g + 3) & 3 : g);                                          \
+    (void)A; (void)B; (void)C; (void)D;                                                   \
+    EXPR;                                                                                 \
+  }                                                                                       \
   if (FENCE) B3_FENCE(v);
-  B3_STEP(v[A] = v[A] + v[B] + m[s[2 * g]])
+  B3_STEP(v[A] = v[A] + v[B] + m[b3_sigma(R, 2 * g + 8 * DIAG)])
   B3_STEP(v[D] = v[D] ^ v[A])
   B3_STEP(v[D] = rotr32(v[D], 16))
   B3_STEP(v[C] = v[C] + v[D])
   B3_STEP(v[B] = v[B] ^ v[C])
   B3_STEP(v[B] = rotr32(v[B], 12))
-  B3_STEP(v[A] = v[A] + v[B] + m[s[2 * g + 1]])
+  B3_STEP(v[A] = v[A] + v[B] + m[b3_sigma(R, 2 * g + 1 + 8 * DIAG)])
   B3_STEP(v[D] = v[D] ^ v[A])
   B3_STEP(v[D] = rotr32(v[D], 8))
   B3_STEP(v[C] = v[C] + v[D])
@@ -170,18 +172,18 @@ __device__ __forceinline__ void b3_half_round(uint32_t (&v)[16], const uint32_t 
   B3_STEP(v[B] = rotr32(v[B], 7))
 #undef B3_STEP
 }
+template <int R>
+__device__ __forceinline__ void b3_rounds(uint32_t (&v)[16], const uint32_t (&m)[16]) {
+  b3_half_round<R, false, (R > 0)>(v, m);
+  b3_half_round<R, true, (R > 0)>(v, m);
+  if constexpr (R < 6) b3_rounds<R + 1>(v, m);
+}
 
 // One-block root hash: out = first 32 bytes of BLAKE3(message of block_len bytes).
 __device__ __forceinline__ void b3_hash_block(const uint32_t (&m)[16], uint32_t block_len, uint32_t (&out)[8]) {
   uint32_t v[16] = {B3_IV0, B3_IV1, B3_IV2, B3_IV3, B3_IV4, B3_IV5, B3_IV6, B3_IV7,
                     B3_IV0, B3_IV1, B3_IV2, B3_IV3, 0,      0,      block_len, B3_ROOT_FLAGS};
-  b3_half_round<false, false>(v, m, B3_SIGMA[0]);
-  b3_half_round<true, false>(v, m, B3_SIGMA[0] + 8);
-#pragma unroll
-  for (int r = 1; r < 7; r++) {
-    b3_half_round<false, true>(v, m, B3_SIGMA[r]);
-    b3_half_round<true, true>(v, m, B3_SIGMA[r] + 8);
-  }
+  b3_rounds<0>(v, m);
 #pragma unroll
   for (int w = 0; w < 8; w++) out[w] = v[w] ^ v[8 + w];
 }

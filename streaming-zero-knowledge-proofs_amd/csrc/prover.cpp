@@ -165,7 +165,7 @@ struct sezkp_ctx {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // side stream: small FRI layers overlap the forest
   hipStream_t stc = nullptr;  // copy stream: staged uploads (sezkp_ctx_stage)
-  hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr, ev_deep = nullptr;
+  hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr;
   // Trace images, double-buffered: slot[active] feeds the proofs; stage()
   // fills slot[1 - active] on the copy stream while a proof runs, and the
   // next prove() switches to it (its kernels wait for the copy on the device).
@@ -225,24 +225,10 @@ struct sezkp_ctx {
   uint64_t* d_lde = nullptr;
   uint64_t* d_fri = nullptr;
   uint32_t* d_roots = nullptr;
-  // ---- Fiat-Shamir challenges (DevChal) and the device transcript
+  // ---- Fiat-Shamir challenges (DevChal), written by the host transcript
   DevChal* d_chal = nullptr;        // read by every challenge-dependent kernel
-  DevChal* h_chal = nullptr;        // pinned: host-transcript mode's copy source
-  uint32_t* h_status = nullptr;     // pinned: column roots + guard words (device mode)
-  uint32_t* d_req_dev = nullptr;    // device mode: path / opening requests
+  DevChal* h_chal = nullptr;        // pinned: the host transcript's copy source
   uint32_t* d_dict_of = nullptr;
-  bool fs_ok = false;               // the shape's transcript stream fits the device kernel
-  uint8_t* d_fs_S = nullptr;
-  uint32_t fs_s_bytes = 0;
-  uint32_t *d_fs_cvs = nullptr, *d_fs_ccv = nullptr;
-  uint8_t* d_fs_out = nullptr;
-  FsFill* d_fs_fill = nullptr;
-  FsChal* d_fs_chal = nullptr;
-  struct FsPoint {
-    uint32_t B0, B1, nfill, c0, nchal;
-  } fs_pt[4]{};
-  uint32_t fs_out_alpha = 0, fs_out_beta = 0, fs_out_rowq = 0;
-  void build_transcript_layout();
   // ---- sharding: one proof over `world` GPUs (world == 1: the whole prover
   // on this device; every sharded quantity below degenerates to it)
   int rank = 0, world = 1, logP = 0;
@@ -289,10 +275,10 @@ struct sezkp_ctx {
   size_t max_fri_req = 0, max_open_req = 0;
   hipEvent_t ev[ST_NSTAGE + 1]{};
   double stage_ms[ST_NSTAGE + 1]{};
-  // SEZKP_KERNEL_EVENTS=1: event pairs around single launches (the forest,
-  // the three transcript points) for live per-kernel times (bench roofline)
-  hipEvent_t kev[8]{};
-  double kernel_ms[4]{};
+  // SEZKP_KERNEL_EVENTS=1: an event pair around the FRI forest launch for its
+  // live time (bench roofline)
+  hipEvent_t kev[2]{};
+  double kernel_ms = 0;
   // host-side split of one prove(): wall, time blocked in stream syncs,
   // final D2H wait, proof serialization (after the last sync)
   double host_ms[4]{};
@@ -450,7 +436,6 @@ struct sezkp_ctx {
     if (ev_tail) (void)hipEventDestroy(ev_tail);
     if (ev_expand) (void)hipEventDestroy(ev_expand);
     if (ev_cols) (void)hipEventDestroy(ev_cols);
-    if (ev_deep) (void)hipEventDestroy(ev_deep);
     if (stc) (void)hipStreamSynchronize(stc);
     for (auto& sl : slot)
       if (sl.ready) (void)hipEventDestroy(sl.ready);
@@ -475,11 +460,9 @@ struct sezkp_ctx {
   void take_staged();
   // proves into the pinned staging buffer; returns its size (bytes at h_proof)
   size_t prove(const uint8_t root[32]);
-  // host_tr: the host's transcript (three round trips), else the device's;
-  // returns 0 when the device transcript needs the host re-run (DevChal)
-  size_t prove_body(const uint8_t root[32], bool host_tr);
-  FsArgs fs_args(int point, const uint8_t mroot[32]);
-  bool host_transcript() const;
+  // the prover with the host transcript (three round trips: column roots,
+  // layer-0 root, FRI roots)
+  size_t prove_body(const uint8_t root[32]);
 };
 
 // SEZKP_COLL_TIMEOUT_S: how long a sharded rank waits for a stream holding
@@ -673,8 +656,8 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   }
   d_tmpl = dalloc<ColTemplate>(ncols);
   up(d_tmpl, tm.data(), tm.size());
-  // column roots, then the guard words ([0] this rank's guard, [1] the device
-  // transcript's status, [8 + r] rank r's guard when sharded): one D2H copy
+  // column roots, then the guard words ([0] this rank's guard, [8 + r] rank
+  // r's guard when sharded): one D2H copy
   d_colroots = dalloc<uint32_t>((size_t)ncols * 8 + 16);
   d_err = d_colroots + (size_t)ncols * 8;
   HIP_OR_THROW(hipMemset(d_err, 0, 64));
@@ -879,14 +862,11 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
     memcpy(h_proof, w.b.data(), hdr_bytes);
   }
   h_small = halloc<uint32_t>((size_t)(ncols + k + 2) * 8);
-  h_status = halloc<uint32_t>((size_t)ncols * 8 + 16);
   d_chal = dalloc<DevChal>(1);
   h_chal = halloc<DevChal>(1);
-  d_req_dev = dalloc<uint32_t>(max_fri_req * 3 + max_open_req * OPEN_REQ_WORDS);
   d_dict_of = dalloc<uint32_t>((size_t)ncols);
   up(d_dict_of, dict_of.data(), dict_of.size());
   if (k > FS_MAX_BETAS) throw Err{SEZKP_E_INVALID, "LDE domain too large for the challenge record"};
-  build_transcript_layout();
   release_spares();
   loaded = true;
 }
@@ -1029,175 +1009,6 @@ void sezkp_ctx::take_staged() {
   }
 }
 
-// The transcript's byte stream for this shape (crates/sezkp-crypto/src/lib.rs:
-// 74-123 framing, the schedule of prover_body's host mode): every absorb and
-// "after_challenge" ratchet laid out once, the 32-byte roots left as holes
-// the device fills (FsFill), each challenge as its stream position plus its
-// "challenge" || u32 len || label suffix (FsChal). Points: 1 column roots ->
-// alphas, masks, ood point; 2 layer-0 root -> betas; 3 FRI roots -> queries.
-namespace {
-struct FsRec {
-  std::vector<uint8_t> s;
-  std::vector<FsFill> fills;
-  std::vector<FsChal> chal;
-  std::vector<std::string> sfx;
-  void raw(const void* p, size_t n) { s.insert(s.end(), (const uint8_t*)p, (const uint8_t*)p + n); }
-  void str(const std::string& x) { raw(x.data(), x.size()); }
-  void u32(uint32_t x) {
-    const uint8_t b[4] = {(uint8_t)x, (uint8_t)(x >> 8), (uint8_t)(x >> 16), (uint8_t)(x >> 24)};
-    raw(b, 4);
-  }
-  void hdr(const std::string& label, uint32_t len) {
-    str("absorb");
-    u32((uint32_t)label.size());
-    str(label);
-    u32(len);
-  }
-  void absorb_u64(const std::string& label, uint64_t x) {
-    hdr(label, 8);
-    uint8_t b[8];
-    for (int i = 0; i < 8; i++) b[i] = (uint8_t)(x >> (8 * i));
-    raw(b, 8);
-  }
-  void absorb_root(const std::string& label, uint32_t src) {
-    hdr(label, 32);
-    fills.push_back(FsFill{(uint32_t)s.size(), src});
-    s.resize(s.size() + 32, 0);
-  }
-  void challenge(const std::string& label, uint32_t out_len, uint32_t out_off) {
-    std::string x = "challenge";
-    for (int i = 0; i < 4; i++) x.push_back((char)(uint8_t)(label.size() >> (8 * i)));
-    x += label;
-    chal.push_back(FsChal{(uint32_t)s.size(), 0, (uint32_t)x.size(), out_len, out_off});
-    sfx.push_back(x);
-    str("after_challenge");
-    u32((uint32_t)label.size());
-    str(label);
-  }
-};
-}  // namespace
-
-void sezkp_ctx::build_transcript_layout() {
-  const int k = logN;
-  FsRec r;
-  r.str("sezkp.transcript.v0");
-  r.u32(14);
-  r.str("sezkp-stark/v1");
-  r.absorb_root("manifest_root", FS_SRC_MROOT);
-  r.absorb_u64("n", n);
-  r.absorb_u64("tau", tau);
-  r.absorb_u64("n_cols", (uint64_t)ncols);
-  for (int c = 0; c < ncols; c++) r.absorb_root("col_root", FS_SRC_COL + (uint32_t)c);
-  fs_out_alpha = 0;
-  r.challenge("alphas", 64, 0);
-  r.hdr("masks", 5);
-  r.str("masks");
-  r.absorb_u64("n_masks", 1);
-  r.absorb_u64("deg", 4);
-  for (int j = 0; j < 4; j++) r.challenge("mask_coeff", 8, 64 + 8 * j);
-  r.challenge("ood_point", 8, 96);
-  const size_t f1 = r.fills.size(), c1 = r.chal.size();
-  r.absorb_root("fri_layer_root", FS_SRC_FRI);
-  fs_out_beta = 104;
-  r.challenge("fri_betas", 8 * (uint32_t)k, fs_out_beta);
-  const size_t f2 = r.fills.size(), c2 = r.chal.size();
-  for (int l = 1; l <= k; l++) r.absorb_root("fri_layer_root", FS_SRC_FRI + (uint32_t)l);
-  fs_out_rowq = fs_out_beta + 8 * k;
-  r.challenge("row_queries", 8 * NUM_QUERIES, fs_out_rowq);
-  r.challenge("row_queries", 8 * NUM_QUERIES, fs_out_rowq + 8 * NUM_QUERIES);
-  const size_t f3 = r.fills.size(), c3 = r.chal.size();
-  // suffixes after the stream
-  const uint32_t slen = (uint32_t)r.s.size();
-  for (size_t i = 0; i < r.chal.size(); i++) {
-    r.chal[i].sfx_off = (uint32_t)r.s.size();
-    r.str(r.sfx[i]);
-  }
-  fs_s_bytes = (uint32_t)((r.s.size() + 15) & ~(size_t)15);
-  r.s.resize(fs_s_bytes + 16, 0);
-  fs_ok = fs_s_bytes <= (uint32_t)FS_S_MAX;
-  if (!fs_ok) return;  // very wide traces (tau >~ 100): the host transcript
-  auto pmax = [&](size_t a, size_t b) {
-    uint32_t m = 0;
-    for (size_t i = a; i < b; i++) m = std::max(m, r.chal[i].pos);
-    return m;
-  };
-  fs_pt[1] = FsPoint{0, pmax(0, c1) / 64, (uint32_t)f1, 0, (uint32_t)c1};
-  fs_pt[2] = FsPoint{fs_pt[1].B1, pmax(c1, c2) / 64, (uint32_t)f2, (uint32_t)c1, (uint32_t)(c2 - c1)};
-  fs_pt[3] = FsPoint{fs_pt[2].B1, pmax(c2, c3) / 64, (uint32_t)f3, (uint32_t)c2, (uint32_t)(c3 - c2)};
-  (void)slen;
-  d_fs_S = dalloc<uint8_t>(r.s.size());
-  HIP_OR_THROW(hipMemcpy(d_fs_S, r.s.data(), r.s.size(), hipMemcpyHostToDevice));
-  d_fs_cvs = dalloc<uint32_t>(8 * ((size_t)fs_s_bytes / 64 + 2));
-  d_fs_ccv = dalloc<uint32_t>(8 * ((size_t)fs_s_bytes / 1024 + 2));
-  d_fs_out = dalloc<uint8_t>((size_t)fs_out_rowq + 16 * NUM_QUERIES + 64);
-  d_fs_fill = dalloc<FsFill>(r.fills.size());
-  HIP_OR_THROW(hipMemcpy(d_fs_fill, r.fills.data(), r.fills.size() * sizeof(FsFill), hipMemcpyHostToDevice));
-  d_fs_chal = dalloc<FsChal>(r.chal.size());
-  HIP_OR_THROW(hipMemcpy(d_fs_chal, r.chal.data(), r.chal.size() * sizeof(FsChal), hipMemcpyHostToDevice));
-}
-
-FsArgs sezkp_ctx::fs_args(int point, const uint8_t mroot[32]) {
-  const FsPoint& P = fs_pt[point];
-  FsArgs a{};
-  a.S = d_fs_S;
-  a.s_bytes = fs_s_bytes;
-  a.B0 = P.B0;
-  a.B1 = P.B1;
-  a.cvs = d_fs_cvs;
-  a.ccv = d_fs_ccv;
-  a.fills = d_fs_fill;
-  a.nfill = P.nfill;
-  a.chal = d_fs_chal + P.c0;
-  a.nchal = P.nchal;
-  a.out = d_fs_out;
-  for (int i = 0; i < 8; i++)
-    a.mroot[i] = (uint32_t)mroot[4 * i] | (uint32_t)mroot[4 * i + 1] << 8 | (uint32_t)mroot[4 * i + 2] << 16 |
-                 (uint32_t)mroot[4 * i + 3] << 24;
-  a.colroots = d_colroots;
-  a.friroots = d_roots;
-  a.point = point;
-  a.ch = d_chal;
-  a.status = d_err;
-  a.out_alpha = fs_out_alpha;
-  a.out_beta = fs_out_beta;
-  a.out_rowq = fs_out_rowq;
-  a.logn = logn;
-  a.logN = logN;
-  a.logP = logP;
-  a.inv3 = hgl_inv(3);
-  a.threeN = hgl_pow(3, N);
-  a.inv_n = hgl_inv(n % GL_P_HOST);
-  a.w_rank = hgl_pow(hgl_root_2exp((uint32_t)logN), (uint64_t)rank);
-  FsQueryArgs& q = a.q;
-  q.PL = PL;
-  q.req = d_req_dev;
-  q.max_fri_req = max_fri_req;
-  q.dict_of = d_dict_of;
-  q.final_val = lvals[logN];
-  q.ch_lo = ch_lo;
-  q.ch_hi = ch_hi;
-  q.tau = tau;
-  q.sharded = sharded() ? 1u : 0u;
-  q.world = (uint32_t)world;
-  q.rank = (uint32_t)rank;
-  q.rR = rR;
-  return a;
-}
-
-// The host transcript is the default: the device one (SEZKP_DEVICE_TRANSCRIPT=1,
-// csrc/transcript.hip) measured slower in both views (round 4,
-// profiles/r04/transcript_ab.txt: its three one-workgroup kernels take
-// 40 / 23 / 54 us of serial BLAKE3 chains per proof against ~35 us per host
-// round trip, and its single workgroups wait for a free CU behind the other
-// proofs' trees: in flight 7.51 against 7.98 10^9 elements/s). The device
-// transcript is never used for traces below 16 rows (the per-point DEEP), for
-// streams too long for the kernel's LDS or with SEZKP_NO_DEEP_POLY=1 (the
-// per-point DEEP needs z on the host). Read per proof (the tests switch it).
-bool sezkp_ctx::host_transcript() const {
-  const char* e = getenv("SEZKP_DEVICE_TRANSCRIPT");
-  return !(e && atoi(e) != 0) || !fs_ok || logn < 4 || getenv("SEZKP_NO_DEEP_POLY") != nullptr;
-}
-
 size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   if (broken)
     throw Err{SEZKP_E_DEVICE, "context unusable: an earlier sharded prove failed after its first collective and "
@@ -1206,16 +1017,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   coll_used = 0;
   coll_stats.clear();
   try {
-    const bool host = host_transcript();
-    size_t len = prove_body(mroot, host);
-    if (len == 0 && !host) {
-      if (sharded()) {  // the same status on every rank: the collectives start again in step
-        coll_used = 0;
-        coll_stats.clear();
-      }
-      len = prove_body(mroot, true);
-    }
-    return len;
+    return prove_body(mroot);
   } catch (...) {
     // peers may already be waiting in a collective this rank will never join
     // (or this rank in one they never join): abort so that every rank's
@@ -1232,7 +1034,7 @@ size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   }
 }
 
-size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
+size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   if (!loaded) throw Err{SEZKP_E_INVALID, "no trace uploaded"};
   // the trace image was fixed by take_staged() in the public entry point that
   // started this proof (for prove_async: before the worker runs, so a stage()
@@ -1276,11 +1078,11 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   auto rec = [&](int s) {
     if (stage_ev) HIP_OR_THROW(hipEventRecord(ev[s], st));
   };
-  bool kdone[4] = {false, false, false, false};
-  auto krec = [&](int i, bool end) {
+  bool kdone = false;
+  auto krec = [&](bool end) {
     if (!kprobe) return;
-    HIP_OR_THROW(hipEventRecord(kev[2 * i + (end ? 1 : 0)], st));
-    if (end) kdone[i] = true;
+    HIP_OR_THROW(hipEventRecord(kev[end ? 1 : 0], st));
+    if (end) kdone = true;
   };
   static const bool sync_debug = getenv("SEZKP_SYNC_DEBUG") != nullptr;  // name the failing kernel
   auto ok = [&](hipError_t e, const char* what) {
@@ -1388,75 +1190,63 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     }
   };
   // ---- transcript prelude + column roots (prover.rs:67-81) -> alphas,
-  // masks, z. Every rank replays the same transcript, so challenges need no
-  // broadcast. Device mode: one workgroup derives them on the stream (no host
-  // round trip); host mode: the roots come back and the host's transcript
-  // writes the challenge record that the kernels read.
+  // masks, z: the roots come back and the host's transcript writes the
+  // challenge record that the kernels read. (A device transcript that
+  // derived every challenge on the stream was built in round 4 and measured
+  // slower: one workgroup's chain of dependent BLAKE3 compressions took
+  // 40 / 23 / 54 us per point against ~25 / 17 / 21 us of host round trip; it
+  // was removed in round 5.)
   Transcript tr("sezkp-stark/v1");
   const uint64_t shift_inv = hgl_inv(3);
   uint64_t z = 0, zn = 0;
-  if (host_tr) {
-    // one copy: the column roots and the guard words stored right behind them
-    // (d_err = d_colroots + 8 ncols; sharded, every rank's word at d_err + 8)
-    const size_t gofs = sharded ? 8 : 0;
-    HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32 + 4 * (gofs + nguard), hipMemcpyDeviceToHost,
-                                st));
-    sync();
-    mark("sync1");
-    const uint32_t* colroots_h = h_small;
-    check_guards(h_small + 8 * ncols + gofs, nguard);
-    std::vector<uint8_t> colroots((const uint8_t*)colroots_h, (const uint8_t*)colroots_h + (size_t)ncols * 32);
-    for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
+  // one copy: the column roots and the guard words stored right behind them
+  // (d_err = d_colroots + 8 ncols; sharded, every rank's word at d_err + 8)
+  const size_t gofs = sharded ? 8 : 0;
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32 + 4 * (gofs + nguard), hipMemcpyDeviceToHost,
+                              st));
+  sync();
+  mark("sync1");
+  const uint32_t* colroots_h = h_small;
+  check_guards(h_small + 8 * ncols + gofs, nguard);
+  std::vector<uint8_t> colroots((const uint8_t*)colroots_h, (const uint8_t*)colroots_h + (size_t)ncols * 32);
+  for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
 
-    // ---- transcript prelude + column roots (prover.rs:67-81); every rank
-    // replays the same transcript, so challenges need no broadcast
-    tr.absorb("manifest_root", mroot, 32);
-    tr.absorb_u64("n", n);
-    tr.absorb_u64("tau", tau);
-    tr.absorb_u64("n_cols", (uint64_t)ncols);
-    for (int c = 0; c < ncols; c++) tr.absorb("col_root", colroots.data() + 32 * c, 32);
-    // alphas (params.rs:82-92) with the reuse of prover.rs:86-98
-    mark("tr_roots");
-    auto ab = tr.challenge("alphas", 64);
-    uint64_t a[8];
-    for (int i = 0; i < 8; i++) a[i] = rd64(ab.data() + 8 * i) % GL_P_HOST;
-    // masks (masking.rs:56-79): one cubic
-    tr.absorb("masks", "masks", 5);
-    tr.absorb_u64("n_masks", 1);
-    tr.absorb_u64("deg", 4);
-    uint64_t mask[4];
-    for (int j = 0; j < 4; j++) mask[j] = rd64(tr.challenge("mask_coeff", 8).data()) % GL_P_HOST;
-    // OOD point + coset nudge (prover.rs:119-135)
-    z = rd64(tr.challenge("ood_point", 8).data()) % GL_P_HOST;
-    for (;;) {
-      uint64_t t = hgl_mul(z, shift_inv);
-      for (int i = 0; i < k; i++) t = hgl_mul(t, t);
-      if (t != 1) break;
-      z = hgl_add(z, 1);
-    }
-    for (int i = 0; i < 8; i++) h_chal->alpha[i] = a[i];
-    for (int j = 0; j < 4; j++) h_chal->mask[j] = mask[j];
-    zn = hgl_pow(z, n);
-  } else {
-    const FsArgs a1 = fs_args(1, mroot);
-    krec(1, false);
-    ok(launch_fs_point(st, a1), "fs_point1");
-    krec(1, true);
-    // the DEEP constants' chain of products beside the composition (side stream)
-    HIP_OR_THROW(hipEventRecord(ev_fold, st));
-    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
-    ok(launch_fs_deep(st2, a1), "fs_deep");
-    HIP_OR_THROW(hipEventRecord(ev_deep, st2));
+  // ---- transcript prelude + column roots (prover.rs:67-81); every rank
+  // replays the same transcript, so challenges need no broadcast
+  tr.absorb("manifest_root", mroot, 32);
+  tr.absorb_u64("n", n);
+  tr.absorb_u64("tau", tau);
+  tr.absorb_u64("n_cols", (uint64_t)ncols);
+  for (int c = 0; c < ncols; c++) tr.absorb("col_root", colroots.data() + 32 * c, 32);
+  // alphas (params.rs:82-92) with the reuse of prover.rs:86-98
+  mark("tr_roots");
+  auto ab = tr.challenge("alphas", 64);
+  uint64_t a[8];
+  for (int i = 0; i < 8; i++) a[i] = rd64(ab.data() + 8 * i) % GL_P_HOST;
+  // masks (masking.rs:56-79): one cubic
+  tr.absorb("masks", "masks", 5);
+  tr.absorb_u64("n_masks", 1);
+  tr.absorb_u64("deg", 4);
+  uint64_t mask[4];
+  for (int j = 0; j < 4; j++) mask[j] = rd64(tr.challenge("mask_coeff", 8).data()) % GL_P_HOST;
+  // OOD point + coset nudge (prover.rs:119-135)
+  z = rd64(tr.challenge("ood_point", 8).data()) % GL_P_HOST;
+  for (;;) {
+    uint64_t t = hgl_mul(z, shift_inv);
+    for (int i = 0; i < k; i++) t = hgl_mul(t, t);
+    if (t != 1) break;
+    z = hgl_add(z, 1);
   }
+  for (int i = 0; i < 8; i++) h_chal->alpha[i] = a[i];
+  for (int j = 0; j < 4; j++) h_chal->mask[j] = mask[j];
+  zn = hgl_pow(z, n);
   // ---- composition (this rank's rows), DEEP quotient, INTT
   mark("z_done");
   // single device: DEEP as the LDE of H = q + c S (DeepPoly); the base
   // evaluations become q(w^j) before the INTT. Not when z^n = 1 (z on the
   // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
   mark("compose_issued");
-  // (device mode is only chosen where the polynomial form applies; a z that
-  // falls outside it sets the status flag and the host proves again)
-  const bool dq = host_tr ? (logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY")) : true;
+  const bool dq = logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY");
   // sharded: each rank turns its own rows into q(w^j) (the partial sums of
   // f(z) are allgathered in between), then the q values are allgathered for
   // the n-point INTT every rank's coset needs; without the quotient the
@@ -1468,7 +1258,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   // n values and runs the n-point INTT on every rank instead.
   const bool dist_intt = sharded && world > 1 && !getenv("SEZKP_REPLICATED_INTT");
   DeepPoly dpoly{d_dq_rlo, d_dq_rhi, d_dq_rhk};
-  if (dq && host_tr) {
+  if (dq) {
     const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
     const uint64_t zN = hgl_pow(zn, N / n);
     uint64_t K2 = hgl_mul(hgl_pow(z, N - 1), hgl_inv(hgl_sub(hgl_pow(3, N), zN)));  // c' = f(z) K2
@@ -1492,8 +1282,8 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     h_chal->rho4096 = hgl_pow(rho, 4096);
     h_chal->K3 = hgl_mul(hgl_mul(zn, hgl_inv(z)), hgl_inv(n % GL_P_HOST));  // z^(n-1) / n: kappa = K3 S
   }
-  if (host_tr)  // alphas, masks and the DEEP constants for the kernels below
-    HIP_OR_THROW(hipMemcpyAsync(d_chal, h_chal, offsetof(DevChal, beta), hipMemcpyHostToDevice, st));
+  // alphas, masks and the DEEP constants for the kernels below
+  HIP_OR_THROW(hipMemcpyAsync(d_chal, h_chal, offsetof(DevChal, beta), hipMemcpyHostToDevice, st));
   ok(launch_compose(st, T, d_chal, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
   if (sharded && !dq && !dist_intt)
     coll("base_values", P1 * (row_hi - row_lo) * 8,
@@ -1537,10 +1327,8 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     }
     ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
   }
-  if (dq) {  // the DEEP constants of the side-stream kernel (device transcript)
-    if (!host_tr) HIP_OR_THROW(hipStreamWaitEvent(st, ev_deep, 0));
+  if (dq)
     ok(launch_q_tables(st, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk), "q_tables");
-  }
   rec(5);
   // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on
   // 3 w_N^g <w_M> (M = N/P), no communication
@@ -1584,20 +1372,14 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   rec(ST_L0UP + 1);
   // ---- layer-0 root -> all betas at once (prover.rs:184-198)
   std::vector<uint8_t> roots((size_t)(k + 1) * 32);
-  if (host_tr) {
-    HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
-    sync();
-    mark("sync2");
-    memcpy(roots.data(), h_small, 32);
-    tr.absorb("fri_layer_root", roots.data(), 32);
-    auto bb = tr.challenge("fri_betas", 8 * (size_t)k);
-    for (int r = 0; r < k; r++) h_chal->beta[r] = rd64(bb.data() + 8 * r) % GL_P_HOST;
-    HIP_OR_THROW(hipMemcpyAsync(d_chal->beta, h_chal->beta, 8 * (size_t)k, hipMemcpyHostToDevice, st));
-  } else {
-    krec(2, false);
-    ok(launch_fs_point(st, fs_args(2, mroot)), "fs_point2");
-    krec(2, true);
-  }
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
+  sync();
+  mark("sync2");
+  memcpy(roots.data(), h_small, 32);
+  tr.absorb("fri_layer_root", roots.data(), 32);
+  auto bb = tr.challenge("fri_betas", 8 * (size_t)k);
+  for (int r = 0; r < k; r++) h_chal->beta[r] = rd64(bb.data() + 8 * r) % GL_P_HOST;
+  HIP_OR_THROW(hipMemcpyAsync(d_chal->beta, h_chal->beta, 8 * (size_t)k, hipMemcpyHostToDevice, st));
 
   // ---- FRI folds + layer trees (prover.rs:192-239). Folds of run layers are
   // rank-local (i and i + len/2 share i mod 4096P). The kernels read the
@@ -1647,9 +1429,9 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   // workgroups (sharded: their own kernel on the side stream)
   if (tail_merged) {
     const TailArgs ta = tail_args(rep_src);
-    krec(0, false);
+    krec(false);
     ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf, 0, tree_wg_log), "fri_forest");
-    krec(0, true);
+    krec(true);
   } else if (!sharded) {
     launch_tail(rep_src);
     ok(launch_forest16(st, d_forest, n_forest, forest_wgs, nullptr, nullptr, 0, tree_wg_log), "fri_forest");
@@ -1707,87 +1489,77 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   std::vector<uint64_t> pos((size_t)NUM_QUERIES * (k + 1));
   size_t nf = 0, no = 0;
   if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
-  if (host_tr) {
-    HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
-    sync();
-    mark("sync3");
-    memcpy(roots.data(), h_small, (size_t)(k + 1) * 32);
-    for (int r = 1; r <= k; r++) tr.absorb("fri_layer_root", roots.data() + 32 * r, 32);
+  HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
+  sync();
+  mark("sync3");
+  memcpy(roots.data(), h_small, (size_t)(k + 1) * 32);
+  for (int r = 1; r <= k; r++) tr.absorb("fri_layer_root", roots.data() + 32 * r, 32);
 
-    // ---- queries (prover.rs:248, 297)
-    mark("tr_fri");
-    auto qb = tr.challenge("row_queries", 8 * NUM_QUERIES);
-    for (int i = 0; i < NUM_QUERIES; i++) rows[i] = rd64(qb.data() + 8 * i) % n;
-    auto fb = tr.challenge("row_queries", 8 * NUM_QUERIES);
-    for (int i = 0; i < NUM_QUERIES; i++) frows[i] = rd64(fb.data() + 8 * i) % N;
+  // ---- queries (prover.rs:248, 297)
+  mark("tr_fri");
+  auto qb = tr.challenge("row_queries", 8 * NUM_QUERIES);
+  for (int i = 0; i < NUM_QUERIES; i++) rows[i] = rd64(qb.data() + 8 * i) % n;
+  auto fb = tr.challenge("row_queries", 8 * NUM_QUERIES);
+  for (int i = 0; i < NUM_QUERIES; i++) frows[i] = rd64(fb.data() + 8 * i) % N;
 
-    mark("queries");
-    // FRI path requests (layer, index, ordinal) for the records this rank owns:
-    // run layers by run owner, replicated layers on rank 0
-    for (int q = 0; q < NUM_QUERIES; q++) {
-      uint64_t* p = &pos[(size_t)q * (k + 1)];
-      p[0] = frows[q];
-      uint64_t len = N;
-      for (int r = 0; r < k; r++) {
-        const uint64_t half = len / 2;
-        for (int side = 0; side < 2; side++) {
-          const uint64_t idx = side ? (p[r] ^ half) : p[r];
-          const int owner = (sharded && r <= rR) ? (int)((idx >> L16_LOG) & (uint64_t)(world - 1)) : 0;
-          if (owner != rank) continue;
-          h_req[3 * nf] = (uint32_t)r;
-          h_req[3 * nf + 1] = (uint32_t)idx;
-          h_req[3 * nf + 2] = (uint32_t)(q * 2 * k + 2 * r + side);
-          nf++;
-        }
-        p[r + 1] = p[r] % half;
-        len = half;
+  mark("queries");
+  // FRI path requests (layer, index, ordinal) for the records this rank owns:
+  // run layers by run owner, replicated layers on rank 0
+  for (int q = 0; q < NUM_QUERIES; q++) {
+    uint64_t* p = &pos[(size_t)q * (k + 1)];
+    p[0] = frows[q];
+    uint64_t len = N;
+    for (int r = 0; r < k; r++) {
+      const uint64_t half = len / 2;
+      for (int side = 0; side < 2; side++) {
+        const uint64_t idx = side ? (p[r] ^ half) : p[r];
+        const int owner = (sharded && r <= rR) ? (int)((idx >> L16_LOG) & (uint64_t)(world - 1)) : 0;
+        if (owner != rank) continue;
+        h_req[3 * nf] = (uint32_t)r;
+        h_req[3 * nf + 1] = (uint32_t)idx;
+        h_req[3 * nf + 2] = (uint32_t)(q * 2 * k + 2 * r + side);
+        nf++;
       }
+      p[r + 1] = p[r] % half;
+      len = half;
     }
-    // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66),
-    // each by the rank owning the row's chunk
-    uint32_t* oreq = h_req + 3 * max_fri_req;
-    size_t ord = 0;
-    auto push_open = [&](int c, uint64_t row) {
-      const uint64_t ch = n >= 1024 ? row >> COL_CHUNK_LOG2 : 0;
-      if (ch >= ch_lo && ch < ch_hi) {
-        uint32_t* rq = oreq + (size_t)OPEN_REQ_WORDS * no;
-        rq[0] = (uint32_t)c;
-        rq[1] = (uint32_t)row;
-        rq[2] = (uint32_t)(row >> 32);
-        rq[3] = (uint32_t)ord;
-        rq[4] = dict_of[c];
-        no++;
-      }
-      ord++;
-    };
-    for (int q = 0; q < NUM_QUERIES; q++) {
-      const uint64_t row = rows[q], ip1 = row + 1 < n ? row + 1 : 0;  // next_wrap
-      for (uint32_t r = 0; r < tau; r++) {
-        push_open(3 + 0 * tau + r, row);   // mv
-        push_open(3 + 0 * tau + r, ip1);   // next_mv
-        push_open(3 + 1 * tau + r, row);   // write_flag
-        push_open(3 + 2 * tau + r, row);   // write_sym
-        push_open(3 + 3 * tau + r, row);   // head
-        push_open(3 + 3 * tau + r, ip1);   // next_head
-        push_open(3 + 4 * tau + r, row);   // win_len
-        push_open(3 + 5 * tau + r, row);   // in_off
-        push_open(3 + 6 * tau + r, row);   // out_off
-      }
-      push_open(1, row);  // is_first
-      push_open(2, row);  // is_last
-      push_open(0, row);  // input_mv
+  }
+  // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66),
+  // each by the rank owning the row's chunk
+  uint32_t* oreq = h_req + 3 * max_fri_req;
+  size_t ord = 0;
+  auto push_open = [&](int c, uint64_t row) {
+    const uint64_t ch = n >= 1024 ? row >> COL_CHUNK_LOG2 : 0;
+    if (ch >= ch_lo && ch < ch_hi) {
+      uint32_t* rq = oreq + (size_t)OPEN_REQ_WORDS * no;
+      rq[0] = (uint32_t)c;
+      rq[1] = (uint32_t)row;
+      rq[2] = (uint32_t)(row >> 32);
+      rq[3] = (uint32_t)ord;
+      rq[4] = dict_of[c];
+      no++;
     }
-  } else {
-    krec(3, false);
-    ok(launch_fs_point(st, fs_args(3, mroot)), "fs_point3");
-    krec(3, true);
-    // grids sized for the most requests this rank can own; the kernels read the counts
-    nf = sharded ? max_fri_req : (size_t)NUM_QUERIES * 2 * k;
-    no = sharded ? max_open_req : (size_t)NUM_QUERIES * (3 + 9 * tau);
+    ord++;
+  };
+  for (int q = 0; q < NUM_QUERIES; q++) {
+    const uint64_t row = rows[q], ip1 = row + 1 < n ? row + 1 : 0;  // next_wrap
+    for (uint32_t r = 0; r < tau; r++) {
+      push_open(3 + 0 * tau + r, row);   // mv
+      push_open(3 + 0 * tau + r, ip1);   // next_mv
+      push_open(3 + 1 * tau + r, row);   // write_flag
+      push_open(3 + 2 * tau + r, row);   // write_sym
+      push_open(3 + 3 * tau + r, row);   // head
+      push_open(3 + 3 * tau + r, ip1);   // next_head
+      push_open(3 + 4 * tau + r, row);   // win_len
+      push_open(3 + 5 * tau + r, row);   // in_off
+      push_open(3 + 6 * tau + r, row);   // out_off
+    }
+    push_open(1, row);  // is_first
+    push_open(2, row);  // is_last
+    push_open(0, row);  // input_mv
   }
   mark("req_copy");
-  const uint32_t* req = host_tr ? d_req : d_req_dev;
-  const uint32_t* cnt = host_tr ? nullptr : d_chal->counts;
+  const uint32_t* req = d_req;
   // the openings and the FRI paths write disjoint sections of the proof image
   // and are both latency-bound small grids: the openings run on the side
   // stream beside the path kernel, and (single device) their section (~70% of
@@ -1796,14 +1568,14 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   HIP_OR_THROW(hipEventRecord(ev_fold, st));
   HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
   ok(launch_col_open(st2, T, d_tmpl, d_outer, outer_stride, logChunks, req + 3 * max_fri_req, (int)no, PL, d_tabs,
-                     d_dlev, d_dplans, d_dtabs, d_dcols, cnt ? cnt + 1 : nullptr),
+                     d_dlev, d_dplans, d_dtabs, d_dcols, nullptr),
      "col_open");
   rec(ST_OPEN + 1);
   mark("col_open_issued");
   if (!sharded) HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.fr_off, hipMemcpyDeviceToHost, st2));
   HIP_OR_THROW(hipEventRecord(ev_tail, st2));
   mark("open_d2h_issued");
-  ok(launch_fri_paths(st, d_layers, req, (int)nf, PL, cnt), "fri_paths");
+  ok(launch_fri_paths(st, d_layers, req, (int)nf, PL, nullptr), "fri_paths");
   mark("fri_paths_issued");
   if (sharded) {
     HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));  // the openings are part of the byte-sum
@@ -1814,26 +1586,13 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
   HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes + d2h_from, (const uint8_t*)PL.base + d2h_from,
                               PL.total - d2h_from, hipMemcpyDeviceToHost, st));
   mark("proof_d2h_issued");
-  if (host_tr) {
-    HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), lvals[k], 8, hipMemcpyDeviceToHost, st));
-  } else {  // column roots, guard words and the transcript's status flag in one copy
-    HIP_OR_THROW(hipMemcpyAsync(h_status, d_colroots, ((size_t)ncols * 8 + 16) * 4, hipMemcpyDeviceToHost, st));
-  }
+  HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), lvals[k], 8, hipMemcpyDeviceToHost, st));
   if (!sharded) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
   mark("issued");
   sync();
   mark("sync4");
   if (htrace) {
     for (auto& m : hmarks) fprintf(stderr, "%s %.1f ", m.first, m.second);
-    if (!host_tr) {  // device transcript: us per kernel phase (fill, chain, tails, xof, derive) of each point
-      uint64_t t[3][6];
-      HIP_OR_THROW(hipMemcpy(t, d_chal->fs_t, sizeof t, hipMemcpyDeviceToHost));
-      for (int p = 0; p < 3; p++) {
-        fprintf(stderr, "fs%d", p + 1);
-        for (int i = 1; i < 6; i++) fprintf(stderr, " %.1f", (double)(t[p][i] - t[p][i - 1]) / 100.0);
-        fprintf(stderr, " ");
-      }
-    }
     fprintf(stderr, "\n");
   }
   for (int s = 0; s <= ST_NSTAGE; s++) stage_ms[s] = 0;
@@ -1846,30 +1605,14 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32], bool host_tr) {
     (void)hipEventElapsedTime(&tot, ev[0], ev[ST_NSTAGE]);
     stage_ms[ST_NSTAGE] = tot;
   }
-  for (int i = 0; i < 4; i++) {
+  {
     float ms = 0;
-    kernel_ms[i] = kdone[i] && hipEventElapsedTime(&ms, kev[2 * i], kev[2 * i + 1]) == hipSuccess ? ms : 0.0;
+    kernel_ms = kdone && hipEventElapsedTime(&ms, kev[0], kev[1]) == hipSuccess ? ms : 0.0;
   }
   have_times = true;
   // an event pair not recorded on this path fails above; that error must not
   // surface as the next launch's hipGetLastError()
   (void)hipGetLastError();
-  if (!host_tr) {
-    const uint32_t* err_h = h_status + 8 * ncols;
-    check_guards(sharded ? err_h + 8 : err_h, nguard);
-    // z fell outside the DEEP polynomial's domain (probability ~n/p): the
-    // proof is recomputed with the host's transcript (per-point DEEP)
-    // (test hook SEZKP_DEBUG_FS_RARE=1: take that path on every proof)
-    const char* force_rare = getenv("SEZKP_DEBUG_FS_RARE");
-    if (err_h[1] || (force_rare && atoi(force_rare) != 0)) return 0;
-    for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], h_status + 8 * c, 32);
-    host_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - t_enter).count();
-    host_ms[1] = t_sync;
-    host_ms[2] = t_last;
-    host_ms[3] = 0;
-    return hdr_bytes + PL.total;
-  }
-
   // ---- host-known parts of the body: counts, query headers, FRI roots,
   // positions, final value (prover.rs:242-243), manifest root
   const auto t_ser = clk::now();
@@ -1944,7 +1687,6 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_cols, hipEventDisableTiming));
-    HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_deep, hipEventDisableTiming));
     c->tw = tables_for_device(device);
     // SEZKP_FORCE_SHARDED=1 runs the sharded algorithm (and its RCCL calls)
     // with a one-rank communicator: tests it on a single GPU
@@ -2171,7 +1913,7 @@ int32_t sezkp_ctx_stage_times(const sezkp_ctx* ctx, double* out_ms, int32_t max)
   int cnt = 0;
   for (int s = 0; s <= ST_NSTAGE && cnt < max; s++) out_ms[cnt++] = ctx->stage_ms[s];
   for (int s = 0; s < 4 && cnt < max; s++) out_ms[cnt++] = ctx->host_ms[s];
-  for (int s = 0; s < 4 && cnt < max; s++) out_ms[cnt++] = ctx->kernel_ms[s];
+  if (cnt < max) out_ms[cnt++] = ctx->kernel_ms;
   return cnt;
 }
 void* sezkp_ctx_stream(const sezkp_ctx* ctx) { return ctx ? (void*)ctx->st : nullptr; }
@@ -2373,58 +2115,18 @@ int32_t sezkp_fri_fold(const uint64_t* in, uint64_t n_out, uint64_t beta, uint64
 
 int32_t sezkp_fs_xof(const uint8_t* stream_bytes, size_t stream_len, const uint32_t* pos, const uint8_t* suffixes,
                      const uint32_t* sfx_len, const uint32_t* out_len, uint32_t nchal, uint8_t* out, void* stream) {
-  if (!nchal || nchal > (uint32_t)FS_MAX_CHAL || !pos || !sfx_len || !out_len || !out || (stream_len && !stream_bytes))
-    return SEZKP_E_INVALID;
-  std::vector<uint8_t> S(stream_bytes, stream_bytes + stream_len);
-  std::vector<FsChal> ch(nchal);
-  size_t sfx_total = 0, out_total = 0;
-  uint32_t pmax = 0;
+  (void)stream;  // ABI 3 signature; the transcript runs on the host since round 5
+  if (!nchal || !pos || !sfx_len || !out_len || !out || (stream_len && !stream_bytes)) return SEZKP_E_INVALID;
+  std::vector<uint8_t> msg;
   for (uint32_t i = 0; i < nchal; i++) {
-    if (pos[i] > stream_len || out_len[i] % 8 || !out_len[i] || sfx_len[i] > 1024) return SEZKP_E_INVALID;
-    ch[i] = FsChal{pos[i], 0, sfx_len[i], out_len[i], (uint32_t)out_total};
-    sfx_total += sfx_len[i];
-    out_total += out_len[i];
-    pmax = std::max(pmax, pos[i]);
-  }
-  if (stream_len + sfx_total > (size_t)FS_S_MAX - 16 || (sfx_total && !suffixes)) return SEZKP_E_INVALID;
-  for (uint32_t i = 0; i < nchal; i++) {
-    ch[i].sfx_off = (uint32_t)S.size();
-    S.insert(S.end(), suffixes, suffixes + sfx_len[i]);
+    if (pos[i] > stream_len || (sfx_len[i] && !suffixes)) return SEZKP_E_INVALID;
+    msg.assign(stream_bytes, stream_bytes + pos[i]);
+    msg.insert(msg.end(), suffixes, suffixes + sfx_len[i]);
     suffixes += sfx_len[i];
+    sezkp_blake3(msg.data(), msg.size(), out, out_len[i]);
+    out += out_len[i];
   }
-  const size_t sb = (S.size() + 15) & ~(size_t)15;
-  S.resize(sb + 16, 0);
-  hipStream_t st = (hipStream_t)stream;
-  void *dS = nullptr, *dcv = nullptr, *dcc = nullptr, *dout = nullptr, *dch = nullptr;
-  int32_t rc = SEZKP_OK;
-  const size_t nblk = sb / 64 + 2, nck = sb / 1024 + 2;
-  if (hipMalloc(&dS, S.size()) != hipSuccess || hipMalloc(&dcv, nblk * 32) != hipSuccess ||
-      hipMalloc(&dcc, nck * 32) != hipSuccess || hipMalloc(&dout, out_total) != hipSuccess ||
-      hipMalloc(&dch, nchal * sizeof(FsChal)) != hipSuccess) {
-    rc = SEZKP_E_DEVICE;
-  } else if (hipMemcpyAsync(dS, S.data(), S.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
-             hipMemcpyAsync(dch, ch.data(), nchal * sizeof(FsChal), hipMemcpyHostToDevice, st) != hipSuccess) {
-    rc = SEZKP_E_DEVICE;
-  } else {
-    FsArgs a{};
-    a.S = (const uint8_t*)dS;
-    a.s_bytes = (uint32_t)sb;
-    a.B0 = 0;
-    a.B1 = pmax / 64;
-    a.cvs = (uint32_t*)dcv;
-    a.ccv = (uint32_t*)dcc;
-    a.chal = (const FsChal*)dch;
-    a.nchal = nchal;
-    a.out = (uint8_t*)dout;
-    a.point = 0;
-    if (launch_fs_point(st, a) != hipSuccess ||
-        hipMemcpyAsync(out, dout, out_total, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      rc = SEZKP_E_DEVICE;
-  }
-  for (void* p : {dS, dcv, dcc, dout, dch})
-    if (p) (void)hipFree(p);
-  return rc;
+  return SEZKP_OK;
 }
 
 int32_t sezkp_blake3_leaves_u64(const uint64_t* vals, uint64_t n, uint8_t* leaves32, void* stream) {

@@ -237,75 +237,15 @@ struct ProofLayout {
 
 // ------------------------------------------------- Fiat-Shamir challenges
 // The transcript-derived values every challenge-dependent kernel reads from
-// device memory: written by the device transcript (transcript.hip) or, in the
-// host-transcript mode, copied from the host.
-constexpr int FS_NQ = 30;           // NUM_QUERIES (params.rs:31)
+// device memory, written by the host transcript (one H2D copy per point).
 constexpr int FS_MAX_BETAS = 64;
 struct DevChal {
   uint64_t alpha[8];                // derive_alphas (params.rs:82-92); reuse of prover.rs:86-98 in the kernels
   uint64_t mask[4];                 // derive_mask_coeffs (masking.rs:56-79)
   uint64_t z, zn, K1, K2, rho, rho4096;  // OOD point (nudged) and the DEEP-polynomial constants
-  uint64_t K3;                      // z^(n-1) / n: f(z) K3' = K3 S (DeepPoly, the q correction)
+  uint64_t K3;                      // z^(n-1) / n: kappa = K3 S (DeepPoly, the q correction)
   uint64_t beta[FS_MAX_BETAS];      // derive_betas_for_fri (params.rs:109-119)
-  uint64_t rows[FS_NQ], frows[FS_NQ];    // derive_queries mod n / mod N (prover.rs:248, 297)
-  uint32_t counts[2];               // FRI path / opening requests this rank owns
-  uint32_t pad[2];
-  uint64_t fs_t[3][6];              // device transcript: s_memrealtime at each kernel phase (SEZKP_HOST_TRACE prints)
 };
-
-// Device transcript (transcript.hip): the stream S (template from the host,
-// roots filled in on the device), the chaining values of its blocks and
-// chunks, and one workgroup per transcript point.
-constexpr int FS_S_MAX = 40960;     // stream + suffix bytes held in LDS
-constexpr int FS_MAX_CHAL = 16;     // challenges per point
-constexpr uint32_t FS_SRC_MROOT = 0, FS_SRC_COL = 1, FS_SRC_FRI = 0x10000;
-struct FsChal {
-  uint32_t pos;      // stream bytes before the challenge
-  uint32_t sfx_off;  // its suffix "challenge" || u32 len || label, at S[sfx_off ..)
-  uint32_t sfx_len;
-  uint32_t out_len;
-  uint32_t out_off;  // into the output bytes
-};
-struct FsFill {
-  uint32_t s_off;  // 32 root bytes at S[s_off ..)
-  uint32_t src;    // FS_SRC_MROOT, FS_SRC_COL + column, FS_SRC_FRI + layer
-};
-struct FsQueryArgs {  // point 3: requests and proof-body fields
-  ProofLayout PL;
-  uint32_t* req;          // FRI requests (3 words) then opening requests at 3 * max_fri_req
-  uint64_t max_fri_req;
-  const uint32_t* dict_of;
-  const uint64_t* final_val;  // the last FRI layer
-  uint64_t ch_lo, ch_hi;
-  uint32_t tau, sharded, world, rank;
-  int rR;
-};
-struct FsArgs {
-  const uint8_t* S;
-  uint32_t s_bytes;        // template bytes (stream + suffix area)
-  uint32_t B0, B1;         // stream blocks this point chains
-  uint32_t* cvs;           // chaining value in front of block b (8 words each)
-  uint32_t* ccv;           // chunk chaining values
-  const FsFill* fills;
-  uint32_t nfill;
-  const FsChal* chal;
-  uint32_t nchal;
-  uint8_t* out;
-  uint32_t mroot[8];
-  const uint32_t* colroots;
-  const uint32_t* friroots;
-  int point;               // 0 raw outputs (KAT), 1 alphas/masks/z, 2 betas, 3 queries
-  DevChal* ch;
-  uint32_t* status;        // [1] <- 1: z off the DEEP-polynomial domain (host re-proves)
-  uint32_t out_alpha, out_beta, out_rowq;
-  int logn, logN, logP;
-  uint64_t inv3, threeN, inv_n, w_rank;
-  FsQueryArgs q;
-};
-hipError_t launch_fs_point(hipStream_t st, const FsArgs& a);
-// the DEEP-polynomial constants (DevChal z^n, K1, K2, rho, rho^4096, status)
-// from the z of point 1: one thread, meant for a side stream
-hipError_t launch_fs_deep(hipStream_t st, const FsArgs& a);
 
 // kernels launched by the host orchestrator (prover.cpp)
 // blocks [blk_lo, blk_lo + blk_cnt) only (a sharded rank's rows + one row of halo)

@@ -949,6 +949,27 @@ struct RawLeaves {
   }
 };
 
+// Binary-counter Merkle step: node x (index j of the lane's run) merges with
+// the pending left siblings s[L], s[L+1], ... while bit L of j is set, then
+// waits at its level (or is the root). Template recursion keeps every stack
+// index static: the stack stays in registers.
+template <int L, int D>
+__device__ __forceinline__ void counter_push(uint32_t (&s)[D > 0 ? D : 1][8], uint32_t (&x)[8], int j,
+                                             uint32_t (&h)[8]) {
+  if constexpr (L == D) {
+#pragma unroll
+    for (int w = 0; w < 8; w++) h[w] = x[w];
+  } else {
+    if ((j >> L) & 1) {
+      b3_parent(s[L], x, x);
+      counter_push<L + 1, D>(s, x, j, h);
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; w++) s[L][w] = x[w];
+    }
+  }
+}
+
 // Binary-counter Merkle reduction of 2^D consecutive nodes in a rolled loop:
 // the stack is indexed statically (merges unrolled per level, branch on the
 // uniform loop counter), so code size is D+1 compressions, not 2^(D+1).
@@ -958,23 +979,7 @@ __device__ __forceinline__ void lane_tree(const Prov& P, uint32_t (&h)[8]) {
   for (int j = 0; j < (1 << D); j++) {
     uint32_t x[8];
     P.get(j, x);
-    bool done = false;
-#pragma unroll
-    for (int l = 0; l < D; l++) {
-      if (!done) {
-        if ((j >> l) & 1) {
-          b3_parent(s[l], x, x);
-        } else {
-#pragma unroll
-          for (int w = 0; w < 8; w++) s[l][w] = x[w];
-          done = true;
-        }
-      }
-    }
-    if (!done) {
-#pragma unroll
-      for (int w = 0; w < 8; w++) h[w] = x[w];
-    }
+    counter_push<0, D>(s, x, j, h);
   }
 }
 // lane_tree with the gathers software-pipelined: while node j is merged, the
@@ -996,23 +1001,7 @@ __device__ __forceinline__ void lane_tree_pf(const Prov& P, uint32_t (&h)[8]) {
     for (int w = 0; w < 8; w++) x[w] = nx[w];
     if (j + 1 < N) P.node(k1, j + 1, nx);
     if (j + 2 < N) k1 = P.raw(j + 2);
-    bool done = false;
-#pragma unroll
-    for (int l = 0; l < D; l++) {
-      if (!done) {
-        if ((j >> l) & 1) {
-          b3_parent(s[l], x, x);
-        } else {
-#pragma unroll
-          for (int w = 0; w < 8; w++) s[l][w] = x[w];
-          done = true;
-        }
-      }
-    }
-    if (!done) {
-#pragma unroll
-      for (int w = 0; w < 8; w++) h[w] = x[w];
-    }
+    counter_push<0, D>(s, x, j, h);
   }
 }
 

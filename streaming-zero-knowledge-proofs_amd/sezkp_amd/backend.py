@@ -18,8 +18,8 @@ STAGES = ["expand", "col_commit", "col_outer", "compose", "intt", "lde_ntt", "de
           "layer0_upper", "fri_fold_trees", "col_openings", "fri_paths", "total",
           # host-side split of the same prove() call (wall clock)
           "host_wall", "host_sync_wait", "host_final_wait", "host_serialize",
-          # single launches (SEZKP_KERNEL_EVENTS=1; 0 when not recorded)
-          "k_forest16", "fs_point1", "fs_point2", "fs_point3"]
+          # the FRI forest launch (SEZKP_KERNEL_EVENTS=1; 0 when not recorded)
+          "k_forest16"]
 
 
 @dataclass

@@ -365,8 +365,8 @@ def test_stage_events_opt_in_same_bytes(gpu_ok, product, oracle, monkeypatch):
 def test_prove_headline_size_matches_openmp_oracle(gpu_ok, product, monkeypatch):
     """The bench workload itself: `sezkp-cli simulate --t 2097152 --b 512
     --tau 8` blocks (T = 2^21, N = 2^24). The GPU proof equals the OpenMP build
-    of the C oracle byte for byte, with the host transcript (default) and with
-    the device transcript; the oracle runs in a child process on 16 threads
+    of the C oracle byte for byte (twice on one context: a re-proof of a
+    resident trace); the oracle runs in a child process on 16 threads
     (~10 s), so the other tests keep the single-thread build."""
     import sys
     T = 1 << 21
@@ -380,7 +380,6 @@ def test_prove_headline_size_matches_openmp_oracle(gpu_ok, product, monkeypatch)
     ctx = product.ProverContext(0)
     ctx.upload(blocks)
     got = hashlib.sha256(ctx.prove(blocks.manifest_root()).proof_bytes).hexdigest()
-    monkeypatch.setenv("SEZKP_DEVICE_TRANSCRIPT", "1")
     got_dev = hashlib.sha256(ctx.prove(blocks.manifest_root()).proof_bytes).hexdigest()
     ctx.close()
     out, err = child.communicate(timeout=150)

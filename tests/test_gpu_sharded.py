@@ -79,18 +79,6 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
         assert all(c["bytes"] > 0 and c["ms"] >= 0 for c in calls["stats"])
 
 
-@pytest.mark.parametrize("world,T,b,tau,seed", [(2, 1 << 13, 512, 2, 42), (4, 1 << 14, 100, 3, 7)])
-def test_sharded_device_transcript_matches_oracle(gpu_ok, product, oracle, monkeypatch, world, T, b, tau, seed):
-    """The optional device transcript (SEZKP_DEVICE_TRANSCRIPT=1) in the
-    sharded prover: every rank derives the challenges and its own path and
-    opening requests on the device; rank 0 alone writes the body fields."""
-    monkeypatch.setenv("SEZKP_DEVICE_TRANSCRIPT", "1")  # inherited by the spawned ranks
-    blocks = product.synthetic_blocks(T, b, tau, seed)
-    want = hashlib.sha256(oracle.prove_v1(blocks, blocks.manifest_root())).hexdigest()
-    for rank, digest, repeat_ok, _ in _run(world, T, b, tau, seed):
-        assert digest == want and repeat_ok, f"rank {rank}: {digest}"
-
-
 def test_sharded_config5_size_p8_matches_openmp_oracle(gpu_ok, product):
     """BASELINE config 5's shape: T = 2^22 (N = 2^25), tau = 8, over P = 8
     ranks (here sharing one GPU through host collectives). Every rank returns
