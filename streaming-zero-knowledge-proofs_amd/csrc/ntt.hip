@@ -21,6 +21,7 @@
 
 #include "dev_common.h"
 #include "sezkp_internal.h"
+#include "compose.h"
 
 namespace sezkp {
 
@@ -1140,14 +1141,16 @@ __global__ void __launch_bounds__(256) k_bintt_dft_twiddle(uint64_t* __restrict_
 }
 
 // ------------------------------------------- DEEP quotient (base domain)
-// See DeepPoly (sezkp_internal.h). k_inv_base: C_j <- D_j = C_j / (w_n^j - z)
-// for the base points j in [row0, row0 + nrows) (16 per lane, one Montgomery
-// batch per 4096) and the per-WG partial sums of D_j w_n^j; WG b of the range
+// See DeepPoly (sezkp_internal.h). k_inv_base: D_j = C_j / (w_n^j - z) for the
+// base points j in [row0, row0 + nrows), C_j the composition value of the
+// row (compose.h, from k_compose_terms' sums: the composition's
+// transcript-dependent half runs here), DQ_PER per lane, one Montgomery batch
+// per WG, and the per-WG partial sums of D_j w_n^j; WG b of the range
 // writes partial[b] (sharded ranks each own a block of rows and allgather
 // their partials with the INTT coefficients, so every rank reduces the same sum).
-constexpr int DQ_PER = 16;
-__global__ void __launch_bounds__(NTT_THREADS) k_inv_base(uint64_t* __restrict__ C, uint64_t* __restrict__ partial,
-                                                          int logn,
+template <int DQ_PER>
+__global__ void __launch_bounds__(NTT_THREADS) k_inv_base(ComposeTerms Tm, uint64_t* __restrict__ Dout,
+                                                          uint64_t* __restrict__ partial, int logn,
                                                           const DevChal* __restrict__ ch, NttTables T, uint64_t row0,
                                                           uint64_t nrows) {
   const uint64_t z = ch->z;
@@ -1156,15 +1159,17 @@ __global__ void __launch_bounds__(NTT_THREADS) k_inv_base(uint64_t* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t i0 = row0 + ((uint64_t)blockIdx.x * NTT_THREADS + tid) * DQ_PER;
   const bool act = i0 < row0 + nrows;  // nrows % 16 == 0: a lane's points are all in or all out
-  uint64_t d[DQ_PER], a[DQ_PER];
+  uint64_t d[DQ_PER], a[DQ_PER], cv[DQ_PER];
   uint64_t Pp = 1;
   if (act) {
+    const ComposeCoef K = compose_coef(ch);
     const uint64_t e = i0 << (T.K - logn);
     uint64_t x = gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]);
     const uint64_t e1 = 1ULL << (T.K - logn);
     const uint64_t wn = gl_mul(T.hi[e1 >> T.S], T.lo[e1 & ((1ULL << T.S) - 1)]);
 #pragma unroll
     for (int j = 0; j < DQ_PER; j++) {
+      cv[j] = compose_value(Tm, K, i0 + j, x);  // C_j (air.rs:49-136 + mask)
       d[j] = gl_sub(x, z);
       Pp = j ? gl_mul(Pp, d[j]) : d[j];
       a[j] = Pp;
@@ -1204,8 +1209,8 @@ __global__ void __launch_bounds__(NTT_THREADS) k_inv_base(uint64_t* __restrict__
       const uint64_t ij = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
       if (j) inv_run = gl_mul(inv_run, d[j]);
       const uint64_t xj = gl_add(d[j], z);  // w_n^(i0 + j)
-      const uint64_t Dj = gl_mul(C[i0 + j], ij);
-      C[i0 + j] = Dj;
+      const uint64_t Dj = gl_mul(cv[j], ij);
+      Dout[i0 + j] = Dj;
       acc = gl_add(acc, gl_mul(Dj, xj));
     }
   }
@@ -1288,20 +1293,32 @@ __global__ void __launch_bounds__(NTT_THREADS) k_q_tables(const uint64_t* __rest
   for (uint64_t t = g0; t < nhk; t += gs) rhk[t] = gl_mul(kappa, gl_pow_dev(r4096, t));
 }
 
-hipError_t launch_inv_base(hipStream_t st, uint64_t* C, uint64_t* partial, int logn, const DevChal* ch,
-                           const NttTables& T, uint64_t row0, uint64_t nrows) {
-  const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
-  if (logn < 4 || nrows % DQ_PER || row0 % per || row0 + nrows > (1ULL << logn)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_inv_base, dim3((unsigned)((nrows + per - 1) / per)), dim3(NTT_THREADS), 0, st, C,
-                     partial + row0 / per, logn, ch, T, row0, nrows);
+uint64_t dq_rows_per_part(uint64_t nrows) {
+  // 8 rows per lane (the composition values of the lane stay in registers:
+  // 16 took 158 VGPRs); 4 when that leaves fewer than 512 workgroups (a
+  // sharded rank's block: its batch inversions then run twice as parallel)
+  return (uint64_t)NTT_THREADS * (nrows >= 512ull * NTT_THREADS * 8 ? 8 : 4);
+}
+
+hipError_t launch_inv_base(hipStream_t st, const ComposeTerms& Tm, uint64_t* D, uint64_t* partial, int logn,
+                           const DevChal* ch, const NttTables& T, uint64_t row0, uint64_t nrows, uint64_t per) {
+  if (logn < 4 || (per != 8 * NTT_THREADS && per != 4 * NTT_THREADS) || nrows % 16 || row0 % per ||
+      row0 + nrows > (1ULL << logn))
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((nrows + per - 1) / per));
+  if (per == 8 * NTT_THREADS)
+    hipLaunchKernelGGL(k_inv_base<8>, grid, dim3(NTT_THREADS), 0, st, Tm, D, partial + row0 / per, logn, ch, T, row0,
+                       nrows);
+  else
+    hipLaunchKernelGGL(k_inv_base<4>, grid, dim3(NTT_THREADS), 0, st, Tm, D, partial + row0 / per, logn, ch, T, row0,
+                       nrows);
   return hipGetLastError();
 }
 
 hipError_t launch_q_tables(hipStream_t st, const uint64_t* partial, int logn, int logN, const DevChal* ch,
-                           uint64_t* rlo, uint64_t* rhi, uint64_t* rhk) {
-  if (logn < 4 || logN < logn || logN > 32) return hipErrorInvalidValue;
+                           uint64_t* rlo, uint64_t* rhi, uint64_t* rhk, uint64_t per) {
+  if (logn < 4 || logN < logn || logN > 32 || !per) return hipErrorInvalidValue;
   const uint64_t n = 1ULL << logn;
-  const uint64_t per = (uint64_t)NTT_THREADS * DQ_PER;
   const uint32_t nparts = (uint32_t)((n + per - 1) / per);
   const uint32_t nhi = logN > 12 ? (1u << (logN - 12)) : 1u;
   const uint32_t nhk = logn > 12 ? (1u << (logn - 12)) : 1u;

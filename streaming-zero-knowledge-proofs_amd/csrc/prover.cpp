@@ -221,6 +221,7 @@ struct sezkp_ctx {
   uint64_t outer_stride = 0;
   uint32_t* d_colroots = nullptr;
   uint64_t* d_base = nullptr;
+  ComposeTerms Tm{};  // per-row composition sums (k_compose_terms, side stream)
   uint64_t *d_dq_part = nullptr, *d_dq_rlo = nullptr, *d_dq_rhi = nullptr, *d_dq_rhk = nullptr;  // DeepPoly
   uint64_t* d_lde = nullptr;
   uint64_t* d_fri = nullptr;
@@ -697,9 +698,18 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   const int k = logN;
   const uint64_t S = 1ULL << L16_LOG;
   d_base = dalloc<uint64_t>(n);
+  Tm.hr = dalloc<uint64_t>(n);
+  Tm.sl = dalloc<uint64_t>(n);
+  Tm.c3 = dalloc<int64_t>(n);
+  Tm.c2 = dalloc<int32_t>(n + 2);
+  Tm.sy = dalloc<int32_t>(n + 2);
+  Tm.bf = dalloc<uint64_t>((size_t)nblk + 1);
+  Tm.bl = dalloc<uint64_t>((size_t)nblk + 1);
+  Tm.row_flags = T.row_flags;
+  Tm.row_blk = T.row_blk;
   {  // DEEP quotient tables (sized for this rank's M = N / P LDE points)
     const uint64_t Ml = N >> logP;
-    d_dq_part = dalloc<uint64_t>(n / 4096 + 1);
+    d_dq_part = dalloc<uint64_t>(n / 1024 + 1);  // partials of >= 1024 rows (dq_rows_per_part)
     d_dq_rlo = dalloc<uint64_t>(4096);
     d_dq_rhi = dalloc<uint64_t>(Ml > 4096 ? Ml >> 12 : 1);
     d_dq_rhk = dalloc<uint64_t>(n > 4096 ? n >> 12 : 1);
@@ -1145,6 +1155,10 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
   ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
                           outer_stride, d_err), "col_commit_pw");
+  // the composition's transcript-independent half (the row sums), also
+  // beside the dictionary commitments: only its combine with the alphas is
+  // left after the transcript's first round trip
+  ok(launch_compose_terms(st2, T, Tm, row_lo, row_hi - row_lo), "compose_terms");
   HIP_OR_THROW(hipEventRecord(ev_cols, st2));
   ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
                         row_hi - row_lo, d_dlev),
@@ -1247,16 +1261,18 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
   mark("compose_issued");
   const bool dq = logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY");
-  // sharded: each rank turns its own rows into q(w^j) (the partial sums of
-  // f(z) are allgathered in between), then the q values are allgathered for
-  // the n-point INTT every rank's coset needs; without the quotient the
-  // composition values are allgathered as they are
-  // sharded INTT over the ranks (block rows in, all n coefficients out): one
+  // sharded: each rank turns its own rows into D_j (DeepPoly) and one
+  // allgather (with the partial sums of f(z)) gives every rank the n values
+  // for the n-point INTT its coset needs; without the quotient the
+  // composition values are allgathered as they are. SEZKP_DIST_INTT=1 runs
+  // the distributed INTT instead (block rows in, all n coefficients out: one
   // all-to-all, P-point DFTs + twiddle, one all-to-all, a local (n/P)-point
-  // INTT, then the allgather every rank's coset needs anyway. Rank g's rows
-  // are [g n/P, (g+1) n/P) (n >= 4096 P). SEZKP_REPLICATED_INTT=1 gathers the
-  // n values and runs the n-point INTT on every rank instead.
-  const bool dist_intt = sharded && world > 1 && !getenv("SEZKP_REPLICATED_INTT");
+  // INTT, then the allgather every rank's coset needs anyway; rank g's rows
+  // are [g n/P, (g+1) n/P), n >= 4096 P). Round 5's per-rank cost model
+  // prefers the replicated INTT at every P (profiles/r05/intt_ab.txt: two
+  // collectives fewer outweigh (P - 1)/P of a 2^21-point INTT; P = 8 1.204
+  // -> 1.132 ms predicted), so it is the default.
+  const bool dist_intt = sharded && world > 1 && getenv("SEZKP_DIST_INTT") && atoi(getenv("SEZKP_DIST_INTT")) != 0;
   DeepPoly dpoly{d_dq_rlo, d_dq_rhi, d_dq_rhk};
   if (dq) {
     const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
@@ -1284,17 +1300,19 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   }
   // alphas, masks and the DEEP constants for the kernels below
   HIP_OR_THROW(hipMemcpyAsync(d_chal, h_chal, offsetof(DevChal, beta), hipMemcpyHostToDevice, st));
-  ok(launch_compose(st, T, d_chal, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
-  if (sharded && !dq && !dist_intt)
-    coll("base_values", P1 * (row_hi - row_lo) * 8,
-         [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
-  rec(4);
-  const uint64_t dq_per = 4096;  // base rows per partial sum (k_inv_base WG)
+  const uint64_t dq_per = dq_rows_per_part(row_hi - row_lo);  // base rows per partial sum (k_inv_base WG)
   if (dq) {
-    // D_j = C_j / (w^j - z) in place + the partial sums of f(z): z only
-    // (DeepPoly); the INTT runs on D, f(z) is needed by the tables only
-    ok(launch_inv_base(st, d_base, d_dq_part, logn, d_chal, tw, row_lo, row_hi - row_lo), "inv_base");
+    // the composition's combine (alphas, mask) fused with the DEEP quotient:
+    // D_j = C_j / (w^j - z) and the partial sums of f(z) (DeepPoly); the
+    // INTT runs on D, f(z) is needed by the tables only
+    ok(launch_inv_base(st, Tm, d_base, d_dq_part, logn, d_chal, tw, row_lo, row_hi - row_lo, dq_per), "inv_base");
+  } else {
+    ok(launch_compose_combine(st, Tm, d_chal, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
+    if (sharded && !dist_intt)
+      coll("base_values", P1 * (row_hi - row_lo) * 8,
+           [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
   }
+  rec(4);
   // sharded: this rank's partial sums of f(z) travel with the INTT exchange
   // that gathers every rank's values (one collective)
   auto gather_fz = [&](uint64_t nrows) {
@@ -1328,7 +1346,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
   }
   if (dq)
-    ok(launch_q_tables(st, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk), "q_tables");
+    ok(launch_q_tables(st, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk, dq_per), "q_tables");
   rec(5);
   // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on
   // 3 w_N^g <w_M> (M = N/P), no communication

@@ -9,7 +9,8 @@
 
 namespace sezkp {
 
-struct DevChal;  // transcript-derived values in device memory (below)
+struct DevChal;        // transcript-derived values in device memory (below)
+struct ComposeTerms;   // per-row composition sums (below)
 
 // w_{2^K}^e = hi[e >> S] * lo[e & (2^S - 1)]; p3_* likewise for 3^e.
 struct NttTables {
@@ -76,16 +77,19 @@ struct DeepPoly {
   const uint64_t* rhi;  // N >> 12 entries: c' r^(4096 t)
   const uint64_t* rhk;  // max(1, n >> 12) entries: kappa r^(4096 t)
 };
-// over a block of base rows [row0, row0 + nrows) (row0 a multiple of 4096):
-// C_j <- D_j = C_j / (w^j - z) in place (one Montgomery batch inversion per
-// 4096) and this block's partial sums of C_j w^j / (w^j - z) at
-// partial[row0 / 4096 ...] (z from ch)
-hipError_t launch_inv_base(hipStream_t st, uint64_t* C, uint64_t* partial, int logn, const DevChal* ch,
-                           const NttTables& T, uint64_t row0, uint64_t nrows);
+// over a block of base rows [row0, row0 + nrows) (row0 a multiple of per):
+// D_j = C_j / (w^j - z) into D, C_j = compose_value of the row's terms (one
+// Montgomery batch inversion per `per` rows), and this block's partial sums
+// of C_j w^j / (w^j - z) at partial[row0 / per ...] (z, alphas, mask from ch)
+// (partials of `per` rows each: dq_rows_per_part of the block's row count,
+// the same on every rank)
+uint64_t dq_rows_per_part(uint64_t nrows);
+hipError_t launch_inv_base(hipStream_t st, const ComposeTerms& Tm, uint64_t* D, uint64_t* partial, int logn,
+                           const DevChal* ch, const NttTables& T, uint64_t row0, uint64_t nrows, uint64_t per);
 // once every partial of the n rows is in `partial`: f(z) = K1 S, the DeepPoly
 // tables rlo / rhi / rhk (K1, K2, K3, rho, rho^4096 from ch)
 hipError_t launch_q_tables(hipStream_t st, const uint64_t* partial, int logn, int logN, const DevChal* ch,
-                           uint64_t* rlo, uint64_t* rhi, uint64_t* rhk);
+                           uint64_t* rlo, uint64_t* rhi, uint64_t* rhk, uint64_t per);
 
 hipError_t ntt_dif(hipStream_t st, uint64_t* a, int logN, bool inverse, const NttTables& T);
 // natural order in and out through `scratch` (n words): the first pass reads a
@@ -146,6 +150,22 @@ struct TraceDev {
   uint8_t* row_flags;         // [n]   bit0 first, bit1 last (derived)
   int32_t* head;              // [tau][n] post-move head (derived; block-local; k_expand rejects |head| >= 2^31)
   int64_t* head_rng;          // [tau][nblk][2] per-block min / max of head (derived by k_expand)
+};
+
+// Per-row constraint sums of the composition (k_compose_terms): everything
+// of C(i) that does not depend on the transcript, summed over the tapes
+// exactly (integers where they are small, canonical field values otherwise).
+// Rows [row0, row_end) of this device; the boundary sums once per block.
+struct ComposeTerms {
+  uint64_t* hr;               // [n] sum of head - (head & 0xFFFF) over written tapes
+  uint64_t* sl;               // [n] sum of slack - (slack & 0xFFFF) over written tapes
+  int64_t* c3;                // [n] head-update sum (1 - is_last) (head' - head - mv')
+  int32_t* c2;                // [n] mv domain sum mv^3 - mv
+  int32_t* sy;                // [n] symbol sum sym & ~0xF over written tapes
+  uint64_t* bf;               // [nblk] boundary_first sum of the block's first row
+  uint64_t* bl;               // [nblk] boundary_last sum of the block's last row
+  const uint8_t* row_flags;   // = TraceDev::row_flags
+  const uint32_t* row_blk;    // = TraceDev::row_blk
 };
 
 // guard word bits (d_err): a kernel saw input it cannot represent
@@ -266,10 +286,13 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
 hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);
-// rows [row0, row0 + nrows) (nrows = n for the whole trace)
-// alphas and mask coefficients from ch (device memory)
-hipError_t launch_compose(hipStream_t st, const TraceDev& T, const DevChal* ch, const NttTables& tw, int logn,
-                          uint64_t* out, uint64_t row0, uint64_t nrows);
+// composition, rows [row0, row0 + nrows) (nrows = n for the whole trace):
+// the transcript-independent row sums (ComposeTerms), then C(i) from them
+// with the alphas and mask coefficients of ch (device memory)
+hipError_t launch_compose_terms(hipStream_t st, const TraceDev& T, const ComposeTerms& Tm, uint64_t row0,
+                                uint64_t nrows);
+hipError_t launch_compose_combine(hipStream_t st, const ComposeTerms& Tm, const DevChal* ch, const NttTables& tw,
+                                  int logn, uint64_t* out, uint64_t row0, uint64_t nrows);
 // DEEP divide of y[j] at x = shift * w_{2^logN}^(g + (j << logP)) (logP = 0, g = 0: natural layout)
 hipError_t launch_deep(hipStream_t st, uint64_t* y, int logN, uint64_t z, const NttTables& tw, int logP = 0,
                        uint32_t g = 0, uint64_t shift = 3);

@@ -16,6 +16,7 @@
 #include "dev_common.h"
 #include "col_leaf.h"
 #include "sezkp_internal.h"
+#include "compose.h"
 
 namespace sezkp {
 
@@ -556,125 +557,45 @@ __global__ void __launch_bounds__(PW_THREADS) k_col_commit_pw(TraceDev T, const 
 }
 
 // ------------------------------------------------------------ composition
-// C(i) per air.rs:49-136. Exact simplifications (flags are 0/1 by
-// construction, bit columns are boolean): every alpha*flag*(flag-1) and
+// C(i) per air.rs:49-136 in two steps. Exact simplifications (flags are 0/1
+// by construction, bit columns are boolean): every alpha*flag*(flag-1) and
 // alpha*flg*sum(b(b-1)) term is identically zero and is skipped; the bit
-// reconstructions equal x & 0xFFFF / x & 0xF of the canonical value.
-// the alphas with the reuse of prover.rs:86-98 and the mask coefficients,
-// from the transcript's device record
-__device__ __forceinline__ Alphas alphas_of(const DevChal* ch) {
-  const uint64_t* a = ch->alpha;
-  return Alphas{a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[0], a[2], a[2]};
-}
-__global__ void __launch_bounds__(TR_THREADS) k_compose(TraceDev T, const DevChal* __restrict__ ch, NttTables tw,
-                                                        int logn, uint64_t* __restrict__ out, uint64_t row0,
-                                                        uint64_t row_end) {
-  const uint64_t n = T.n;
-  const Alphas A = alphas_of(ch);
-  const uint64_t m0 = ch->mask[0], m1 = ch->mask[1], m2 = ch->mask[2], m3 = ch->mask[3];
-  // one row per lane: each load instruction covers 64 consecutive rows
-  // (coalesced), row i+1 shares the neighbour's cache line; many rows in
-  // flight per CU hide the dependent loads of the tape loop
-  const uint64_t i = row0 + (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
-  if (i >= row_end) return;
-  const uint64_t e0 = i << (tw.K - logn);
-  const uint64_t x = gl_mul(tw.hi[e0 >> tw.S], tw.lo[e0 & ((1ULL << tw.S) - 1)]);  // w_n^i
-  {
-    const uint64_t ip1 = (i + 1) & (n - 1);
-    const uint8_t fl = T.row_flags[i];
-    const bool is_first = fl & 1, is_last = (fl >> 1) & 1;
-    const uint32_t blk = T.row_blk[i];
-    // Each constraint type shares one alpha across tapes (air.rs:49-136), so
-    // its per-tape terms are summed first (exactly, as integers where they are
-    // small) and multiplied once: sum_r a*t_r = a * sum_r t_r in the field.
-    int32_t s_c2 = 0, s_sy = 0;
-    int64_t s_c3 = 0;
-    uint64_t s_bf = 0, s_bl = 0;
-    // x - (x & 0xFFFF) = x & ~0xFFFF for canonical x: the head / slack terms
-    // are summed as exact integers (< 2^67, lo + carry count), reduced once
-    uint64_t hr_lo = 0, sl_lo = 0;
-    uint32_t hr_hi = 0, sl_hi = 0;
-#pragma unroll 4
-    for (int r = 0; r < T.tau; r++) {
-      const uint64_t o = (uint64_t)r * n;
-      const int32_t mv = T.mv[o + i];
-      const int64_t head = T.head[o + i];
-      const uint64_t head_f = gl_from_i64(head);
-      // C2: mv(mv-1)(mv+1) = mv^3 - mv  (|mv| <= 128: exact in i32, 8 tapes)
-      s_c2 += mv * mv * mv - mv;
-      // C3: (1 - is_last) * (head' - head - mv'), |head| <= 128 n
-      if (!is_last) s_c3 += T.head[o + ip1] - head - (int64_t)T.mv[o + ip1];
-      if (T.wflag[o + i]) {
-        uint32_t c;
-        // head - sum(head_bits * 2^k)
-        hr_lo = add64c(hr_lo, head_f & ~0xFFFFULL, c);
-        hr_hi += c;
-        // slack = (win_len - 1) - head, reconstructed from 16 bits
-        const uint64_t winlen = T.blk_winlen[(uint64_t)r * T.nblk + blk];
-        const uint64_t slack = gl_sub(gl_sub(winlen, 1), head_f);
-        sl_lo = add64c(sl_lo, slack & ~0xFFFFULL, c);
-        sl_hi += c;
-        // symbol 4-bit decomposition
-        const int32_t sym = T.wsym[o + i];
-        s_sy += sym & ~0xF;
-      }
-      if (is_first) {
-        const uint64_t offin = T.blk_offin[(uint64_t)r * T.nblk + blk];
-        s_bf = gl_add(s_bf, gl_sub(gl_sub(head_f, gl_from_i64(mv)), offin));
-      }
-      if (is_last) {
-        const uint64_t offout = T.blk_offout[(uint64_t)r * T.nblk + blk];
-        s_bl = gl_add(s_bl, gl_sub(head_f, offout));
-      }
-    }
-    const uint64_t s_hr = gl_reduce128(hr_lo, hr_hi), s_sl = gl_reduce128(sl_lo, sl_hi);
-    uint64_t acc = 0;
-    if (s_c2) acc = gl_mul(A.mv_domain, gl_from_i64(s_c2));
-    if (s_c3) acc = gl_add(acc, gl_mul(A.head_update, gl_from_i64(s_c3)));
-    if (s_hr) acc = gl_add(acc, gl_mul(A.head_reconstruct, s_hr));
-    if (s_sl) acc = gl_add(acc, gl_mul(A.slack_reconstruct, s_sl));
-    if (s_sy) acc = gl_add(acc, gl_mul(A.sym_reconstruct, (uint64_t)s_sy));
-    if (is_first) acc = gl_add(acc, gl_mul(A.boundary_first, s_bf));
-    if (is_last) acc = gl_add(acc, gl_mul(A.boundary_last, s_bl));
-    // mask R(x) = m0 + m1 x + m2 x^2 + m3 x^3 (Horner)
-    uint64_t R = gl_add(gl_mul(gl_add(gl_mul(gl_add(gl_mul(m3, x), m2), x), m1), x), m0);
-    out[i] = gl_add(acc, R);
-  }
-}
-
-// RW adjacent rows per lane (RW = 2 or 4; the same terms as k_compose): the
-// lane's mv / wflag / wsym / head cells of one tape are single 2-8 / 2-8 /
-// 4-8 / 16-32-byte loads, the next row of all but the last comes from the
-// group itself, and the outputs are 16-byte stores. Needs row0 and the row
-// count to be multiples of RW (n >= RW).
+// reconstructions equal x & 0xFFFF / x & 0xF of the canonical value. Each
+// constraint type shares one alpha across tapes, so its per-tape terms are
+// summed first (exactly, as integers where they are small) and multiplied
+// once: sum_r a*t_r = a * sum_r t_r in the field.
+// k_compose_terms needs only the trace: it runs on the side stream beside
+// the column commitments, before the transcript has the alphas, and stores
+// the row sums (ComposeTerms); compose_value (compose.h) combines them with
+// the alphas and the mask in k_inv_base (fused with the DEEP quotient) or
+// k_compose_combine. RW adjacent rows per lane (1, 2 or 4): the lane's mv /
+// wflag / wsym / head cells of one tape are single loads, the next row of all
+// but the last comes from the group itself. Needs row0 and the row count to
+// be multiples of RW (n >= RW).
 template <int RW>
-__global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, const DevChal* __restrict__ ch, NttTables tw,
-                                                             int logn, uint64_t* __restrict__ out, uint64_t row0,
-                                                             uint64_t row_end) {
-  const Alphas A = alphas_of(ch);
-  const uint64_t m0 = ch->mask[0], m1 = ch->mask[1], m2 = ch->mask[2], m3 = ch->mask[3];
-  static_assert(RW == 2 || RW == 4, "2 or 4 rows per lane");
-  using Narrow = typename std::conditional<RW == 2, uint16_t, uint32_t>::type;  // RW bytes
-  using Wide = typename std::conditional<RW == 2, uint32_t, uint64_t>::type;    // RW u16
+__global__ void __launch_bounds__(TR_THREADS) k_compose_terms(TraceDev T, ComposeTerms Tm, uint64_t row0,
+                                                              uint64_t row_end) {
+  static_assert(RW == 1 || RW == 2 || RW == 4, "1, 2 or 4 rows per lane");
+  using Narrow = typename std::conditional<RW == 1, uint8_t,
+                                           typename std::conditional<RW == 2, uint16_t, uint32_t>::type>::type;
+  using Wide = typename std::conditional<RW == 1, uint16_t,
+                                         typename std::conditional<RW == 2, uint32_t, uint64_t>::type>::type;
   const uint64_t n = T.n;
   const uint64_t i = row0 + RW * ((uint64_t)blockIdx.x * TR_THREADS + threadIdx.x);
   if (i >= row_end) return;
-  const uint64_t mask_s = (1ULL << tw.S) - 1;
-  const uint64_t e0 = i << (tw.K - logn), e1 = 1ULL << (tw.K - logn);
-  const uint64_t w = gl_mul(tw.hi[e1 >> tw.S], tw.lo[e1 & mask_s]);  // w_n
-  uint64_t x[RW];
-  x[0] = gl_mul(tw.hi[e0 >> tw.S], tw.lo[e0 & mask_s]);  // w_n^i
-#pragma unroll
-  for (int j = 1; j < RW; j++) x[j] = gl_mul(x[j - 1], w);
   const uint64_t inx = (i + RW) & (n - 1);
   const Narrow flw = *reinterpret_cast<const Narrow*>(T.row_flags + i);
   uint32_t blk[RW];
   bool is_first[RW], is_last[RW];
+  if constexpr (RW == 1) {
+    blk[0] = T.row_blk[i];
+  } else {
 #pragma unroll
-  for (int j = 0; j < RW; j += 2) {
-    const uint2 b2 = *reinterpret_cast<const uint2*>(T.row_blk + i + j);
-    blk[j] = b2.x;
-    blk[j + 1] = b2.y;
+    for (int j = 0; j < RW; j += 2) {
+      const uint2 b2 = *reinterpret_cast<const uint2*>(T.row_blk + i + j);
+      blk[j] = b2.x;
+      blk[j + 1] = b2.y;
+    }
   }
 #pragma unroll
   for (int j = 0; j < RW; j++) {
@@ -698,11 +619,15 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, const D
     const Narrow wfw = *reinterpret_cast<const Narrow*>(T.wflag + o + i);
     const Wide wsw = *reinterpret_cast<const Wide*>(T.wsym + o + i);
     int64_t head[RW + 1];
+    if constexpr (RW == 1) {
+      head[0] = T.head[o + i];
+    } else {
 #pragma unroll
-    for (int j = 0; j < RW; j += 2) {
-      const int2 h2 = *reinterpret_cast<const int2*>(T.head + o + i + j);
-      head[j] = h2.x;
-      head[j + 1] = h2.y;
+      for (int j = 0; j < RW; j += 2) {
+        const int2 h2 = *reinterpret_cast<const int2*>(T.head + o + i + j);
+        head[j] = h2.x;
+        head[j + 1] = h2.y;
+      }
     }
     head[RW] = T.head[o + inx];
     int32_t mv[RW + 1];
@@ -712,16 +637,21 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, const D
 #pragma unroll
     for (int j = 0; j < RW; j++) {
       const uint64_t head_f = gl_from_i64(head[j]);
+      // C2: mv(mv-1)(mv+1) = mv^3 - mv  (|mv| <= 128: exact in i32, 8 tapes)
       s_c2[j] += mv[j] * mv[j] * mv[j] - mv[j];
+      // C3: (1 - is_last) * (head' - head - mv'), |head| <= 128 n
       if (!is_last[j]) s_c3[j] += head[j + 1] - head[j] - (int64_t)mv[j + 1];
       if ((wfw >> (8 * j)) & 0xFF) {
         uint32_t c;
+        // head - sum(head_bits * 2^k)
         hr_lo[j] = add64c(hr_lo[j], head_f & ~0xFFFFULL, c);
         hr_hi[j] += c;
+        // slack = (win_len - 1) - head, reconstructed from 16 bits
         const uint64_t winlen = T.blk_winlen[(uint64_t)r * T.nblk + blk[j]];
         const uint64_t slack = gl_sub(gl_sub(winlen, 1), head_f);
         sl_lo[j] = add64c(sl_lo[j], slack & ~0xFFFFULL, c);
         sl_hi[j] += c;
+        // symbol 4-bit decomposition
         const int32_t sym = (int32_t)((wsw >> (16 * j)) & 0xFFFF);
         s_sy[j] += sym & ~0xF;
       }
@@ -735,23 +665,43 @@ __global__ void __launch_bounds__(TR_THREADS) k_compose_rows(TraceDev T, const D
       }
     }
   }
-  uint64_t res[RW];
+  uint64_t hr[RW], sl[RW];
 #pragma unroll
   for (int j = 0; j < RW; j++) {
-    const uint64_t s_hr = gl_reduce128(hr_lo[j], hr_hi[j]), s_sl = gl_reduce128(sl_lo[j], sl_hi[j]);
-    uint64_t acc = 0;
-    if (s_c2[j]) acc = gl_mul(A.mv_domain, gl_from_i64(s_c2[j]));
-    if (s_c3[j]) acc = gl_add(acc, gl_mul(A.head_update, gl_from_i64(s_c3[j])));
-    if (s_hr) acc = gl_add(acc, gl_mul(A.head_reconstruct, s_hr));
-    if (s_sl) acc = gl_add(acc, gl_mul(A.slack_reconstruct, s_sl));
-    if (s_sy[j]) acc = gl_add(acc, gl_mul(A.sym_reconstruct, (uint64_t)s_sy[j]));
-    if (is_first[j]) acc = gl_add(acc, gl_mul(A.boundary_first, s_bf[j]));
-    if (is_last[j]) acc = gl_add(acc, gl_mul(A.boundary_last, s_bl[j]));
-    const uint64_t R = gl_add(gl_mul(gl_add(gl_mul(gl_add(gl_mul(m3, x[j]), m2), x[j]), m1), x[j]), m0);
-    res[j] = gl_add(acc, R);
+    hr[j] = gl_reduce128(hr_lo[j], hr_hi[j]);
+    sl[j] = gl_reduce128(sl_lo[j], sl_hi[j]);
+    if (is_first[j]) Tm.bf[blk[j]] = s_bf[j];
+    if (is_last[j]) Tm.bl[blk[j]] = s_bl[j];
   }
+  if constexpr (RW == 1) {
+    Tm.hr[i] = hr[0];
+    Tm.sl[i] = sl[0];
+    Tm.c3[i] = s_c3[0];
+    Tm.c2[i] = s_c2[0];
+    Tm.sy[i] = s_sy[0];
+  } else {
 #pragma unroll
-  for (int j = 0; j < RW; j += 2) *reinterpret_cast<ulonglong2*>(out + i + j) = make_ulonglong2(res[j], res[j + 1]);
+    for (int j = 0; j < RW; j += 2) {
+      *reinterpret_cast<ulonglong2*>(Tm.hr + i + j) = make_ulonglong2(hr[j], hr[j + 1]);
+      *reinterpret_cast<ulonglong2*>(Tm.sl + i + j) = make_ulonglong2(sl[j], sl[j + 1]);
+      *reinterpret_cast<longlong2*>(Tm.c3 + i + j) = make_longlong2(s_c3[j], s_c3[j + 1]);
+      *reinterpret_cast<int2*>(Tm.c2 + i + j) = make_int2(s_c2[j], s_c2[j + 1]);
+      *reinterpret_cast<int2*>(Tm.sy + i + j) = make_int2(s_sy[j], s_sy[j + 1]);
+    }
+  }
+}
+
+// C(i) for rows [row0, row_end) from the terms (the path without the DEEP
+// quotient: per-point DEEP, or fewer than 16 rows)
+__global__ void __launch_bounds__(TR_THREADS) k_compose_combine(ComposeTerms Tm, const DevChal* __restrict__ ch,
+                                                                NttTables tw, int logn, uint64_t* __restrict__ out,
+                                                                uint64_t row0, uint64_t row_end) {
+  const uint64_t i = row0 + (uint64_t)blockIdx.x * TR_THREADS + threadIdx.x;
+  if (i >= row_end) return;
+  const ComposeCoef K = compose_coef(ch);
+  const uint64_t e0 = i << (tw.K - logn);
+  const uint64_t x = gl_mul(tw.hi[e0 >> tw.S], tw.lo[e0 & ((1ULL << tw.S) - 1)]);  // w_n^i
+  out[i] = compose_value(Tm, K, i, x);
 }
 
 // ------------------------------------------------ dictionary commitments
@@ -1685,22 +1635,29 @@ hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemp
                      T, d_tmpl, d_pw_cols, n_pw_cols, d_chunks, nchunks, tabs, outer_nodes, outer_stride_nodes, d_err);
   return hipGetLastError();
 }
-hipError_t launch_compose(hipStream_t st, const TraceDev& T, const DevChal* ch,
-                          const NttTables& tw, int logn, uint64_t* out, uint64_t row0, uint64_t nrows) {
+hipError_t launch_compose_terms(hipStream_t st, const TraceDev& T, const ComposeTerms& Tm, uint64_t row0,
+                                uint64_t nrows) {
   if (row0 + nrows > T.n) return hipErrorInvalidValue;
-  // two adjacent rows per lane (4 measured even in round 2); the one-row
-  // kernel for n = 1 and odd row ranges. SEZKP_COMPOSE_ROWS=1 forces the
-  // one-row kernel (read per launch: the parity test switches it).
+  if (nrows == 0) return hipSuccess;
+  // two adjacent rows per lane (4 measured even in round 2); one row for n = 1
+  // and odd row ranges. SEZKP_COMPOSE_ROWS=1|2|4 forces a form (read per
+  // launch: the parity test switches it).
   const char* rw_s = getenv("SEZKP_COMPOSE_ROWS");
-  if (!(rw_s && atoi(rw_s) == 1) && T.n >= 2 && (row0 | nrows) % 2 == 0) {
-    const unsigned g = (unsigned)((nrows / 2 + TR_THREADS - 1) / TR_THREADS);
-    if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compose_rows<2>, dim3(g), dim3(TR_THREADS), 0, st, T, ch, tw, logn, out, row0, row0 + nrows);
-    return hipGetLastError();
-  }
+  int rw = rw_s ? atoi(rw_s) : 2;
+  if (rw != 1 && rw != 2 && rw != 4) rw = 2;
+  while (rw > 1 && (T.n < (uint64_t)rw || (row0 | nrows) % rw)) rw >>= 1;
+  const unsigned g = (unsigned)((nrows / rw + TR_THREADS - 1) / TR_THREADS);
+  if (rw == 4) hipLaunchKernelGGL(k_compose_terms<4>, dim3(g), dim3(TR_THREADS), 0, st, T, Tm, row0, row0 + nrows);
+  else if (rw == 2) hipLaunchKernelGGL(k_compose_terms<2>, dim3(g), dim3(TR_THREADS), 0, st, T, Tm, row0, row0 + nrows);
+  else hipLaunchKernelGGL(k_compose_terms<1>, dim3(g), dim3(TR_THREADS), 0, st, T, Tm, row0, row0 + nrows);
+  return hipGetLastError();
+}
+hipError_t launch_compose_combine(hipStream_t st, const ComposeTerms& Tm, const DevChal* ch, const NttTables& tw,
+                                  int logn, uint64_t* out, uint64_t row0, uint64_t nrows) {
   const unsigned grid = (unsigned)((nrows + TR_THREADS - 1) / TR_THREADS);
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_compose, dim3(grid), dim3(TR_THREADS), 0, st, T, ch, tw, logn, out, row0, row0 + nrows);
+  hipLaunchKernelGGL(k_compose_combine, dim3(grid), dim3(TR_THREADS), 0, st, Tm, ch, tw, logn, out, row0,
+                     row0 + nrows);
   return hipGetLastError();
 }
 hipError_t launch_col_open(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* outer_nodes,

@@ -69,13 +69,13 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
     for rank, digest, repeat_ok, calls in res:
         assert digest == want, f"rank {rank}: {digest}"
         assert repeat_ok
-        # per prove: three all-to-alls (two for the INTT, one for the LDE), one
-        # byte-sum (proof body), allgathers
-        assert calls["alltoall"] == 6 and calls["allreduce"] == 2 and calls["allgather"] > 0
+        # per prove: one all-to-all (the LDE's), one byte-sum (proof body),
+        # allgathers (the replicated INTT's values ride in one of them)
+        assert calls["alltoall"] == 2 and calls["allreduce"] == 2 and calls["allgather"] > 0
         # sezkp_ctx_comm_stats: one entry per collective of the last prove
         st = {c["name"]: c for c in calls["stats"]}
-        assert {"col_chunk_roots", "intt_alltoall1", "intt_alltoall2", "intt_coeffs",
-                "lde_alltoall", "layer0_run_roots", "fri_run_roots", "proof_allreduce"} <= set(st), sorted(st)
+        assert {"col_chunk_roots", "d_values", "lde_alltoall", "layer0_run_roots", "fri_rep_values",
+                "fri_run_roots", "proof_allreduce"} == set(st), sorted(st)
         assert all(c["bytes"] > 0 and c["ms"] >= 0 for c in calls["stats"])
 
 
@@ -114,20 +114,25 @@ def test_sharded_per_point_deep_matches_oracle(gpu_ok, product, oracle, monkeypa
 
 
 @pytest.mark.parametrize("no_deep_poly", [False, True])
-def test_sharded_replicated_intt_matches_oracle(gpu_ok, product, oracle, monkeypatch, no_deep_poly):
-    """SEZKP_REPLICATED_INTT=1: the ranks gather all n base values and run the
-    n-point INTT each (the round-1 schedule) instead of the distributed INTT;
-    same bytes, one all-to-all per prove."""
-    monkeypatch.setenv("SEZKP_REPLICATED_INTT", "1")
+@pytest.mark.parametrize("world,T,b,tau,seed", [(4, 1 << 14, 512, 3, 11), (2, 1 << 15, 100, 8, 9),
+                                                (8, 1 << 16, 333, 2, 13)])
+def test_sharded_distributed_intt_matches_oracle(gpu_ok, product, oracle, monkeypatch, no_deep_poly, world, T, b,
+                                                 tau, seed):
+    """SEZKP_DIST_INTT=1: the distributed INTT (two all-to-alls, P-point DFTs,
+    a local n/P-point INTT, the coefficient allgather) instead of the default
+    replicated n-point INTT on every rank; same bytes, three all-to-alls per
+    prove (two of them the INTT's)."""
+    monkeypatch.setenv("SEZKP_DIST_INTT", "1")
     if no_deep_poly:
         monkeypatch.setenv("SEZKP_NO_DEEP_POLY", "1")
-    T, b, tau, seed = 1 << 14, 512, 3, 11
     blocks = product.synthetic_blocks(T, b, tau, seed)
     want = hashlib.sha256(oracle.prove_v1(blocks, blocks.manifest_root())).hexdigest()
-    for rank, digest, repeat_ok, calls in _run(4, T, b, tau, seed):
+    for rank, digest, repeat_ok, calls in _run(world, T, b, tau, seed):
         assert digest == want, f"rank {rank}: {digest}"
         assert repeat_ok
-        assert calls["alltoall"] == 2
+        assert calls["alltoall"] == 6
+        st = {c["name"] for c in calls["stats"]}
+        assert {"intt_alltoall1", "intt_alltoall2", "intt_coeffs"} <= st, sorted(st)
 
 
 def test_sharded_context_world1_is_single_gpu(gpu_ok, product, oracle):
