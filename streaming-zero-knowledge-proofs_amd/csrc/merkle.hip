@@ -571,6 +571,16 @@ __global__ void __launch_bounds__(256) k_cyc_unpack(const uint64_t* __restrict__
   const uint64_t k1 = r >> lsp, t = r & ((1ULL << lsp) - 1);
   local[(k1 << L16_LOG) + (t << logP) + g] = recv[o];
 }
+// rank g's runs out of the whole LDE (P = 2, full_lde): local[k1 S + t] =
+// full[(k1 P + g) S + t], two values per lane
+__global__ void __launch_bounds__(256) k_runs_extract(const uint64_t* __restrict__ full, uint64_t* __restrict__ local,
+                                                      uint64_t M, int logP, uint32_t g) {
+  const uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;  // local index
+  if (o >= M) return;
+  const uint64_t k1 = o >> L16_LOG, t = o & (L16_TILE - 1);
+  *reinterpret_cast<ulonglong2*>(local + o) =
+      *reinterpret_cast<const ulonglong2*>(full + (((k1 << logP) + g) << L16_LOG) + t);
+}
 // run roots allgathered as [rank d][run k1] -> cap level L16_LOG node k1*P + d
 __global__ void __launch_bounds__(256) k_runroots_scatter(const uint32_t* __restrict__ gathered, TreeDev cap,
                                                           uint64_t nrun, int logP) {
@@ -696,6 +706,12 @@ hipError_t launch_cyc_pack(hipStream_t st, const uint64_t* cyc, uint64_t* send, 
 hipError_t launch_cyc_unpack(hipStream_t st, const uint64_t* recv, uint64_t* local, uint64_t M, int logP) {
   if (M % L16_TILE || (1 << logP) > (int)L16_TILE) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_cyc_unpack, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, recv, local, M, logP);
+  return hipGetLastError();
+}
+hipError_t launch_runs_extract(hipStream_t st, const uint64_t* full, uint64_t* local, uint64_t M, int logP,
+                               uint32_t g) {
+  if (M % L16_TILE || (g >> logP)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_runs_extract, dim3((unsigned)((M / 2 + 255) / 256)), dim3(256), 0, st, full, local, M, logP, g);
   return hipGetLastError();
 }
 hipError_t launch_runroots_scatter(hipStream_t st, const uint32_t* gathered, TreeDev cap, uint64_t nrun_per_rank,

@@ -1157,23 +1157,34 @@ __global__ void __launch_bounds__(NTT_THREADS) k_inv_base(ComposeTerms Tm, uint6
   __shared__ uint64_t wtot[NTT_THREADS / 64];
   __shared__ uint64_t s_inv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t i0 = row0 + ((uint64_t)blockIdx.x * NTT_THREADS + tid) * DQ_PER;
-  const bool act = i0 < row0 + nrows;  // nrows % 16 == 0: a lane's points are all in or all out
+  // the WG's rows wg0 + j NTT_THREADS + tid (j < DQ_PER): every load and
+  // store of a j step is one coalesced row range (lane-consecutive rows
+  // touched 8x the cache lines per instruction)
+  const uint64_t wg0 = row0 + (uint64_t)blockIdx.x * NTT_THREADS * DQ_PER, end = row0 + nrows;
   uint64_t d[DQ_PER], a[DQ_PER], cv[DQ_PER];
   uint64_t Pp = 1;
-  if (act) {
+  {
     const ComposeCoef K = compose_coef(ch);
-    const uint64_t e = i0 << (T.K - logn);
+    // exponents mod 2^K (w^(2^K) = 1): rows past a small n stay inside the
+    // twiddle tables (their values are never used)
+    const uint64_t kmask = (1ULL << T.K) - 1;
+    const uint64_t e = ((wg0 + tid) << (T.K - logn)) & kmask;
     uint64_t x = gl_mul(T.hi[e >> T.S], T.lo[e & ((1ULL << T.S) - 1)]);
-    const uint64_t e1 = 1ULL << (T.K - logn);
-    const uint64_t wn = gl_mul(T.hi[e1 >> T.S], T.lo[e1 & ((1ULL << T.S) - 1)]);
+    const uint64_t e1 = ((uint64_t)NTT_THREADS << (T.K - logn)) & kmask;
+    const uint64_t ws = gl_mul(T.hi[e1 >> T.S], T.lo[e1 & ((1ULL << T.S) - 1)]);  // w_n^NTT_THREADS
 #pragma unroll
     for (int j = 0; j < DQ_PER; j++) {
-      cv[j] = compose_value(Tm, K, i0 + j, x);  // C_j (air.rs:49-136 + mask)
-      d[j] = gl_sub(x, z);
+      const uint64_t row = wg0 + (uint64_t)j * NTT_THREADS + tid;
+      if (row < end) {
+        cv[j] = compose_value(Tm, K, row, x);  // C_row (air.rs:49-136 + mask)
+        d[j] = gl_sub(x, z);
+      } else {  // past the block: a unit factor in the batch
+        cv[j] = 0;
+        d[j] = 1;
+      }
       Pp = j ? gl_mul(Pp, d[j]) : d[j];
       a[j] = Pp;
-      x = gl_mul(x, wn);
+      x = gl_mul(x, ws);
     }
   }
   uint64_t S = Pp, Tq = Pp;
@@ -1203,14 +1214,15 @@ __global__ void __launch_bounds__(NTT_THREADS) k_inv_base(ComposeTerms Tm, uint6
     if (w != wave) invW = gl_mul(invW, wtot[w]);
   uint64_t inv_run = gl_mul(gl_mul(invW, Q), Sprev);
   uint64_t acc = 0;
-  if (act) {
 #pragma unroll
-    for (int j = DQ_PER - 1; j >= 0; j--) {
-      const uint64_t ij = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
-      if (j) inv_run = gl_mul(inv_run, d[j]);
-      const uint64_t xj = gl_add(d[j], z);  // w_n^(i0 + j)
+  for (int j = DQ_PER - 1; j >= 0; j--) {
+    const uint64_t ij = j ? gl_mul(inv_run, a[j - 1]) : inv_run;
+    if (j) inv_run = gl_mul(inv_run, d[j]);
+    const uint64_t row = wg0 + (uint64_t)j * NTT_THREADS + tid;
+    if (row < end) {
+      const uint64_t xj = gl_add(d[j], z);  // w_n^row
       const uint64_t Dj = gl_mul(cv[j], ij);
-      Dout[i0 + j] = Dj;
+      Dout[row] = Dj;
       acc = gl_add(acc, gl_mul(Dj, xj));
     }
   }

@@ -250,7 +250,12 @@ struct sezkp_ctx {
   int rR = -1;                          // run layers 0..rR (len >= 4096 P), the rest replicated
   uint64_t ch_lo = 0, ch_hi = 0;        // this rank's column chunks
   uint32_t blk_lo = 0, blk_cnt = 0;     // blocks overlapping this rank's rows (+ the next row)
-  uint64_t* d_cyc = nullptr;            // P > 1: coset values f(3 w^(rank + P j))
+  uint64_t* d_cyc = nullptr;            // P > 1: coset values f(3 w^(rank + P j)) (full_lde: all N values)
+  // P = 2: every rank computes the whole N-point LDE (the single-device
+  // schedule) and takes its own runs from it, instead of its coset and the
+  // all-to-all: one link carries the all-to-all's N/4 values per rank at
+  // 153 GB/s (~0.22 ms), more than the other half of the LDE costs (~0.09 ms)
+  bool full_lde = false;
   uint64_t* d_xbuf = nullptr;           // P > 1: all-to-all send buffer
   uint64_t* d_rep = nullptr;            // replicated layers (P > 1: first the whole layer rR)
   std::vector<uint64_t*> lvals;         // per FRI layer: this rank's values
@@ -707,8 +712,9 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   Tm.bl = dalloc<uint64_t>((size_t)nblk + 1);
   Tm.row_flags = T.row_flags;
   Tm.row_blk = T.row_blk;
-  {  // DEEP quotient tables (sized for this rank's M = N / P LDE points)
-    const uint64_t Ml = N >> logP;
+  full_lde = sharded() && world == 2;
+  {  // DEEP quotient tables (sized for this rank's M = N / P LDE points, or N)
+    const uint64_t Ml = full_lde ? N : N >> logP;
     d_dq_part = dalloc<uint64_t>(n / 1024 + 1);  // partials of >= 1024 rows (dq_rows_per_part)
     d_dq_rlo = dalloc<uint64_t>(4096);
     d_dq_rhi = dalloc<uint64_t>(Ml > 4096 ? Ml >> 12 : 1);
@@ -720,8 +726,8 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   rR = sharded() ? k - L16_LOG - logP : (k >= L16_LOG ? k - L16_LOG : -1);
   d_lde = dalloc<uint64_t>(M);
   if (sharded()) {
-    d_cyc = dalloc<uint64_t>(M);
-    d_xbuf = dalloc<uint64_t>(M);
+    d_cyc = dalloc<uint64_t>(full_lde ? N : M);
+    if (!full_lde) d_xbuf = dalloc<uint64_t>(M);
   }
   lvals.assign(k + 1, nullptr);
   ltrees.assign(k + 1, TreeDev{});
@@ -1281,11 +1287,14 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     // rank g evaluates the coset 3 w_N^g <w_M>: H's N coefficients fold to M
     // (M >= n): h'_k = [k < n] q_k (3 w_N^g)^k + c' G rho^k, rho = (3/z) w_N^g,
     // G = sum_{t<P} rho^(tM); single device: rho = 3/z, G = 1
-    const uint64_t M_ = N >> logP;
-    const uint64_t rho = hgl_mul(hgl_mul(3, hgl_inv(z)), hgl_pow(hgl_root_2exp((uint32_t)logN), (uint64_t)rank));
+    // (full_lde: the whole domain, as on one device)
+    const int cP = full_lde ? 0 : logP;
+    const uint64_t cg = full_lde ? 0 : (uint64_t)rank;
+    const uint64_t M_ = N >> cP;
+    const uint64_t rho = hgl_mul(hgl_mul(3, hgl_inv(z)), hgl_pow(hgl_root_2exp((uint32_t)logN), cg));
     const uint64_t rhoM = hgl_pow(rho, M_);
     uint64_t G = 0, pw = 1;
-    for (int t = 0; t < (1 << logP); t++) {
+    for (int t = 0; t < (1 << cP); t++) {
       G = hgl_add(G, pw);
       pw = hgl_mul(pw, rhoM);
     }
@@ -1346,25 +1355,32 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
   }
   if (dq)
-    ok(launch_q_tables(st, d_dq_part, logn, logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk, dq_per), "q_tables");
+    ok(launch_q_tables(st, d_dq_part, logn, full_lde ? logN : logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk, dq_per),
+       "q_tables");
   rec(5);
   // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on
   // 3 w_N^g <w_M> (M = N/P), no communication
   const uint64_t inv_n = hgl_inv(n % GL_P_HOST);
   uint64_t* lde_out = sharded ? d_cyc : d_lde;
-  const uint64_t coset_e = sharded ? ((uint64_t)rank << (tw.K - logN)) : 0;
-  const DeepFuse dfuse{z, logN, logP, (uint32_t)rank};
+  // the evaluated coset: 3 w_N^g <w_M> (rank g of P), or the whole domain
+  const int eP = full_lde ? 0 : logP;
+  const uint32_t eg = full_lde ? 0u : (uint32_t)rank;
+  const int logE = logN - eP;
+  const uint64_t coset_e = sharded && !full_lde ? ((uint64_t)rank << (tw.K - logN)) : 0;
+  const DeepFuse dfuse{z, logN, eP, eg};
   bool deep_fused = dq;
   const int src_logP = dist_intt ? logP : 0;
   if (dq)
-    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, nullptr, nullptr, &dpoly, src_logP),
+    ok(ntt_dit(st, lde_out, logE, false, tw, d_base, logn, inv_n, coset_e, nullptr, nullptr, &dpoly, src_logP),
        "lde_ntt");
   else
-    ok(ntt_dit(st, lde_out, logM, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused, nullptr, src_logP),
+    ok(ntt_dit(st, lde_out, logE, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused, nullptr, src_logP),
        "lde_ntt");
   rec(6);
-  if (!deep_fused) ok(launch_deep(st, lde_out, logN, z, tw, logP, (uint32_t)rank), "deep");
-  if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI
+  if (!deep_fused) ok(launch_deep(st, lde_out, logN, z, tw, eP, eg), "deep");
+  if (full_lde) {  // this rank's runs of 4096 out of the whole LDE
+    ok(launch_runs_extract(st, d_cyc, d_lde, M, logP, (uint32_t)rank), "runs_extract");
+  } else if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI
     ok(launch_cyc_pack(st, d_cyc, d_xbuf, M, logP), "cyc_pack");
     coll("lde_alltoall", P1 * (M >> logP) * 8, [&] { comm->alltoall(d_xbuf, d_cyc, (size_t)(M >> logP) * 8, st); });
     ok(launch_cyc_unpack(st, d_cyc, d_lde, M, logP), "cyc_unpack");

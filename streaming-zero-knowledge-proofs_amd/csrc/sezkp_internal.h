@@ -317,6 +317,10 @@ hipError_t launch_merkle_paths(hipStream_t st, const uint32_t* nodes, const Merk
 hipError_t launch_cyc_pack(hipStream_t st, const uint64_t* cyc, uint64_t* send, uint64_t M, int logP);
 hipError_t launch_cyc_unpack(hipStream_t st, const uint64_t* recv, uint64_t* local, uint64_t M, int logP);
 // gathered[d][k1] (run roots of rank d) -> level-12 node k1*P + d of `cap`
+// rank g's runs of 4096 (local index k1 S + t = global (k1 P + g) S + t) out
+// of the whole N-point LDE (sharded P = 2)
+hipError_t launch_runs_extract(hipStream_t st, const uint64_t* full, uint64_t* local, uint64_t M, int logP,
+                               uint32_t g);
 constexpr int RR_BATCH_MAX = 40;
 struct RunRootsBatch {
   const uint32_t* gathered[RR_BATCH_MAX];

@@ -69,13 +69,15 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
     for rank, digest, repeat_ok, calls in res:
         assert digest == want, f"rank {rank}: {digest}"
         assert repeat_ok
-        # per prove: one all-to-all (the LDE's), one byte-sum (proof body),
-        # allgathers (the replicated INTT's values ride in one of them)
-        assert calls["alltoall"] == 2 and calls["allreduce"] == 2 and calls["allgather"] > 0
+        # per prove: one all-to-all (the LDE's; none at P = 2, where every
+        # rank computes the whole LDE), one byte-sum (proof body), allgathers
+        # (the replicated INTT's values ride in one of them)
+        a2a = 0 if world == 2 else 1
+        assert calls["alltoall"] == 2 * a2a and calls["allreduce"] == 2 and calls["allgather"] > 0
         # sezkp_ctx_comm_stats: one entry per collective of the last prove
         st = {c["name"]: c for c in calls["stats"]}
-        assert {"col_chunk_roots", "d_values", "lde_alltoall", "layer0_run_roots", "fri_rep_values",
-                "fri_run_roots", "proof_allreduce"} == set(st), sorted(st)
+        assert {"col_chunk_roots", "d_values", "layer0_run_roots", "fri_rep_values", "fri_run_roots",
+                "proof_allreduce"} | ({"lde_alltoall"} if a2a else set()) == set(st), sorted(st)
         assert all(c["bytes"] > 0 and c["ms"] >= 0 for c in calls["stats"])
 
 
@@ -130,7 +132,7 @@ def test_sharded_distributed_intt_matches_oracle(gpu_ok, product, oracle, monkey
     for rank, digest, repeat_ok, calls in _run(world, T, b, tau, seed):
         assert digest == want, f"rank {rank}: {digest}"
         assert repeat_ok
-        assert calls["alltoall"] == 6
+        assert calls["alltoall"] == (4 if world == 2 else 6)
         st = {c["name"] for c in calls["stats"]}
         assert {"intt_alltoall1", "intt_alltoall2", "intt_coeffs"} <= st, sorted(st)
 
@@ -274,7 +276,7 @@ def _fail_worker(rank, world, port, point, q):
     os._exit(0)  # gloo may hold a timed-out collective: leave without a teardown handshake
 
 
-@pytest.mark.parametrize("point", ["lde_alltoall", "fri_run_roots", "proof_allreduce"])
+@pytest.mark.parametrize("point", ["d_values", "fri_run_roots", "proof_allreduce"])
 def test_sharded_failure_on_one_rank_fails_every_rank(gpu_ok, point):
     """A rank that fails after the first collective of a prove (injected right
     before a later collective) must not leave its peers blocked: every rank
