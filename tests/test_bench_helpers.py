@@ -67,8 +67,7 @@ def test_stdout_line_is_bounded_and_parseable():
     assert len(s) <= b.LINE_MAX_BYTES
     line = json.loads(s)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
-              "roofline", "cpu_baseline", "trace_resident", "single_proof", "configs", "dist_ntt",
-              "sharded_predicted", "detail"):
+              "roofline", "cpu_baseline", "single_proof", "configs", "dist_ntt", "sharded_predicted", "detail"):
         assert k in line, k
     assert line["value"] == full["value"]
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "hbm"):
