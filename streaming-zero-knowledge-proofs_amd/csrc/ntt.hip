@@ -768,6 +768,13 @@ __global__ void __launch_bounds__(512, 2) k_ntt_dif9(NttPassArgs P) {
 // w_{8L}^(low * rev3(q)) and stores them back (the four-step identity of
 // k_ntt4's DIF, three stages per LDS exchange).
 constexpr int R8_NT = 512;
+// LDS hand-off between lanes of ONE wave: a wave's LDS instructions execute
+// in issue order, so only the compiler has to keep its reads after its writes
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ int r8_pad(int e) { return e + (e >> 3); }  // conflict-free strides 64 / 8 / 1
 // w_64 = 2^39, w_64^-1 = 2^153 (2 has order 192)
 template <bool INV>
@@ -798,17 +805,31 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_w8r8(NttPassArgs P) {
   const uint64_t tiles_per_blk = (1ULL << G.sL) / NTT_CMAX;
   G.blk_base = (G.tile / tiles_per_blk) * (256ULL << G.sL);
   G.low0 = (G.tile % tiles_per_blk) * NTT_CMAX;
+  const int tw_shift = T.K - 8 - G.sL;
   uint64_t low;
+  (void)tile_pos(G, 0, c, low);
+  // stages 1..0 take rows 4h..4h+3, h = h0 and h0 + 4: the 32 rows stages
+  // 4..2 of this wave (g >> 2) wrote, so the last exchange stays in the wave.
+  // Every table twiddle depends on the lane only: fetched beside the data.
+  const int h0 = 8 * (g >> 2) + (g & 3);
+  const uint64_t w1 = tw_pow(T, (uint64_t)g << (T.K - 8), INV);  // w_256^g
+  uint64_t ta[2], tb = 1;
+  if (low) {  // pass twiddle w_{2^(8+sL)}^(low rev8(t)), rev8(4h + rev2(k)) = 64 k + rev6(h)
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++)
+      ta[hh] = tw_pow(T, (low * (uint64_t)(__brev((uint32_t)(h0 + 4 * hh)) >> 26)) << tw_shift, INV);
+    tb = tw_pow(T, (low * 64ULL) << tw_shift, INV);
+  }
   uint64_t x[8];
   // stages 7..5 (stride 32), straight from HBM
 #pragma unroll
   for (int d = 0; d < 8; d++) x[d] = P.a[tile_pos(G, g + 32 * d, c, low)];
   fft_dif_regs<3, INV>(x);
-  if (g) r8_twiddle(x, tw_pow(T, (uint64_t)g << (T.K - 8), INV));  // w_256^(g k)
+  if (g) r8_twiddle(x, w1);  // w_256^(g k)
 #pragma unroll
   for (int q = 0; q < 8; q++) sh[(g + 32 * q) * NTT_PADC + c] = x[q];
   __syncthreads();
-  {  // stages 4..2 (stride 4), twiddles w_32^(lo k): shifts
+  {  // stages 4..2 (stride 4) on rows 32 (g >> 2) + ..., twiddles w_32^(lo k): shifts
     const int lo = g & 3, base = (g >> 2) * 32 + lo;
 #pragma unroll
     for (int d = 0; d < 8; d++) x[d] = sh[(base + 4 * d) * NTT_PADC + c];
@@ -820,26 +841,21 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_w8r8(NttPassArgs P) {
 #pragma unroll
     for (int d = 0; d < 8; d++) sh[(base + 4 * d) * NTT_PADC + c] = x[d];
   }
-  __syncthreads();
-  // stages 1..0: 4-point groups t = 4h + d (h = g, g + 32), then the pass
-  // twiddle w_{2^(8+sL)}^(low rev8(t)), rev8(4h + rev2(k)) = 64 k + rev6(h)
-  const int tw_shift = T.K - 8 - G.sL;
+  wave_lds_sync();
   uint64_t* dst = P.out ? P.out : P.a;
 #pragma unroll
   for (int hh = 0; hh < 2; hh++) {
-    const int h = g + 32 * hh;
+    const int h = h0 + 4 * hh;
     uint64_t y[4];
 #pragma unroll
     for (int d = 0; d < 4; d++) y[d] = sh[(4 * h + d) * NTT_PADC + c];
     fft_dif_regs<2, INV>(y);
-    (void)tile_pos(G, 0, c, low);
     if (low) {
-      uint64_t a = tw_pow(T, (low * (uint64_t)(__brev((uint32_t)h) >> 26)) << tw_shift, INV);
-      const uint64_t b = tw_pow(T, (low * 64ULL) << tw_shift, INV);
+      uint64_t t = ta[hh];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        y[rev<2>(k)] = gl_mul(y[rev<2>(k)], a);
-        if (k < 3) a = gl_mul(a, b);
+        y[rev<2>(k)] = gl_mul(y[rev<2>(k)], t);
+        if (k < 3) t = gl_mul(t, tb);
       }
     }
 #pragma unroll
@@ -859,24 +875,30 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_n12r8(NttPassArgs P) {
   const uint64_t tile = nat_tile(blockIdx.x, gridDim.x);
   const uint64_t p0 = tile << 12;
   uint64_t x[8];
+  // both table twiddles depend on the lane only: fetched beside the data
+  const int lo2 = g & 63;
+  const uint64_t w1 = tw_pow(T, (uint64_t)g << (T.K - 12), INV);    // w_4096^g
+  const uint64_t w2 = tw_pow(T, (uint64_t)lo2 << (T.K - 9), INV);   // w_512^lo
   // stages 11..9 (stride 512), straight from HBM
 #pragma unroll
   for (int d = 0; d < 8; d++) x[d] = P.a[p0 + g + 512 * d];
   fft_dif_regs<3, INV>(x);
-  if (g) r8_twiddle(x, tw_pow(T, (uint64_t)g << (T.K - 12), INV));  // w_4096^(g k)
+  if (g) r8_twiddle(x, w1);
 #pragma unroll
   for (int q = 0; q < 8; q++) sh[r8_pad(g + 512 * q)] = x[q];
   __syncthreads();
+  // stages 8..0 stay inside 512-point block g >> 6: wave w's own block, so
+  // the exchanges below are between lanes of one wave
   {  // stages 8..6 (stride 64)
-    const int lo = g & 63, base = (g >> 6) * 512 + lo;
+    const int base = (g >> 6) * 512 + lo2;
 #pragma unroll
     for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(base + 64 * d)];
     fft_dif_regs<3, INV>(x);
-    if (lo) r8_twiddle(x, tw_pow(T, (uint64_t)lo << (T.K - 9), INV));  // w_512^(lo k)
+    if (lo2) r8_twiddle(x, w2);
 #pragma unroll
     for (int d = 0; d < 8; d++) sh[r8_pad(base + 64 * d)] = x[d];
   }
-  __syncthreads();
+  wave_lds_sync();
   {  // stages 5..3 (stride 8), twiddles w_64^(lo k): shifts
     const int lo = g & 7, base = (g >> 3) * 64 + lo;
 #pragma unroll
@@ -889,7 +911,7 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_n12r8(NttPassArgs P) {
 #pragma unroll
     for (int d = 0; d < 8; d++) sh[r8_pad(base + 8 * d)] = x[d];
   }
-  __syncthreads();
+  wave_lds_sync();
   // stages 2..0 on 8 consecutive points
 #pragma unroll
   for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(8 * g + d)];
@@ -904,7 +926,8 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_n12r8(NttPassArgs P) {
 // the radix-8 forms of the natural-order 2^20 DIF's passes (wide m = 8 with
 // 16 columns, narrow m = 12 with the natural-order store), else false.
 // Measured (round 4, profiles/r04/c2_ab.txt): 2^20 fwd + inv 72.7 -> 70.4 us;
-// the prover's in-place 12-stage INTT pass measured 2 us slower with it, so
+// round 5 (wave-local exchanges, twiddle loads beside the data) 69.3 -> 65.7 us.
+// The prover's in-place 12-stage INTT pass measured 2 us slower with it, so
 // it keeps k_ntt4's X16 form.
 static bool launch_r8(hipStream_t st, const NttPassArgs& P, bool inverse, unsigned tiles) {
   if (P.src || P.dp_rlo || P.nat_tr) return false;
