@@ -1247,7 +1247,9 @@ __device__ __forceinline__ DictPlan make_plan(int64_t lo, int64_t hi, bool has_m
   const uint64_t R = hi >= lo ? (uint64_t)hi - (uint64_t)lo + 1 : 1;
   if (R <= DICT_CAP) {
     P.R = (uint32_t)R;
-    uint64_t best = 2 * n, tabcost = 0, sz = R;  // K = -1: n leaves + n parents
+    // cost of level K: the tables' entries + the nodes this device gathers
+    // (nrows, not n: a sharded rank builds the same tables for 1/P of the rows)
+    uint64_t best = 2 * nrows, tabcost = 0, sz = R;  // K = -1: nrows leaves + parents
     bool open = true;
     // unrolled: constant pw[] indices keep P in registers (a runtime index put
     // it in scratch memory, and the kernel took ~23 us for 33 tiny workgroups)
@@ -1257,7 +1259,7 @@ __device__ __forceinline__ DictPlan make_plan(int64_t lo, int64_t hi, bool has_m
       if (open) {
         P.pw[k] = (uint32_t)sz;
         tabcost += sz;
-        const uint64_t cost = tabcost + (n >> k);
+        const uint64_t cost = tabcost + (nrows >> k);
         if (cost < best) { best = cost; P.K = k; }
         sz = sz * sz;
       }
