@@ -5,6 +5,7 @@
 #   2. kernel stats of the default bench (3 proofs in flight)
 #   3. one PMC pass of VALU/LDS issue counters (tools/pmc_valu.py)
 #   4. FETCH_SIZE and WRITE_SIZE in separate passes (tools/pmc_summary.py)
+#   5. one PMC pass of wave-cycle split counters (tools/pmc_table.py)
 # Each step has its own time limit; the first failure ends the script.
 set -euo pipefail
 export TMPDIR=/tmp
@@ -19,6 +20,9 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INST
   SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/valu -o run -- $B > $O/valu.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $B > $O/fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $B > $O/write.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+  SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES --output-format csv -d $O/waits -o run -- $B > $O/waits.log 2>&1
 python3 tools/pmc_summary.py $O/fetch $O/write $O/valu > $O/pmc_summary.json
+python3 tools/pmc_table.py $(find $O/waits -name "*counter_collection.csv") > $O/pmc_waits.txt
 python3 tools/pmc_valu.py $O/valu/run_counter_collection.csv > $O/pmc_valu.txt
 echo profile_round done
