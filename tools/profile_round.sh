@@ -6,6 +6,7 @@
 #   3. one PMC pass of VALU/LDS issue counters (tools/pmc_valu.py)
 #   4. FETCH_SIZE and WRITE_SIZE in separate passes (tools/pmc_summary.py)
 #   5. one PMC pass of wave-cycle split counters (tools/pmc_table.py)
+#   6. config 2 (the 2^20 NTT round trip): kernel stats and PMC passes (tools/c2_pmc.sh)
 # Each step has its own time limit; the first failure ends the script.
 set -euo pipefail
 export TMPDIR=/tmp
@@ -25,4 +26,5 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_
 python3 tools/pmc_summary.py $O/fetch $O/write $O/valu > $O/pmc_summary.json
 python3 tools/pmc_table.py $(find $O/waits -name "*counter_collection.csv") > $O/pmc_waits.txt
 python3 tools/pmc_valu.py $O/valu/run_counter_collection.csv > $O/pmc_valu.txt
+bash tools/c2_pmc.sh
 echo profile_round done
