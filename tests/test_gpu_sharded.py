@@ -81,13 +81,16 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
         assert all(c["bytes"] > 0 and c["ms"] >= 0 for c in calls["stats"])
 
 
-def test_sharded_config5_size_p8_matches_openmp_oracle(gpu_ok, product):
+@pytest.mark.parametrize("T,tau,seed", [(1 << 22, 8, 5), (1 << 21, 2, 6)])
+def test_sharded_config5_size_p8_matches_openmp_oracle(gpu_ok, product, T, tau, seed):
     """BASELINE config 5's shape: T = 2^22 (N = 2^25), tau = 8, over P = 8
-    ranks (here sharing one GPU through host collectives). Every rank returns
-    the bytes of the OpenMP oracle, run in a child process on 16 threads."""
+    ranks (here sharing one GPU through host collectives); and the headline's
+    N = 2^24 over P = 8 (M = 2^21 LDE points per rank: the 2048-leaf tree
+    workgroups). Every rank returns the bytes of the OpenMP oracle, run in a
+    child process on 16 threads."""
     import subprocess
     from conftest import ROOT
-    T, b, tau, seed = 1 << 22, 512, 8, 5
+    b = 512
     code = ("import sys; sys.path[:0]=[%r,%r]\n"
             "import hashlib, oracle_ctypes as O, sezkp_amd as S\n"
             "O.use_mt(16)\n"
