@@ -1280,11 +1280,14 @@ __device__ __forceinline__ DictPlan make_plan(int64_t lo, int64_t hi, bool has_m
       for (int k = 3; k < DICT_LEVELS; k++) P.pw[k] = 0;
     }
   }
-  // a lane's rows: 2^(6 + dict_extra(K)) (32 gathered nodes for K >= 1), and
-  // fewer when this device commits fewer than 2^21 rows (a sharded rank), so
-  // the commit still has ~4 waves per SIMD: one step of a per halving
+  // a lane's rows: 2^(6 + a), a = dict_extra(K) lowered one step per halving
+  // of the device's rows below 2^22, so the commit has waves enough to fill
+  // the chip (one wave per 64-lane WG, 4 per SIMD) on every shape: at 2^21
+  // rows the K >= 3 columns take 128 rows per lane, the K = 2 ones 64
+  // (round 5: k_col_commit_dict 314 -> 291 us per launch; a second step
+  // 306 us, profiles/r05/ab/dict_rows_per_lane_ab{1,2}.txt)
   int a = dict_extra(P.K);
-  for (uint64_t r = nrows; r < (1ULL << 21) && a > 0; r <<= 1) a--;
+  for (uint64_t r = nrows; r < (1ULL << 22) && a > 0; r <<= 1) a--;
   P.a = (uint32_t)a;
   return P;
 }
