@@ -12,11 +12,11 @@ set -euo pipefail
 export TMPDIR=/tmp
 O=gpurun_out/prof
 mkdir -p $O
-B="python3 bench.py --inflight 1 --steps 3 --warmup 1 --no-cpu-baseline --no-configs --no-worst-case --no-host-to-proof --no-host-rows --no-sharded --dntt-log-n 0"
+B="python3 bench.py --inflight 1 --steps 3 --warmup 1 --no-cpu-baseline --no-configs --no-worst-case --no-host-to-proof --no-host-rows --no-sharded --dntt-log-n 0 --detail $O/pmc.detail.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/if1 -o run -- \
-  python3 bench.py --inflight 1 --steps 20 --no-cpu-baseline --no-configs --no-worst-case --no-host-to-proof --no-host-rows --no-sharded --dntt-log-n 0 > $O/if1.log 2>&1
+  python3 bench.py --inflight 1 --steps 20 --no-cpu-baseline --no-configs --no-worst-case --no-host-to-proof --no-host-rows --no-sharded --dntt-log-n 0 --detail $O/if1.detail.json > $O/if1.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/default -o run -- \
-  python3 bench.py --no-cpu-baseline --no-sharded > $O/default.log 2>&1
+  python3 bench.py --no-cpu-baseline --no-sharded --detail $O/default.detail.json > $O/default.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
   SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/valu -o run -- $B > $O/valu.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $B > $O/fetch.log 2>&1
