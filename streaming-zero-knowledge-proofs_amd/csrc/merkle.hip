@@ -759,11 +759,14 @@ hipError_t launch_leaf_subtree(hipStream_t st, const uint64_t* in, uint64_t* out
 
 hipError_t launch_layer16(hipStream_t st, const uint64_t* in, uint64_t* out_vals, int logLen, int fold, uint64_t beta,
                           TreeDev tree, int stop, const uint64_t* dbeta, int wg_log) {
-  if ((wg_log != L16_LOG && wg_log != L16S_LOG) || logLen < wg_log || stop < tree.lstore || stop > wg_log)
+  if ((wg_log != L16_LOG && wg_log != L16M_LOG && wg_log != L16S_LOG) || logLen < wg_log || stop < tree.lstore ||
+      stop > wg_log)
     return hipErrorInvalidValue;
   const dim3 grid((unsigned)(1ULL << (logLen - wg_log)));
   if (wg_log == L16_LOG)
     hipLaunchKernelGGL(k_layer16<4>, grid, dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, dbeta, tree, stop);
+  else if (wg_log == L16M_LOG)
+    hipLaunchKernelGGL(k_layer16<3>, grid, dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, dbeta, tree, stop);
   else
     hipLaunchKernelGGL(k_layer16<2>, grid, dim3(MK_THREADS), 0, st, in, out_vals, logLen, fold, beta, dbeta, tree, stop);
   return hipGetLastError();
@@ -798,6 +801,9 @@ hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlay
   const TailArgs none{};
   if (wg_log == L16_LOG)
     hipLaunchKernelGGL(k_forest16<4>, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
+                       tail ? *tail : none, ntail, tailbuf, wg_base);
+  else if (wg_log == L16M_LOG)
+    hipLaunchKernelGGL(k_forest16<3>, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
                        tail ? *tail : none, ntail, tailbuf, wg_base);
   else if (wg_log == L16S_LOG)
     hipLaunchKernelGGL(k_forest16<2>, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,

@@ -722,7 +722,11 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   }
   M = N >> logP;
   logM = logN - logP;
-  tree_wg_log = M <= (1ULL << 21) ? L16S_LOG : L16_LOG;
+  // tree workgroups of 2048 leaves (1024 on small per-device LDEs): alone a
+  // 4096-leaf workgroup is as fast, but with proofs in flight the half-size
+  // ones let the concurrent proofs' kernels interleave (+5% in flight, round 5,
+  // profiles/r05/ab/tree_wg2048_headline_ab.txt)
+  tree_wg_log = M <= (1ULL << 21) ? L16S_LOG : L16M_LOG;
   rR = sharded() ? k - L16_LOG - logP : (k >= L16_LOG ? k - L16_LOG : -1);
   d_lde = dalloc<uint64_t>(M);
   if (sharded()) {

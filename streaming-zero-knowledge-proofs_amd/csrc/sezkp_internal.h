@@ -361,6 +361,7 @@ hipError_t launch_upper_jobs(hipStream_t st, const UpperJob* d_jobs, int njobs);
 
 constexpr int L16_LOG = 12;  // leaves per WG of the 16-leaves-per-lane layer kernel
 constexpr int L16S_LOG = 10; // leaves per WG of its 4-leaves-per-lane form (small trees)
+constexpr int L16M_LOG = 11; // leaves per WG of its 8-leaves-per-lane form
 // stop: highest level the WG reduces to (L16_LOG = its run root; LSTORE_FRI
 // leaves levels 7..12 to the upper jobs, whose lanes are all busy)
 // wg_log: leaves per WG (L16_LOG, or L16S_LOG for trees too small to fill

@@ -10,7 +10,7 @@ import re
 import sys
 
 D = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/libab"
-KS = ("k_col_commit_dict", "k_forest16<4>", "k_layer16<4>", "k_dict_level")
+KS = ("k_col_commit_dict", "k_forest16", "k_layer16", "k_dict_level")
 for rep in (1, 2):
     for arm in ("main", "alt"):
         f = glob.glob(os.path.join(D, f"{arm}{rep}", "*kernel_stats.csv"))
@@ -19,8 +19,8 @@ for rep in (1, 2):
         avg = {}
         for r in csv.DictReader(open(f[0])):
             m = re.search(r"sezkp::(k_[A-Za-z0-9_]+)(<[^(]*>)?", r["Name"])
-            if m:
-                avg[m.group(1) + (m.group(2) or "")] = float(r["AverageNs"]) / 1e3
+            if m:  # template instances summed per kernel name (one instance runs per shape)
+                avg[m.group(1)] = avg.get(m.group(1), 0) + float(r["TotalDurationNs"]) / 1e3 / max(1, int(r["Calls"]))
         d1 = json.load(open(os.path.join(D, f"{arm}{rep}_if1.json")))
         ln = open(os.path.join(D, f"{arm}{rep}_bench.log")).read().strip().splitlines()[-1]
         v = json.loads(ln)["value"]
