@@ -4,7 +4,7 @@
  * Drop-in boundary for logannye/streaming-zero-knowledge-proofs:
  *   - top level: replaces `impl ProvingBackend for StarkV1`
  *     (crates/sezkp-core/src/backend.rs:41-61, crates/sezkp-stark/src/lib.rs:126-190);
- *   - version symbols: crates/sezkp-ffi/src/lib.rs:65-79 (ABI bumped 1 -> 3);
+ *   - version symbols: crates/sezkp-ffi/src/lib.rs:65-79 (ABI bumped 1 -> 4);
  *   - kernel level: the hot loops of crates/sezkp-ffts (ntt.rs:79-177,
  *     coset.rs:85-102), crates/sezkp-stark/src/v1/{lde.rs:42-97,
  *     fri_stream.rs:37-121, merkle.rs:46-160, prover.rs:200-239}.
@@ -24,7 +24,11 @@
 extern "C" {
 #endif
 
-#define SEZKP_ABI_VERSION 3u
+/* ABI 4 (round 6): sezkp_fs_xof runs on the host and ignores `stream`;
+ * sezkp_ctx_stage_times writes 17 values (the three fs_point slots of ABI 3
+ * are gone) and col_openings is the openings kernel's own time; blocks of
+ * zero steps (step_hi = step_lo - 1) are accepted as the reference does. */
+#define SEZKP_ABI_VERSION 4u
 
 #define SEZKP_OK 0
 #define SEZKP_E_INVALID (-1)   /* malformed input (shape, non power-of-two n, ...) */
@@ -135,7 +139,9 @@ int32_t sezkp_ctx_prove_borrow(sezkp_ctx* ctx, const uint8_t manifest_root[32], 
  * the context's stream when SEZKP_STAGE_EVENTS=1 (or SEZKP_KERNEL_EVENTS=1) is
  * set, else 0 (timed events lengthen a proof). Order: expand, col_commit,
  * col_outer, compose, intt, lde_ntt, deep, layer0_tree, layer0_upper,
- * fri_fold_trees, col_openings, fri_paths, total, then host wall / sync-wait /
+ * fri_fold_trees, col_openings (the openings kernel alone, on the side
+ * stream: it overlaps fri_paths; the query round trip before both is only in
+ * total), fri_paths, total, then host wall / sync-wait /
  * final-wait / serialize (always measured),
  * then the FRI forest launch (k_forest16), timed only when
  * SEZKP_KERNEL_EVENTS=1 is set (else 0).
@@ -343,7 +349,7 @@ void sezkp_blake3(const uint8_t* data, size_t len, uint8_t* out, size_t out_len)
  * the next sfx_len[i] bytes of `suffixes` (a transcript passes "challenge" ||
  * u32 LE len || label). Outputs are concatenated in `out` (sum of out_len
  * bytes). The known-answer interface of the prover's transcript. `stream` is
- * ignored (kept from ABI 3, when this ran a device kernel). */
+ * ignored (ABI 3 ran a device kernel on it; ABI 4 answers on the host). */
 int32_t sezkp_fs_xof(const uint8_t* stream_bytes, size_t stream_len, const uint32_t* pos, const uint8_t* suffixes,
                      const uint32_t* sfx_len, const uint32_t* out_len, uint32_t nchal, uint8_t* out, void* stream);
 

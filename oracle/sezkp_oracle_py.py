@@ -205,7 +205,7 @@ def row_snapshots(blocks):
     tau = len(blocks[0]["windows"]) if blocks else 0
     rows = []
     for b in blocks:
-        blen = b["step_hi"] - b["step_lo"] + 1
+        blen = (b["step_hi"] - b["step_lo"] + 1) % (1 << 64)  # usize wrap: step_hi = step_lo - 1 is 0 rows
         heads = [0] * tau
         wl = [abs(b["windows"][r]["right"] - b["windows"][r]["left"]) + 1 for r in range(tau)]
         for j in range(blen):

@@ -285,6 +285,9 @@ struct sezkp_ctx {
   // live time (bench roofline)
   hipEvent_t kev[2]{};
   double kernel_ms = 0;
+  // stage events: the openings kernel on the side stream (it overlaps
+  // fri_paths on the prover stream, so it has its own pair)
+  hipEvent_t oev[2]{};
   // host-side split of one prove(): wall, time blocked in stream syncs,
   // final D2H wait, proof serialization (after the last sync)
   double host_ms[4]{};
@@ -437,6 +440,8 @@ struct sezkp_ctx {
     for (auto& e : coll_ev) (void)hipEventDestroy(e);
     for (auto& e : kev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : oev)
+      if (e) (void)hipEventDestroy(e);
     if (st2) (void)hipStreamSynchronize(st2);
     if (ev_fold) (void)hipEventDestroy(ev_fold);
     if (ev_tail) (void)hipEventDestroy(ev_tail);
@@ -513,7 +518,75 @@ static void shard_range(const uint64_t* step_start, uint32_t nblk, int logn, int
   blk_cnt = block_of(r1) - blk_lo + 1;
 }
 
-void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows) {
+// Blocks of zero steps (step_hi = step_lo - 1, so step_hi - step_lo + 1 wraps
+// to 0) contribute no rows: TraceColumns::build and RowIter skip them
+// (columns.rs:254-257,281-284; openings.rs:209-238) and nothing else of
+// prove_v1 reads a block (tau comes from the view). The device image is built
+// from the view without them; the step arrays are shared, and every per-block
+// field is copied here, on the host, before any asynchronous copy is issued
+// (write_trace reads the per-block fields into its pinned table synchronously).
+struct NonEmptyBlocks {
+  sezkp_block_view v{};
+  std::vector<uint16_t> version, ctrl_in, ctrl_out;
+  std::vector<uint32_t> block_id, off_in, off_out;
+  std::vector<uint64_t> step_lo, step_hi, step_start;
+  std::vector<int64_t> in_head_in, in_head_out, win_left, win_right;
+};
+static const sezkp_block_view& drop_empty_blocks(const sezkp_block_view& in, NonEmptyBlocks& keep) {
+  uint32_t empty = 0;
+  for (uint32_t k = 0; k < in.n_blocks; k++) {
+    if (in.step_hi[k] - in.step_lo[k] + 1 != 0) continue;  // wrapping, as the reference's usize cast
+    if (in.step_start[k + 1] != in.step_start[k])
+      throw Err{SEZKP_E_INVALID, "block " + std::to_string(k) + ": zero-step range [" + std::to_string(in.step_lo[k]) +
+                                     ", " + std::to_string(in.step_hi[k]) + "] but movement_log has " +
+                                     std::to_string(in.step_start[k + 1] - in.step_start[k]) + " steps"};
+    empty++;
+  }
+  if (empty == 0) return in;
+  const uint32_t tau = in.tau;
+  keep = NonEmptyBlocks{};
+  keep.step_start.push_back(in.step_start[0]);
+  for (uint32_t k = 0; k < in.n_blocks; k++) {
+    if (in.step_hi[k] - in.step_lo[k] + 1 == 0) continue;
+    keep.version.push_back(in.version[k]);
+    keep.block_id.push_back(in.block_id[k]);
+    keep.step_lo.push_back(in.step_lo[k]);
+    keep.step_hi.push_back(in.step_hi[k]);
+    keep.ctrl_in.push_back(in.ctrl_in[k]);
+    keep.ctrl_out.push_back(in.ctrl_out[k]);
+    keep.in_head_in.push_back(in.in_head_in[k]);
+    keep.in_head_out.push_back(in.in_head_out[k]);
+    for (uint32_t r = 0; r < tau; r++) {
+      const size_t i = (size_t)k * tau + r;
+      keep.win_left.push_back(in.win_left[i]);
+      keep.win_right.push_back(in.win_right[i]);
+      keep.off_in.push_back(in.off_in[i]);
+      keep.off_out.push_back(in.off_out[i]);
+    }
+    keep.step_start.push_back(in.step_start[k + 1]);
+  }
+  sezkp_block_view& v = keep.v;
+  v = in;  // the step arrays stay the caller's
+  v.n_blocks = in.n_blocks - empty;
+  v.version = keep.version.data();
+  v.block_id = keep.block_id.data();
+  v.step_lo = keep.step_lo.data();
+  v.step_hi = keep.step_hi.data();
+  v.ctrl_in = keep.ctrl_in.data();
+  v.ctrl_out = keep.ctrl_out.data();
+  v.in_head_in = keep.in_head_in.data();
+  v.in_head_out = keep.in_head_out.data();
+  v.win_left = keep.win_left.data();
+  v.win_right = keep.win_right.data();
+  v.off_in = keep.off_in.data();
+  v.off_out = keep.off_out.data();
+  v.step_start = keep.step_start.data();
+  return v;
+}
+
+void sezkp_ctx::upload(const sezkp_block_view& v_in, uint64_t row0, uint64_t nrows) {
+  NonEmptyBlocks keep;
+  const sezkp_block_view& v = drop_empty_blocks(v_in, keep);
   HIP_OR_THROW(hipSetDevice(device));
   // a stage() may still be copying into / transposing a slot on the copy
   // stream: it must finish before its buffers become spares for this upload
@@ -527,7 +600,8 @@ void sezkp_ctx::upload(const sezkp_block_view& v, uint64_t row0, uint64_t nrows)
   // rows: sum over blocks of (step_hi - step_lo + 1) (columns.rs:254-257)
   uint64_t rows = 0;
   // the kernels index the step arrays through step_start: it must start at 0
-  // and every block must hold step_hi - step_lo + 1 >= 1 steps (no wrap-around)
+  // and every block must hold step_hi - step_lo + 1 >= 1 steps (no wrap-around;
+  // the blocks of zero steps, whose range wraps to 0, are gone already)
   if (nblk && v.step_start[0] != 0) throw Err{SEZKP_E_INVALID, "step_start[0] must be 0"};
   for (uint32_t k = 0; k < nblk; k++) {
     if (v.step_hi[k] < v.step_lo[k] || v.step_hi[k] - v.step_lo[k] >= (1ULL << 28))
@@ -984,8 +1058,10 @@ void sezkp_ctx::check_shape_same(const sezkp_block_view& v) const {
       throw Err{SEZKP_E_INVALID, "block " + std::to_string(k) + ": step range does not match its steps"};
 }
 
-void sezkp_ctx::stage(const sezkp_block_view& v) {
+void sezkp_ctx::stage(const sezkp_block_view& v_in) {
   if (!loaded) throw Err{SEZKP_E_INVALID, "no trace uploaded: the first trace of a shape goes through upload"};
+  NonEmptyBlocks keep;
+  const sezkp_block_view& v = drop_empty_blocks(v_in, keep);
   check_shape_same(v);
   HIP_OR_THROW(hipSetDevice(device));
   std::lock_guard<std::mutex> lk(stage_mu);
@@ -1031,8 +1107,9 @@ void sezkp_ctx::take_staged() {
 
 size_t sezkp_ctx::prove(const uint8_t mroot[32]) {
   if (broken)
-    throw Err{SEZKP_E_DEVICE, "context unusable: an earlier sharded prove failed after its first collective and "
-                              "aborted the communicator (destroy the context and create a new one)"};
+    throw Err{SEZKP_E_DEVICE, "context unusable: an earlier prove aborted the communicator after a failure past "
+                              "its first collective, or could not clear a tripped guard word (destroy the context "
+                              "and create a new one)"};
   coll_issued = false;
   coll_used = 0;
   coll_stats.clear();
@@ -1205,7 +1282,17 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
       // the guard carries a data-dependent flag (GUARD_HEAD_RANGE from
       // k_expand): clear it, stream-ordered, so one bad trace does not fail
       // the later proofs of good ones on this context
-      if (g) (void)hipMemsetAsync(d_err, 0, 64, st);
+      if (g) {
+        // a failed clear would leave the guard set and fail every later proof
+        // with this one's error: mark the context unusable instead
+        const hipError_t me = hipMemsetAsync(d_err, 0, 64, st);
+        if (me != hipSuccess) {
+          broken = true;
+          throw Err{SEZKP_E_DEVICE, std::string("guard word tripped (code ") + std::to_string(g) +
+                                        ") and clearing it failed: " + hipGetErrorString(me) +
+                                        "; the context is unusable"};
+        }
+      }
       const std::string who = " on rank " + std::to_string(sharded ? r : rank);
       if (g & GUARD_HEAD_RANGE)
         throw Err{SEZKP_E_INVALID, "a block's head position leaves the i32 range" + who +
@@ -1279,7 +1366,8 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   // all-to-all, P-point DFTs + twiddle, one all-to-all, a local (n/P)-point
   // INTT, then the allgather every rank's coset needs anyway; rank g's rows
   // are [g n/P, (g+1) n/P), n >= 4096 P). Round 5's per-rank cost model
-  // prefers the replicated INTT at every P (profiles/r05/intt_ab.txt: two
+  // prefers the replicated INTT at every P (profiles/r05/ab/intt_{replicated,
+  // distributed}_detail.json: two
   // collectives fewer outweigh (P - 1)/P of a 2^21-point INTT; P = 8 1.204
   // -> 1.132 ms predicted), so it is the default.
   const bool dist_intt = sharded && world > 1 && getenv("SEZKP_DIST_INTT") && atoi(getenv("SEZKP_DIST_INTT")) != 0;
@@ -1605,9 +1693,11 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   mark("col_open");
   HIP_OR_THROW(hipEventRecord(ev_fold, st));
   HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+  if (stage_ev) HIP_OR_THROW(hipEventRecord(oev[0], st2));
   ok(launch_col_open(st2, T, d_tmpl, d_outer, outer_stride, logChunks, req + 3 * max_fri_req, (int)no, PL, d_tabs,
                      d_dlev, d_dplans, d_dtabs, d_dcols, nullptr),
      "col_open");
+  if (stage_ev) HIP_OR_THROW(hipEventRecord(oev[1], st2));
   rec(ST_OPEN + 1);
   mark("col_open_issued");
   if (!sharded) HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.fr_off, hipMemcpyDeviceToHost, st2));
@@ -1639,6 +1729,11 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
       float ms = 0;
       if (hipEventElapsedTime(&ms, ev[s], ev[s + 1]) == hipSuccess) stage_ms[s] = ms;
     }
+    // col_openings = the openings kernel's own time on the side stream (it
+    // overlaps fri_paths); the host's query round trip before it (roots D2H,
+    // transcript, requests) falls in no stage, only in `total`
+    float oms = 0;
+    stage_ms[ST_OPEN] = hipEventElapsedTime(&oms, oev[0], oev[1]) == hipSuccess ? oms : 0.0;
     float tot = 0;
     (void)hipEventElapsedTime(&tot, ev[0], ev[ST_NSTAGE]);
     stage_ms[ST_NSTAGE] = tot;
@@ -1720,6 +1815,7 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     HIP_OR_THROW(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto& e : c->ev) HIP_OR_THROW(hipEventCreate(&e));
     for (auto& e : c->kev) HIP_OR_THROW(hipEventCreate(&e));
+    for (auto& e : c->oev) HIP_OR_THROW(hipEventCreate(&e));
     HIP_OR_THROW(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_fold, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));

@@ -18,6 +18,7 @@ SEZKP_E_NOMEM = -3
 SEZKP_E_DECODE = -4
 SEZKP_E_VERIFY = -5
 SEZKP_FLAG_STREAMING = 1
+ABI_VERSION = 4  # include/sezkp_stark.h SEZKP_ABI_VERSION: the layouts this module binds
 
 # every symbol include/sezkp_stark.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -96,6 +97,9 @@ def _load():
         raise ImportError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` (or __graft_entry__.build())")
     L = C.CDLL(LIB_PATH)
     L.sezkp_abi_version.restype = C.c_uint32
+    if L.sezkp_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has C ABI {L.sezkp_abi_version()}, this module binds ABI {ABI_VERSION}: "
+                          f"rebuild it (make -C {PKG_ROOT})")
     L.sezkp_version.restype = C.c_char_p
     L.sezkp_buf_free.argtypes = [C.POINTER(Buf)]
     E = [C.c_char_p, C.c_size_t]

@@ -40,6 +40,44 @@ for p in (PKG, ORACLE):
         sys.path.insert(0, p)
 
 
+def insert_zero_step_blocks(blocks, at):
+    """A BlockSoA with zero-step blocks (step_hi = step_lo - 1, no steps)
+    inserted before the block indices in `at` (n_blocks = after the last),
+    copying a neighbour's windows and offsets. The reference gives them 0 rows
+    and skips them (columns.rs:254-257,281-284; RowIter openings.rs:209-238),
+    so with the same manifest root the proof is the one of `blocks`."""
+    import numpy as np
+    import sezkp_amd
+    nb, tau = blocks.n_blocks, blocks.tau
+    src, lo = [], []
+    for i in range(nb + 1):
+        for _ in range(at.count(i)):
+            src.append(-1 - min(i, nb - 1))  # a zero-step copy of block min(i, nb - 1)
+            lo.append(int(blocks.step_hi[i - 1]) + 1 if i else int(blocks.step_lo[0]))
+        if i < nb:
+            src.append(i)
+            lo.append(None)
+    arr = {}
+    for f in ("version", "block_id", "step_lo", "step_hi", "ctrl_in", "ctrl_out", "in_head_in", "in_head_out"):
+        a = getattr(blocks, f)
+        arr[f] = np.array([a[j if j >= 0 else -1 - j] for j in src], dtype=a.dtype)
+    for k, j in enumerate(src):
+        if j < 0:
+            arr["block_id"][k] = 1000 + k
+            arr["step_lo"][k] = np.uint64(lo[k])
+            arr["step_hi"][k] = np.uint64(lo[k]) - np.uint64(1)
+    for f in ("win_left", "win_right", "off_in", "off_out"):
+        a = getattr(blocks, f).reshape(nb, tau)
+        arr[f] = np.concatenate([a[j if j >= 0 else -1 - j][None] for j in src]).reshape(-1)
+    ss = [0]
+    for j in src:
+        ss.append(ss[-1] + (int(blocks.step_start[j + 1] - blocks.step_start[j]) if j >= 0 else 0))
+    arr["step_start"] = np.array(ss, np.uint64)
+    for f in ("input_mv", "mv", "has_write", "wsym"):
+        arr[f] = getattr(blocks, f)
+    return sezkp_amd.BlockSoA(tau, **arr)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
 

@@ -11,7 +11,7 @@ import sys
 
 import pytest
 
-from conftest import ORACLE, PKG, free_port
+from conftest import ORACLE, PKG, free_port, insert_zero_step_blocks
 
 pytestmark = pytest.mark.gpu
 
@@ -20,7 +20,7 @@ def _port():
     return free_port()
 
 
-def _worker(rank, world, port, T, b, tau, seed, q):
+def _worker(rank, world, port, T, b, tau, seed, q, zero_at=None):
     sys.path[:0] = [PKG, ORACLE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -28,6 +28,8 @@ def _worker(rank, world, port, T, b, tau, seed, q):
     try:
         import sezkp_amd
         blocks = sezkp_amd.synthetic_blocks(T, b, tau, seed)
+        if zero_at:
+            blocks = insert_zero_step_blocks(blocks, zero_at)
         ctx = sezkp_amd.ShardedProverContext(rank, world, device=0, comm="host")
         ctx.upload(blocks)
         root = blocks.manifest_root()
@@ -43,12 +45,12 @@ def _worker(rank, world, port, T, b, tau, seed, q):
         dist.destroy_process_group()
 
 
-def _run(world, T, b, tau, seed):
+def _run(world, T, b, tau, seed, zero_at=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, T, b, tau, seed, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, T, b, tau, seed, q, zero_at)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=600) for _ in ps)
@@ -79,6 +81,18 @@ def test_sharded_proof_matches_oracle(gpu_ok, product, oracle, world, T, b, tau,
         assert {"col_chunk_roots", "d_values", "layer0_run_roots", "fri_rep_values", "fri_run_roots",
                 "proof_allreduce"} | ({"lde_alltoall"} if a2a else set()) == set(st), sorted(st)
         assert all(c["bytes"] > 0 and c["ms"] >= 0 for c in calls["stats"])
+
+
+def test_sharded_zero_step_blocks_match_oracle(gpu_ok, product, oracle):
+    """Zero-step blocks at rank boundaries of a P = 4 sharded proof (the
+    blocks a rank reads are found from step_start, where they repeat a
+    boundary): every rank returns the oracle's bytes."""
+    T, b, tau, seed = 1 << 14, 512, 3, 7
+    at = [0, 8, 8, 16, 24, 32]  # 4096-row shards start at blocks 8, 16, 24
+    blocks = insert_zero_step_blocks(product.synthetic_blocks(T, b, tau, seed), at)
+    want = hashlib.sha256(oracle.prove_v1(blocks, blocks.manifest_root())).hexdigest()
+    for rank, digest, repeat_ok, _ in _run(4, T, b, tau, seed, at):
+        assert digest == want and repeat_ok, f"rank {rank}: {digest}"
 
 
 @pytest.mark.parametrize("T,tau,seed", [(1 << 22, 8, 5), (1 << 21, 2, 6)])

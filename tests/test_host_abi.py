@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol(product):
     missing = [s for s in sorted(declared) if not hasattr(lib, s)]
     assert not missing, missing
     assert declared == set(product._lib.EXPORTS)
-    assert lib.sezkp_abi_version() == 3
+    assert lib.sezkp_abi_version() == 4
 
 
 def test_cbor_decode_matches_oracle_decode(product, oracle):
@@ -233,3 +233,19 @@ def test_block_step_start_checked_on_host(product):
     b.step_start[:] += 32
     with pytest.raises(product.SezkpError, match="step_start"):
         b.check_shape()
+
+
+def test_zero_step_blocks_host_side(product, oracle):
+    """Blocks of zero steps (step_hi = step_lo - 1) on the host side of the
+    boundary: the BlockSoA helper gives the oracle's blocks, the manifest
+    commits to every block (leaf_hash has steps.len() = 0; product root ==
+    oracle root), the CBOR codec round-trips them."""
+    from conftest import insert_zero_step_blocks
+    b = product.synthetic_blocks(1 << 10, 100, 3, 5)
+    zb = insert_zero_step_blocks(b, [0, 4, 4, b.n_blocks])
+    assert zb.n_blocks == b.n_blocks + 4 and zb.n_rows == b.n_rows
+    zb.check_shape()
+    assert zb.manifest_root() == oracle.manifest_root(zb) != b.manifest_root()
+    rt = product.BlockSoA.from_cbor(zb.to_cbor())
+    assert rt.manifest_root() == zb.manifest_root()
+    assert (rt.step_hi == zb.step_hi).all() and (rt.step_start == zb.step_start).all()

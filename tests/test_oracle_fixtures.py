@@ -98,6 +98,45 @@ def test_v1_two_oracles_agree_with_golden(oracle, name):
     assert len(c) == gold["proof_len"]
 
 
+def with_zero_step_blocks(dicts, at):
+    """The blocks with zero-step blocks inserted before the indices in `at`
+    (len(dicts) = after the last): step_hi = step_lo - 1, no steps, the windows
+    and offsets of a neighbour. The reference counts them as 0 rows and skips
+    them (columns.rs:254-257,281-284; RowIter openings.rs:209-238)."""
+    import copy
+    out = []
+    for i in range(len(dicts) + 1):
+        for _ in range(at.count(i)):
+            nb = copy.deepcopy(dicts[min(i, len(dicts) - 1)])
+            lo = dicts[i - 1]["step_hi"] + 1 if i else dicts[0]["step_lo"]
+            nb.update(block_id=1000 + len(out), step_lo=lo, step_hi=lo - 1)
+            nb["movement_log"] = dict(nb["movement_log"], steps=[])
+            out.append(nb)
+        if i < len(dicts):
+            out.append(dicts[i])
+    return out
+
+
+ZERO_AT = [0, 3, 3, 8]  # first, two in a row in the middle, last
+
+
+@pytest.mark.parametrize("name", sorted(SETS))
+def test_v1_zero_step_blocks_two_oracles(oracle, name):
+    """Blocks of zero steps contribute no rows: with the same manifest root the
+    proof is the golden proof of the blocks without them, in both oracles."""
+    import sezkp_oracle_py as PY
+    blocks, man, _ = _load(name)
+    mroot = bytes(man["root"])
+    zb = with_zero_step_blocks(blocks, ZERO_AT)
+    assert len(zb) == len(blocks) + len(ZERO_AT)
+    c = oracle.prove_v1(oracle.Blocks(zb), mroot)
+    assert c == PY.prove_v1(zb, mroot)
+    gold = json.load(open(os.path.join(GOLDEN, "v1_proofs.json")))[name]
+    assert hashlib.sha256(c).hexdigest() == gold["proof_sha256"]
+    # the manifest still commits to every block (leaf_hash has steps.len() = 0)
+    assert oracle.manifest_root(oracle.Blocks(zb)) != mroot
+
+
 def test_v1_two_oracles_agree_synthetic(oracle, product):
     import sezkp_oracle_py as PY
     b = product.synthetic_blocks(128, 32, 2, 9)

@@ -61,9 +61,10 @@ def test_fs_xof_random_streams_match_blake3(product, oracle, seed):
         assert g == oracle.blake3(stream[:p] + s, ol), (p, len(s), ol)
 
 
-def test_fs_xof_sizes_up_to_the_lds_limit(product, oracle):
-    """Every chunk count up to the 40 KB limit (single-chunk, exactly one
-    chunk, 2..39 chunks: each stack shape of the chunk-CV merges)."""
+def test_fs_xof_host_blake3_size_sweep(product, oracle):
+    """A size sweep of the host BLAKE3-XOF behind the transcript: stream
+    prefixes of 0..40 KB (single-chunk, exactly one chunk, 2..39 chunks: each
+    stack shape of the chunk-CV merges) against the oracle's BLAKE3."""
     rng = np.random.default_rng(7)
     stream = rng.bytes(40000)
     for base in range(0, 40000, 16 * 1024):
