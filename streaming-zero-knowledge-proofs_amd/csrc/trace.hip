@@ -1206,7 +1206,7 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
   }
 }
 
-constexpr int DICT_WG_ROWS = 64 << DICT_LANE_LOG;                    // 4096 rows per 64-lane WG
+constexpr int DICT_WG_ROWS = 64 << DICT_LANE_LOG;  // 4096: row0 / nrows alignment of a sliced commit
 constexpr int DICT_RANGE_STEP = TR_THREADS * 16;                     // rows per WG sweep
 
 // WG-wide min / max of one column's partial ranges (result valid on tid 0)
@@ -1471,16 +1471,27 @@ __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const
   }
 }
 
-// 64-lane WG = 4096 rows of one dictionary column (4 chunks): each lane folds
-// 64 rows to a level-6 node, 4 LDS levels give the 4 chunk roots, written as
-// leaves of the column's outer tree. Requires n >= 1024 (n % 64 == 0).
-__global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTemplate* __restrict__ tmpl,
-                                                        const DictCol* __restrict__ dcols,
-                                                        const DictPlan* __restrict__ plans,
-                                                        const uint32_t* __restrict__ tabs, uint32_t* __restrict__ outer,
-                                                        uint64_t outer_stride, uint64_t row0, uint64_t row_end,
-                                                        uint32_t* __restrict__ dlev) {
-  __shared__ uint32_t lds[8][64];
+// 256-lane WG (4 waves) = 2^(llog + 8) rows of one dictionary column: each
+// lane folds its 2^llog rows (llog = 6 + a) to one node in registers, and the
+// levels llog+1..10 of the WG's chunks are computed from an LDS image by the
+// first lanes of the WORKGROUP, so a level of 2^j parents keeps 2^j lanes of
+// whole waves busy (128 parents: waves 0-1, the others wait at the barrier
+// and leave their SIMD to other workgroups) instead of 32, 16, 8 of one
+// wave's 64 lanes (round 5's one-wave workgroups: a third of a wave's issue
+// slots at the upper levels went to idle lanes). Levels ping-pong between two
+// LDS images: one barrier per level. The chunk roots are written as leaves of
+// the column's outer tree. Requires n >= 1024; rows [row0, row_end) may end
+// inside a workgroup (small sharded slices): lanes and parents past row_end
+// are skipped (their LDS slots hold garbage that feeds only skipped parents).
+constexpr int DICT_WG_LANES = 256;
+__global__ void __launch_bounds__(DICT_WG_LANES) k_col_commit_dict(TraceDev T, const ColTemplate* __restrict__ tmpl,
+                                                                   const DictCol* __restrict__ dcols,
+                                                                   const DictPlan* __restrict__ plans,
+                                                                   const uint32_t* __restrict__ tabs,
+                                                                   uint32_t* __restrict__ outer, uint64_t outer_stride,
+                                                                   uint64_t row0, uint64_t row_end,
+                                                                   uint32_t* __restrict__ dlev) {
+  __shared__ uint32_t lds[2][8][DICT_WG_LANES];
   // (XCD-interleaved column orders, so that one XCD's workgroups gather
   // from one column's tables at a time, measured slower in rounds 1 and 3)
   const uint32_t by = blockIdx.y, bx = blockIdx.x;
@@ -1493,8 +1504,8 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
   // high-K columns give each lane more rows (fewer LDS levels per row)
   const int a = (int)P.a;
   const int llog = DICT_LANE_LOG + a;  // rows per lane (log2)
-  const uint64_t wg_row = row0 + ((uint64_t)bx << (llog + 6));
-  if (wg_row >= row_end) return;  // grid is sized for a = 0
+  const uint64_t wg_row = row0 + ((uint64_t)bx << (llog + 8));
+  if (wg_row >= row_end) return;  // grid is sized for a = 0 (uniform per WG: no barrier is skipped by half a WG)
   const uint64_t lrow = wg_row + ((uint64_t)lane << llog);
   const uint64_t nch_all = T.n >> COL_CHUNK_LOG2;
   uint32_t* dl = dlev + 8 * (uint64_t)by * nch_all * DLEV_NODES;
@@ -1517,44 +1528,43 @@ __global__ void __launch_bounds__(64) k_col_commit_dict(TraceDev T, const ColTem
         break;
     }
 #pragma unroll
-    for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
+    for (int w = 0; w < 8; w++) lds[0][w][lane] = h[w];
     // chunk levels llog..9 are kept for the openings (DLEV_NODES per chunk)
     node_store(dl + 8 * ((lrow >> COL_CHUNK_LOG2) * DLEV_NODES + dlev_base(llog) +
                          ((lrow >> llog) & ((1u << (COL_CHUNK_LOG2 - llog)) - 1))),
                h);
   }
   __syncthreads();
-  int cnt = 64;
+  int cnt = DICT_WG_LANES, cur = 0;
   for (int lv = llog + 1; lv <= COL_CHUNK_LOG2; lv++) {
     const int half = cnt >> 1;
-    uint32_t h[8];
-    const bool a2 = lane < half;
-    if (a2) {
-      uint32_t l[8], r[8];
+    // parent `lane` of this level covers rows from prow: skip it past row_end
+    const uint64_t prow = wg_row + ((uint64_t)lane << lv);
+    if (lane < half && prow < row_end) {
+      uint32_t l[8], r[8], h[8];
 #pragma unroll
       for (int w = 0; w < 8; w++) {
-        const uint2 pr = *reinterpret_cast<const uint2*>(&lds[w][2 * lane]);
+        const uint2 pr = *reinterpret_cast<const uint2*>(&lds[cur][w][2 * lane]);
         l[w] = pr.x;
         r[w] = pr.y;
       }
       b3_parent(l, r, h);
-    }
-    __syncthreads();
-    if (a2) {
 #pragma unroll
-      for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
-      const int per = 1 << (COL_CHUNK_LOG2 - lv);  // nodes of this level per chunk
-      const uint64_t chq = (wg_row >> COL_CHUNK_LOG2) + lane / per;
-      if (lv < COL_CHUNK_LOG2 && chq < nch_all) node_store(dl + 8 * (chq * DLEV_NODES + dlev_base(lv) + lane % per), h);
+      for (int w = 0; w < 8; w++) lds[cur ^ 1][w][lane] = h[w];
+      if (lv < COL_CHUNK_LOG2)
+        node_store(dl + 8 * ((prow >> COL_CHUNK_LOG2) * DLEV_NODES + dlev_base(lv) +
+                             ((prow >> lv) & ((1u << (COL_CHUNK_LOG2 - lv)) - 1))),
+                   h);
     }
     __syncthreads();
+    cur ^= 1;
     cnt = half;
   }
   // cnt chunk roots of this WG -> leaves of the column's outer tree
-  for (int i = lane; i < cnt * 8; i += 64) {
+  for (int i = lane; i < cnt * 8; i += DICT_WG_LANES) {
     const uint64_t ch = (wg_row >> COL_CHUNK_LOG2) + (i >> 3);
     if (ch < nch_all && (ch << COL_CHUNK_LOG2) < row_end)
-      outer[(uint64_t)dc.col * outer_stride * 8 + ch * 8 + (i & 7)] = lds[i & 7][i >> 3];
+      outer[(uint64_t)dc.col * outer_stride * 8 + ch * 8 + (i & 7)] = lds[cur][i & 7][i >> 3];
   }
 }
 
@@ -1618,8 +1628,9 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
   }
-  const unsigned gx = (unsigned)((nrows + DICT_WG_ROWS - 1) / DICT_WG_ROWS);
-  hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(64), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
+  const uint64_t wg_rows = (uint64_t)DICT_WG_LANES << DICT_LANE_LOG;  // rows of a WG at a = 0
+  const unsigned gx = (unsigned)((nrows + wg_rows - 1) / wg_rows);
+  hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(DICT_WG_LANES), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
                      outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev);
   return hipGetLastError();
 }
