@@ -863,13 +863,25 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_w8r8(NttPassArgs P) {
   }
 }
 
+// LDS slot of point e = 512 a + 64 b + 8 c + d of the 4096-point tile: the XOR
+// swizzle 512 a + 64 b + 8 (c ^ (b & 3)) + (d ^ c) (a permutation, no padding).
+// Every access of k_ntt_n12r8 is then conflict-free: a ds_read_b64 serves 32
+// lanes per LDS cycle (bank = slot mod 32 must differ) and a ds_write_b64 16
+// lanes (slot mod 16); the half-wave sets are (c low 2 bits, d), (b low 2
+// bits, d) and (b low 2 bits, c), each mapped one to one onto the bank bits
+// (round 5's pad e + e / 8 cost 31% of the LDS cycles in conflicts).
+__device__ __forceinline__ int n12_slot(int e) {
+  const int b = (e >> 6) & 7, c = (e >> 3) & 7, d = e & 7;
+  return (e & ~63) | ((c ^ (b & 3)) << 3) | (d ^ c);
+}
+
 // Narrow DIF pass of 12 stages on 4096 contiguous points (sL = 0),
 // 4096 = 8^4: lane g < 512; the natural-order store (nat_out): position
 // p = 4096 tile + e goes to out[bitrev(p)] * out_scale (workgroup order as
 // k_ntt4's nat_out).
 template <bool INV>
 __global__ void __launch_bounds__(R8_NT, 2) k_ntt_n12r8(NttPassArgs P) {
-  __shared__ uint64_t sh[4096 + 512];
+  __shared__ uint64_t sh[4096];
   const int g = threadIdx.x;
   const NttTables& T = P.tw;
   const uint64_t tile = nat_tile(blockIdx.x, gridDim.x);
@@ -885,36 +897,36 @@ __global__ void __launch_bounds__(R8_NT, 2) k_ntt_n12r8(NttPassArgs P) {
   fft_dif_regs<3, INV>(x);
   if (g) r8_twiddle(x, w1);
 #pragma unroll
-  for (int q = 0; q < 8; q++) sh[r8_pad(g + 512 * q)] = x[q];
+  for (int q = 0; q < 8; q++) sh[n12_slot(g + 512 * q)] = x[q];
   __syncthreads();
   // stages 8..0 stay inside 512-point block g >> 6: wave w's own block, so
   // the exchanges below are between lanes of one wave
   {  // stages 8..6 (stride 64)
     const int base = (g >> 6) * 512 + lo2;
 #pragma unroll
-    for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(base + 64 * d)];
+    for (int d = 0; d < 8; d++) x[d] = sh[n12_slot(base + 64 * d)];
     fft_dif_regs<3, INV>(x);
     if (lo2) r8_twiddle(x, w2);
 #pragma unroll
-    for (int d = 0; d < 8; d++) sh[r8_pad(base + 64 * d)] = x[d];
+    for (int d = 0; d < 8; d++) sh[n12_slot(base + 64 * d)] = x[d];
   }
   wave_lds_sync();
   {  // stages 5..3 (stride 8), twiddles w_64^(lo k): shifts
     const int lo = g & 7, base = (g >> 3) * 64 + lo;
 #pragma unroll
-    for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(base + 8 * d)];
+    for (int d = 0; d < 8; d++) x[d] = sh[n12_slot(base + 8 * d)];
     fft_dif_regs<3, INV>(x);
     if (lo) {
 #pragma unroll
       for (int k = 1; k < 8; k++) x[rev<3>(k)] = gl_mul_pow2(x[rev<3>(k)], tw_exp64<INV>(lo * k));
     }
 #pragma unroll
-    for (int d = 0; d < 8; d++) sh[r8_pad(base + 8 * d)] = x[d];
+    for (int d = 0; d < 8; d++) sh[n12_slot(base + 8 * d)] = x[d];
   }
   wave_lds_sync();
   // stages 2..0 on 8 consecutive points
 #pragma unroll
-  for (int d = 0; d < 8; d++) x[d] = sh[r8_pad(8 * g + d)];
+  for (int d = 0; d < 8; d++) x[d] = sh[n12_slot(8 * g + d)];
   fft_dif_regs<3, INV>(x);
   const int sh_r = 32 - P.nat_logN;
   const bool scale = P.out_scale > 1;
