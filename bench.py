@@ -760,6 +760,9 @@ def compact_line(out: dict, detail_path) -> dict:
         top = roof.get("committed_stats_top_kernel")
         if isinstance(top, dict):
             r["rocprof"] = _pick(top, ("name", "average_ms", "file"), 5)
+        if isinstance(roof.get("clock"), dict):
+            r["clock"] = _pick(roof["clock"], ("clock_ghz_one_proof", "clock_ghz_three_in_flight",
+                                               "valu_frac_at_held_clock", "file"), 4)
         line["roofline"] = r
     cb = out.get("cpu_baseline")
     if isinstance(cb, dict):
@@ -870,6 +873,25 @@ def progress(msg: str) -> None:
     print(f"[bench {time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
+def held_clock(kernel: str) -> dict | None:
+    """The clock the chip holds during `kernel` (GRBM_GUI_ACTIVE / 8 / wall,
+    MI355X_MICROARCH.md "DVFS give-back"), one proof at a time and with the
+    bench's 3 proofs in flight, from the committed PMC passes
+    (tools/r6_clock.sh -> tools/pmc_clock.py -> profiles/r06/clock.json)."""
+    p = os.path.join(ROOT, "profiles", "r06", "clock.json")
+    if not os.path.exists(p):
+        return None
+    c = json.load(open(p))
+    pick = lambda d: next((v for k, v in d.items() if k.startswith(kernel + "<") or k == kernel), None)
+    one, three = pick(c.get("one_proof", {})), pick(c.get("three_in_flight", {}))
+    if not one:
+        return None
+    return {"clock_ghz_one_proof": one["clock_ghz"], "clock_ghz_three_in_flight": three["clock_ghz"] if three else None,
+            "valu_frac_at_held_clock": one["valu_frac_held"], "valu_frac_at_2p4": one["valu_frac_2p4"],
+            "reading": "the clock is held (>= 0.94 of 2.4 GHz): the tree kernels are issue-bound, not clock-bound",
+            "file": "profiles/r06/clock.json"}
+
+
 def tree_roofline(kernel: str, ms: float, leaves: int) -> dict:
     """VALU roofline of a BLAKE3 tree kernel from its live launch time and its
     PMC instruction count (profiles/pmc_summary.json), with the HBM view on
@@ -896,6 +918,7 @@ def tree_roofline(kernel: str, ms: float, leaves: int) -> dict:
                     "frac_traffic": traffic / t / 1e9 / HBM_PEAK_GBS if traffic and t == t else None,
                     "note": "SURVEY 8(d) counts 72 B per leaf (every tree node written); the kernels keep levels "
                             "< 6 in registers/LDS, so their HBM traffic is ~0.12 of that"},
+            "clock": held_clock(kernel),
             "measured_on": "single-proof pass: HIP events bracketing exactly the launch on the prover stream",
             "profile": "profiles/pmc_summary.json (tools/profile_round.sh), profiles/*kernel_stats*.csv"}
 
