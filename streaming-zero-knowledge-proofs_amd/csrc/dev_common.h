@@ -198,6 +198,62 @@ __device__ __forceinline__ void b3_parent(const uint32_t (&l)[8], const uint32_t
   b3_hash_block(m, 64, out);
 }
 
+// ------------------------------------------------ BLAKE3 on a quad of lanes
+// One parent compression by four lanes (q = lane & 3): lane q holds column q
+// of the state (v[q], v[4 + q], v[8 + q], v[12 + q]) and runs the G of that
+// column; rows 1..3 are then rotated left by 1..3 lanes (DPP quad_perm) so the
+// same lane runs the G of diagonal q, and rotated back. For the narrow top
+// levels of a tree (fewer parents than lanes) a dependent chain of
+// compressions then costs a quarter of the instructions per lane of the
+// one-lane form. Message word k of round R for this lane is word
+// b3_quad_word(R, k, q) of the 16-word message (k = 0, 1: the column G,
+// 2, 3: the diagonal G). Output: words q and 4 + q of the parent.
+__host__ __device__ constexpr uint32_t b3_quad_pack(int R, int k) {  // 4-bit word index per q
+  uint32_t p = 0;
+  for (int q = 0; q < 4; q++) p |= (uint32_t)b3_sigma(R, (k >= 2 ? 8 : 0) + 2 * q + (k & 1)) << (4 * q);
+  return p;
+}
+__device__ __forceinline__ int b3_quad_word(int R, int k, int q) {
+  return (int)((b3_quad_pack(R, k) >> (4 * q)) & 15u);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_rot(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_QROT1 = 0x39;  // quad_perm(1,2,3,0): lane q reads lane q+1
+constexpr int DPP_QROT2 = 0x4E;  // quad_perm(2,3,0,1)
+constexpr int DPP_QROT3 = 0x93;  // quad_perm(3,0,1,2)
+__device__ __forceinline__ void b3_g1(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t mx, uint32_t my) {
+  a = a + b + mx;
+  d = rotr32(d ^ a, 16);
+  c = c + d;
+  b = rotr32(b ^ c, 12);
+  a = a + b + my;
+  d = rotr32(d ^ a, 8);
+  c = c + d;
+  b = rotr32(b ^ c, 7);
+}
+// mw[R][k]: the message words of this lane (see b3_quad_word); whole quads
+// must be active (DPP reads the other three lanes)
+__device__ __forceinline__ void b3_parent_quad(const uint32_t (&mw)[7][4], int q, uint32_t& h_lo, uint32_t& h_hi) {
+  const uint32_t iv_a = q == 0 ? B3_IV0 : q == 1 ? B3_IV1 : q == 2 ? B3_IV2 : B3_IV3;
+  const uint32_t iv_b = q == 0 ? B3_IV4 : q == 1 ? B3_IV5 : q == 2 ? B3_IV6 : B3_IV7;
+  uint32_t a = iv_a, b = iv_b, c = iv_a, d = q == 2 ? 64u : q == 3 ? B3_ROOT_FLAGS : 0u;
+#pragma unroll
+  for (int R = 0; R < 7; R++) {
+    b3_g1(a, b, c, d, mw[R][0], mw[R][1]);
+    b = quad_rot<DPP_QROT1>(b);
+    c = quad_rot<DPP_QROT2>(c);
+    d = quad_rot<DPP_QROT3>(d);
+    b3_g1(a, b, c, d, mw[R][2], mw[R][3]);
+    b = quad_rot<DPP_QROT3>(b);
+    c = quad_rot<DPP_QROT2>(c);
+    d = quad_rot<DPP_QROT1>(d);
+  }
+  h_lo = a ^ c;
+  h_hi = b ^ d;
+}
+
 // ------------------------------------------------------------ node helpers
 __device__ __forceinline__ void node_load(const uint32_t* __restrict__ p, uint32_t (&h)[8]) {
   const uint4* q = reinterpret_cast<const uint4*>(p);

@@ -42,14 +42,59 @@ __device__ __forceinline__ void lds_pair(uint32_t (*lds)[W], int i, uint32_t (&l
   }
 }
 
+// words q and 4 + q of node idx at level l (a quad's share of store_level)
+__device__ __forceinline__ void store_level_quad(const TreeDev& T, int l, uint64_t idx, int q, uint32_t lo,
+                                                 uint32_t hi) {
+  if (l >= T.lstore && l <= T.logLen) {
+    uint32_t* p = T.nodes + 8 * (tree_level_off(T.logLen, T.lstore, l) + idx);
+    p[q] = lo;
+    p[4 + q] = hi;
+  }
+  if (l == T.logLen) {
+    T.root[q] = lo;
+    T.root[4 + q] = hi;
+  }
+}
+
 // Reduce `cnt` level-`lvl` nodes in LDS to one; WG-local node i at level l has
-// global index wg * (cnt_at_l) + i.
-template <int W>
+// global index wg * (cnt_at_l) + i. A level of at most W / 4 parents runs one
+// parent per quad of lanes (b3_parent_quad): the chain of the last levels is
+// latency-bound, and a quad's compression is a quarter of the instructions
+// per lane of a one-lane compression (round 6). QUAD = false keeps one lane
+// per parent (the throughput-bound tree kernels, whose occupancy is set by
+// their VGPRs: the quad form's 28 message words would cost them waves).
+template <int W, bool QUAD = false>
 __device__ __forceinline__ void wg_reduce(uint32_t (*lds)[W], int cnt, int lvl, uint64_t wg, const TreeDev& T,
                                           int stop = 64) {
   const int tid = threadIdx.x;
   while (cnt > 1 && lvl < stop) {
     const int half = cnt >> 1;
+    if (QUAD && 4 * half <= W) {
+      const int pq = tid >> 2, q = tid & 3;
+      const bool act = pq < half;  // whole quads
+      uint32_t lo = 0, hi = 0;
+      if (act) {
+        uint32_t mw[7][4];
+#pragma unroll
+        for (int R = 0; R < 7; R++)
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int j = b3_quad_word(R, k, q);  // message word j: word j & 7 of child j >> 3
+            mw[R][k] = lds[j & 7][2 * pq + (j >> 3)];
+          }
+        b3_parent_quad(mw, q, lo, hi);
+      }
+      __syncthreads();
+      lvl++;
+      cnt = half;
+      if (act) {
+        lds[q][pq] = lo;
+        lds[4 + q][pq] = hi;
+        store_level_quad(T, lvl, wg * (uint64_t)cnt + pq, q, lo, hi);
+      }
+      __syncthreads();
+      continue;
+    }
     uint32_t h[8];
     const bool act = tid < half;
     if (act) {
@@ -221,7 +266,9 @@ __device__ __forceinline__ void upper_wg(const TreeDev& T, int from, uint64_t wg
   const int top = (to > 0 && to < T.logLen) ? to : T.logLen;
   const int cnt_log = top - from;
   const int sub_log = cnt_log < 10 ? cnt_log : 10;
-  const int logper = cnt_log < 2 ? cnt_log : 2;
+  // up to 256 nodes: one per lane, every level in wg_reduce (its quad levels
+  // take over from 64 parents down); more: 4 per lane, 2 levels in registers
+  const int logper = cnt_log <= 8 ? 0 : 2;
   const int nact = 1 << (sub_log - logper);
   const uint32_t* src = T.nodes + 8 * tree_level_off(T.logLen, T.lstore, from);
   if (tid < nact) {
@@ -252,7 +299,7 @@ __device__ __forceinline__ void upper_wg(const TreeDev& T, int from, uint64_t wg
     lds_put(lds, tid, h);
   }
   __syncthreads();
-  wg_reduce(lds, nact, from + logper, wg, T);
+  wg_reduce<MK_THREADS, true>(lds, nact, from + logper, wg, T);
 }
 
 // grid.y indexes trees of identical shape spaced tree_stride nodes apart.
@@ -454,7 +501,7 @@ __global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
     lds_put(lds, tid, h);
   }
   __syncthreads();
-  wg_reduce(lds, nact, lp, 0, T);
+  wg_reduce<TAIL_THREADS, true>(lds, nact, lp, 0, T);
 }
 
 // The same small-layer job as k_fri_tail, run by the first workgroups of the
