@@ -254,6 +254,21 @@ __device__ __forceinline__ void b3_parent_quad(const uint32_t (&mw)[7][4], int q
   h_hi = b ^ d;
 }
 
+// Parent pq of the LDS image's nodes 2 pq, 2 pq + 1 on the quad of lanes
+// q = lane & 3 (b3_parent_quad): words q and 4 + q in lo / hi.
+template <int W>
+__device__ __forceinline__ void lds_parent_quad(uint32_t (*lds)[W], int pq, int q, uint32_t& lo, uint32_t& hi) {
+  uint32_t mw[7][4];
+#pragma unroll
+  for (int R = 0; R < 7; R++)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int j = b3_quad_word(R, k, q);  // message word j: word j & 7 of child j >> 3
+      mw[R][k] = lds[j & 7][2 * pq + (j >> 3)];
+    }
+  b3_parent_quad(mw, q, lo, hi);
+}
+
 // ------------------------------------------------------------ node helpers
 __device__ __forceinline__ void node_load(const uint32_t* __restrict__ p, uint32_t (&h)[8]) {
   const uint4* q = reinterpret_cast<const uint4*>(p);

@@ -73,17 +73,7 @@ __device__ __forceinline__ void wg_reduce(uint32_t (*lds)[W], int cnt, int lvl, 
       const int pq = tid >> 2, q = tid & 3;
       const bool act = pq < half;  // whole quads
       uint32_t lo = 0, hi = 0;
-      if (act) {
-        uint32_t mw[7][4];
-#pragma unroll
-        for (int R = 0; R < 7; R++)
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const int j = b3_quad_word(R, k, q);  // message word j: word j & 7 of child j >> 3
-            mw[R][k] = lds[j & 7][2 * pq + (j >> 3)];
-          }
-        b3_parent_quad(mw, q, lo, hi);
-      }
+      if (act) lds_parent_quad(lds, pq, q, lo, hi);
       __syncthreads();
       lvl++;
       cnt = half;
@@ -709,20 +699,34 @@ __global__ void __launch_bounds__(64) k_fri_paths(const FriLayerDev* __restrict_
     for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
   }
   __syncthreads();
+  // the group's levels 1..glog-1 (its root, level glog, is not on the path):
+  // 32 parents one per lane, then 16, 8, 4, 2 on quads of lanes (round 6)
   int cnt = (int)g;
   for (int lvl = 0; lvl < glog; lvl++) {
     const int sib = (int)(((li - base) >> lvl) ^ 1);
     if (lane < 8) o[4 + 8 * lvl + lane] = lds[lane][sib];
+    if (lvl + 1 == glog) break;
     const int half = cnt >> 1;
-    uint32_t h[8];
-    if (lane < half) {
-      uint32_t a[8], b[8];
-      for (int w = 0; w < 8; w++) { a[w] = lds[w][2 * lane]; b[w] = lds[w][2 * lane + 1]; }
-      b3_parent(a, b, h);
+    if (4 * half <= 64) {
+      const int pq = lane >> 2, q = lane & 3;
+      uint32_t lo = 0, hi = 0;
+      if (pq < half) lds_parent_quad(lds, pq, q, lo, hi);
+      __syncthreads();
+      if (pq < half) {
+        lds[q][pq] = lo;
+        lds[4 + q][pq] = hi;
+      }
+    } else {
+      uint32_t h[8];
+      if (lane < half) {
+        uint32_t a[8], b[8];
+        for (int w = 0; w < 8; w++) { a[w] = lds[w][2 * lane]; b[w] = lds[w][2 * lane + 1]; }
+        b3_parent(a, b, h);
+      }
+      __syncthreads();
+      if (lane < half)
+        for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
     }
-    __syncthreads();
-    if (lane < half)
-      for (int w = 0; w < 8; w++) lds[w][lane] = h[w];
     __syncthreads();
     cnt = half;
   }

@@ -1142,21 +1142,22 @@ __global__ void __launch_bounds__(TR_THREADS) k_col_open(TraceDev T, const ColTe
     __syncthreads();
     const uint64_t gin = (row - gstart) >> K;
     int cnt = 1 << D;
+    // levels K+1 .. glog-1 of the group (its root, level glog, was stored by
+    // the commitment): <= 32 parents, each on a quad of lanes (round 6: the
+    // chain is latency-bound; b3_parent_quad)
     for (int lvl = K; lvl < glog; lvl++) {
       const int sib = (int)((gin >> (lvl - K)) ^ 1);
       if (tid < 8) o[18 + 8 * lvl + tid] = lds[tid][sib];
+      if (lvl + 1 == glog) break;
       const int half = cnt >> 1;
-      uint32_t hh[8];
-      if (tid < half) {
-        uint32_t a[8], b[8];
-#pragma unroll
-        for (int w = 0; w < 8; w++) { a[w] = lds[w][2 * tid]; b[w] = lds[w][2 * tid + 1]; }
-        b3_parent(a, b, hh);
-      }
+      const int pq = tid >> 2, qq = tid & 3;
+      uint32_t lo = 0, hi = 0;
+      if (pq < half) lds_parent_quad(lds, pq, qq, lo, hi);
       __syncthreads();
-      if (tid < half)
-#pragma unroll
-        for (int w = 0; w < 8; w++) lds[w][tid] = hh[w];
+      if (pq < half) {
+        lds[qq][pq] = lo;
+        lds[4 + qq][pq] = hi;
+      }
       __syncthreads();
       cnt = half;
     }
