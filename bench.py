@@ -910,7 +910,7 @@ def tree_roofline(kernel: str, ms: float, leaves: int) -> dict:
                               "rate) / 4 cycles (half rate) per wave64 instruction (profiles/r02_isa_k_layer16.txt)",
             "peak_basis": "MI355X_MICROARCH.md: 256 CU x 4 SIMD, one wave64 VALU instruction per 2 cycles per SIMD, "
                           "2.4 GHz. BLAKE3's rotates (v_alignbit) and 3-input adds issue at half rate on gfx950 "
-                          "(tools/valu_rates.hip), so a saturated tree kernel stays below 1.0",
+                          "(tools/micro/valu_rates.hip), so a saturated tree kernel stays below 1.0",
             "hbm": {"alg_bytes_per_launch": alg, "achieved_alg_GBs": alg / t / 1e9 if t == t else None,
                     "frac_alg": alg / t / 1e9 / HBM_PEAK_GBS if t == t else None,
                     "traffic_bytes_per_launch": traffic,

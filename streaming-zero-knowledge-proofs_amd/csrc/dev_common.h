@@ -21,7 +21,7 @@ constexpr uint64_t GL_EPS = 0xffffffffULL;  // 2^64 mod p
 // ------------------------------------------------------------------ Goldilocks
 // Carry-chain forms: 64-bit adds/subs as v_add_co/v_addc (v_sub_co/v_subb)
 // pairs whose carry feeds a select, instead of 64-bit compares + cndmask
-// (which also cost s_nop hazards on gfx950). tools/gl_variants.hip measures
+// (which also cost s_nop hazards on gfx950). tools/micro/gl_variants.hip measures
 // them bit-identical to the compare forms and 1.2-1.6x faster.
 __device__ __forceinline__ uint64_t add64c(uint64_t a, uint64_t b, uint32_t& carry) {
   uint32_t c0;
@@ -137,7 +137,7 @@ __host__ __device__ constexpr int b3_sigma(int r, int i) {
 // alignbit, 4 add, ...) instead of the compiler's interleave of half-rate
 // (add3, alignbit) and full-rate (xor, add) instructions: on gfx950 a mix
 // issues as if every instruction were half rate, runs of one kind do not
-// (tools/valu_mix.hip; tools/b3_sched.hip: 57.3 -> 61.1 G parent
+// (tools/micro/valu_mix.hip; tools/micro/b3_sched.hip: 57.3 -> 61.1 G parent
 // compressions/s at 8 waves per SIMD, 57.0 -> 58.9 at 4).
 #define B3_FENCE(v)                                                                                         \
   asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),   \

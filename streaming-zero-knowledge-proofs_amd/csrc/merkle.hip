@@ -250,8 +250,24 @@ __global__ void __launch_bounds__(MK_THREADS) k_leaf_subtree(const uint64_t* __r
 // Input: stored level `from` (count 2^(logLen-from)); one WG reduces up to
 // 1024 nodes (4 per lane, 2 levels in registers) and stores every level, up
 // to level `to` (0: the root).
+// node g of level `from`: stored, or (a sharded cap's first pass) taken from
+// the allgathered run roots and stored at its cap position
+struct GathSrc {  // a sharded cap's first pass: the allgathered run roots (UpperJob)
+  const uint32_t* gath;
+  uint64_t nrun;
+  int logP;
+};
+__device__ __forceinline__ void upper_load(const uint32_t* src, const GathSrc& gs, uint64_t g, uint32_t (&h)[8]) {
+  if (gs.gath) node_load(gs.gath + 8 * ((g & ((1ULL << gs.logP) - 1)) * gs.nrun + (g >> gs.logP)), h);
+  else node_load(src + 8 * g, h);
+}
+__device__ __forceinline__ void upper_src(const TreeDev& T, const uint32_t* src, const GathSrc& gs, int from,
+                                          uint64_t g, uint32_t (&h)[8]) {
+  upper_load(src, gs, g, h);
+  if (gs.gath) store_level(T, from, g, h);
+}
 __device__ __forceinline__ void upper_wg(const TreeDev& T, int from, uint64_t wg, uint32_t (*lds)[MK_THREADS],
-                                         int to = 0) {
+                                         int to = 0, GathSrc gj = GathSrc{nullptr, 0, 0}) {
   const int tid = threadIdx.x;
   const int top = (to > 0 && to < T.logLen) ? to : T.logLen;
   const int cnt_log = top - from;
@@ -265,25 +281,34 @@ __device__ __forceinline__ void upper_wg(const TreeDev& T, int from, uint64_t wg
     const uint64_t g = (wg << (sub_log - logper)) + tid;  // node index at level from+logper
     uint32_t h[8];
     if (logper == 2) {
-      uint32_t a[8], b[8], p0[8], p1[8];
-      node_load(src + 8 * (4 * g + 0), a);
-      node_load(src + 8 * (4 * g + 1), b);
+      // the four loads first, then (gathered caps) their stores: a store
+      // between loads would serialise their latencies (the compiler cannot
+      // tell the gathered roots from the cap apart)
+      uint32_t a[8], b[8], c[8], d[8], p0[8], p1[8];
+      upper_load(src, gj, 4 * g + 0, a);
+      upper_load(src, gj, 4 * g + 1, b);
+      upper_load(src, gj, 4 * g + 2, c);
+      upper_load(src, gj, 4 * g + 3, d);
+      if (gj.gath) {
+        store_level(T, from, 4 * g + 0, a);
+        store_level(T, from, 4 * g + 1, b);
+        store_level(T, from, 4 * g + 2, c);
+        store_level(T, from, 4 * g + 3, d);
+      }
       b3_parent(a, b, p0);
-      node_load(src + 8 * (4 * g + 2), a);
-      node_load(src + 8 * (4 * g + 3), b);
-      b3_parent(a, b, p1);
+      b3_parent(c, d, p1);
       store_level(T, from + 1, 2 * g, p0);
       store_level(T, from + 1, 2 * g + 1, p1);
       b3_parent(p0, p1, h);
       store_level(T, from + 2, g, h);
     } else if (logper == 1) {
       uint32_t a[8], b[8];
-      node_load(src + 8 * (2 * g), a);
-      node_load(src + 8 * (2 * g + 1), b);
+      upper_src(T, src, gj, from, 2 * g, a);
+      upper_src(T, src, gj, from, 2 * g + 1, b);
       b3_parent(a, b, h);
       store_level(T, from + 1, g, h);
     } else {
-      node_load(src + 8 * g, h);
+      upper_src(T, src, gj, from, g, h);
       if (from == T.logLen) node_store(T.root, h);
     }
     lds_put(lds, tid, h);
@@ -306,7 +331,7 @@ __global__ void __launch_bounds__(MK_THREADS) k_tree_upper(TreeDev T0, uint64_t 
 __global__ void __launch_bounds__(MK_THREADS) k_upper_jobs(const UpperJob* __restrict__ jobs) {
   __shared__ uint32_t lds[8][MK_THREADS];
   const UpperJob J = jobs[blockIdx.x];
-  upper_wg(J.tree, J.from, J.wg, lds, J.to);
+  upper_wg(J.tree, J.from, J.wg, lds, J.to, GathSrc{J.gath, J.nrun, J.logP});
 }
 
 // ------------------------------------------------- layers of >= 4096 leaves
@@ -876,15 +901,32 @@ hipError_t launch_upper_jobs(hipStream_t st, const UpperJob* d_jobs, int njobs) 
   return hipGetLastError();
 }
 
-void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes, int to) {
+void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes, int to,
+                     const uint32_t* gath, uint64_t nrun, int logP) {
   const int top = (to > 0 && to < T.logLen) ? to : T.logLen;
+  if (gath && from == top) {  // a one-node cap (P = 1): the job copies the gathered root into it
+    if (passes.empty()) passes.resize(1);
+    UpperJob J{T, from, 0u, to, 0};
+    J.gath = gath;
+    J.nrun = nrun;
+    J.logP = logP;
+    passes[0].push_back(J);
+    return;
+  }
   int p = 0;
   while (from < top) {
     const int c = top - from;
     const int step = c < 10 ? c : 10;
     if ((int)passes.size() <= p) passes.resize(p + 1);
-    for (uint64_t w = 0; w < (1ULL << (T.logLen - from - step)); w++)
-      passes[p].push_back(UpperJob{T, from, (uint32_t)w, to, 0});
+    for (uint64_t w = 0; w < (1ULL << (T.logLen - from - step)); w++) {
+      UpperJob J{T, from, (uint32_t)w, to, 0};
+      if (p == 0 && gath) {  // the first pass reads the gathered run roots (and stores them)
+        J.gath = gath;
+        J.nrun = nrun;
+        J.logP = logP;
+      }
+      passes[p].push_back(J);
+    }
     from += step;
     p++;
   }

@@ -166,6 +166,7 @@ struct sezkp_ctx {
   hipStream_t st2 = nullptr;  // side stream: small FRI layers overlap the forest
   hipStream_t stc = nullptr;  // copy stream: staged uploads (sezkp_ctx_stage)
   hipEvent_t ev_fold = nullptr, ev_tail = nullptr, ev_expand = nullptr, ev_cols = nullptr;
+  hipEvent_t ev_qin = nullptr, ev_qout = nullptr;  // the DEEP tables on the side stream, beside the INTT
   // Trace images, double-buffered: slot[active] feeds the proofs; stage()
   // fills slot[1 - active] on the copy stream while a proof runs, and the
   // next prove() switches to it (its kernels wait for the copy on the device).
@@ -447,6 +448,8 @@ struct sezkp_ctx {
     if (ev_tail) (void)hipEventDestroy(ev_tail);
     if (ev_expand) (void)hipEventDestroy(ev_expand);
     if (ev_cols) (void)hipEventDestroy(ev_cols);
+    if (ev_qin) (void)hipEventDestroy(ev_qin);
+    if (ev_qout) (void)hipEventDestroy(ev_qout);
     if (stc) (void)hipStreamSynchronize(stc);
     for (auto& sl : slot)
       if (sl.ready) (void)hipEventDestroy(sl.ready);
@@ -887,13 +890,18 @@ void sezkp_ctx::upload(const sezkp_block_view& v_in, uint64_t row0, uint64_t nro
     std::vector<std::vector<UpperJob>> p0, pF, pL0, pLR;
     // run layers start from the level their layer16 WGs stopped at
     const int from = tree_stop();
-    if (rR >= 0 && caps[0].logLen > from) plan_upper_jobs(caps[0], from, p0);
+    // sharded: a run layer's cap starts from its allgathered run roots (the
+    // first pass permutes them into cap order itself: no scatter launch)
+    auto gath_of = [&](int r) -> const uint32_t* { return sharded() && r <= rR ? rr_gather[r] : nullptr; };
+    auto nrun_of = [&](int r) -> uint64_t { return sharded() ? (N >> r) >> (L16_LOG + logP) : 0; };
+    if (rR >= 0 && (caps[0].logLen > from || gath_of(0)))
+      plan_upper_jobs(caps[0], from, p0, 0, gath_of(0), nrun_of(0), logP);
     const int rep_from = std::min(L16_LOG, tree_wg_log);
     for (int r = 1; r <= k; r++) {
       const bool runl = r <= rR;
       if ((runl || std::find(rep16.begin(), rep16.end(), r) != rep16.end()) &&
-          caps[r].logLen > (runl ? from : rep_from))
-        plan_upper_jobs(caps[r], runl ? from : rep_from, pF);
+          (caps[r].logLen > (runl ? from : rep_from) || (runl && gath_of(r))))
+        plan_upper_jobs(caps[r], runl ? from : rep_from, pF, 0, runl ? gath_of(r) : nullptr, nrun_of(r), logP);
     }
     // sharded with 1024-leaf WGs: the run trees' levels 11..12 (the run roots
     // the caps are gathered from) by upper jobs before each allgather
@@ -1225,56 +1233,9 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     }
   };
   const uint64_t P1 = (uint64_t)world - 1;
-  rec(0);
-  // ---- column commitments (openings.rs:306-398): this rank's chunks, then
-  // every rank gathers all chunk roots and builds the outer trees
-  ok(launch_expand(st, T, blk_lo, blk_cnt, d_err), "expand");
-  rec(1);
   const uint64_t row_lo = n >= 1024 ? ch_lo << COL_CHUNK_LOG2 : 0;
   const uint64_t row_hi = n >= 1024 ? ch_hi << COL_CHUNK_LOG2 : n;
-  // piecewise / table / dense columns on the side stream, concurrent with the
-  // (VALU-bound) dictionary columns; disjoint outer-tree leaves. (Starting
-  // them later, beside part of the dictionary chain only, or on a CU-masked
-  // stream, measured even or slower in round 3.)
-  HIP_OR_THROW(hipEventRecord(ev_expand, st));
-  HIP_OR_THROW(hipStreamWaitEvent(st2, ev_expand, 0));
-  ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
-  ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
-  ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
-                          outer_stride, d_err), "col_commit_pw");
-  // the composition's transcript-independent half (the row sums), also
-  // beside the dictionary commitments: only its combine with the alphas is
-  // left after the transcript's first round trip
-  ok(launch_compose_terms(st2, T, Tm, row_lo, row_hi - row_lo), "compose_terms");
-  HIP_OR_THROW(hipEventRecord(ev_cols, st2));
-  ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
-                        row_hi - row_lo, d_dlev),
-     "col_commit_dict");
-  HIP_OR_THROW(hipStreamWaitEvent(st, ev_cols, 0));
-  // test hook: SEZKP_DEBUG_TRIP_GUARD=<rank> sets that rank's guard word, to
-  // check that the failure is collective (tests/test_gpu_sharded.py)
-  static const char* trip = getenv("SEZKP_DEBUG_TRIP_GUARD");
-  if (trip && atoi(trip) == rank) HIP_OR_THROW(hipMemsetAsync(d_err, 0x7f, 1, st));
-  if (sharded) {
-    // the chunk roots of every column and every rank's guard word in one
-    // group: sharded ranks see all guard words, so a trip on any rank makes
-    // ALL ranks fail at the first check, before the next collective (no rank
-    // is left blocked in an RCCL call its peers never reach)
-    const size_t bytes = (size_t)(ch_hi - ch_lo) * 32;
-    coll("col_chunk_roots", P1 * (bytes * ncols + 4), [&] {
-      comm->group_start();
-      for (int c = 0; c < ncols; c++) {
-        uint32_t* lvl0 = d_outer + (size_t)c * outer_stride * 8;
-        comm->allgather(lvl0 + ch_lo * 8, lvl0, bytes, st);
-      }
-      comm->allgather(d_err, d_err + 8, 4, st);
-      comm->group_end();
-    });
-  }
-  rec(2);
-  TreeDev outer0{d_outer, d_colroots, logChunks, 0};
-  ok(launch_tree_upper(st, &outer0, ncols, outer_stride, 8, 0), "col_outer");
-  rec(3);
+  const bool no_deep_poly = getenv("SEZKP_NO_DEEP_POLY") != nullptr;
   const int nguard = sharded ? comm->world : 1;
   auto check_guards = [&](const uint32_t* g_h, int ng) {
     for (int r = 0; r < ng; r++) {
@@ -1310,54 +1271,8 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   Transcript tr("sezkp-stark/v1");
   const uint64_t shift_inv = hgl_inv(3);
   uint64_t z = 0, zn = 0;
-  // one copy: the column roots and the guard words stored right behind them
-  // (d_err = d_colroots + 8 ncols; sharded, every rank's word at d_err + 8)
+  bool dq = false;
   const size_t gofs = sharded ? 8 : 0;
-  HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32 + 4 * (gofs + nguard), hipMemcpyDeviceToHost,
-                              st));
-  sync();
-  mark("sync1");
-  const uint32_t* colroots_h = h_small;
-  check_guards(h_small + 8 * ncols + gofs, nguard);
-  std::vector<uint8_t> colroots((const uint8_t*)colroots_h, (const uint8_t*)colroots_h + (size_t)ncols * 32);
-  for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
-
-  // ---- transcript prelude + column roots (prover.rs:67-81); every rank
-  // replays the same transcript, so challenges need no broadcast
-  tr.absorb("manifest_root", mroot, 32);
-  tr.absorb_u64("n", n);
-  tr.absorb_u64("tau", tau);
-  tr.absorb_u64("n_cols", (uint64_t)ncols);
-  for (int c = 0; c < ncols; c++) tr.absorb("col_root", colroots.data() + 32 * c, 32);
-  // alphas (params.rs:82-92) with the reuse of prover.rs:86-98
-  mark("tr_roots");
-  auto ab = tr.challenge("alphas", 64);
-  uint64_t a[8];
-  for (int i = 0; i < 8; i++) a[i] = rd64(ab.data() + 8 * i) % GL_P_HOST;
-  // masks (masking.rs:56-79): one cubic
-  tr.absorb("masks", "masks", 5);
-  tr.absorb_u64("n_masks", 1);
-  tr.absorb_u64("deg", 4);
-  uint64_t mask[4];
-  for (int j = 0; j < 4; j++) mask[j] = rd64(tr.challenge("mask_coeff", 8).data()) % GL_P_HOST;
-  // OOD point + coset nudge (prover.rs:119-135)
-  z = rd64(tr.challenge("ood_point", 8).data()) % GL_P_HOST;
-  for (;;) {
-    uint64_t t = hgl_mul(z, shift_inv);
-    for (int i = 0; i < k; i++) t = hgl_mul(t, t);
-    if (t != 1) break;
-    z = hgl_add(z, 1);
-  }
-  for (int i = 0; i < 8; i++) h_chal->alpha[i] = a[i];
-  for (int j = 0; j < 4; j++) h_chal->mask[j] = mask[j];
-  zn = hgl_pow(z, n);
-  // ---- composition (this rank's rows), DEEP quotient, INTT
-  mark("z_done");
-  // single device: DEEP as the LDE of H = q + c S (DeepPoly); the base
-  // evaluations become q(w^j) before the INTT. Not when z^n = 1 (z on the
-  // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
-  mark("compose_issued");
-  const bool dq = logn >= 4 && z != 0 && zn != 1 && !getenv("SEZKP_NO_DEEP_POLY");
   // sharded: each rank turns its own rows into D_j (DeepPoly) and one
   // allgather (with the partial sums of f(z)) gives every rank the n values
   // for the n-point INTT its coset needs; without the quotient the
@@ -1372,351 +1287,478 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   // -> 1.132 ms predicted), so it is the default.
   const bool dist_intt = sharded && world > 1 && getenv("SEZKP_DIST_INTT") && atoi(getenv("SEZKP_DIST_INTT")) != 0;
   DeepPoly dpoly{d_dq_rlo, d_dq_rhi, d_dq_rhk};
-  if (dq) {
-    const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
-    const uint64_t zN = hgl_pow(zn, N / n);
-    uint64_t K2 = hgl_mul(hgl_pow(z, N - 1), hgl_inv(hgl_sub(hgl_pow(3, N), zN)));  // c' = f(z) K2
-    // rank g evaluates the coset 3 w_N^g <w_M>: H's N coefficients fold to M
-    // (M >= n): h'_k = [k < n] q_k (3 w_N^g)^k + c' G rho^k, rho = (3/z) w_N^g,
-    // G = sum_{t<P} rho^(tM); single device: rho = 3/z, G = 1
-    // (full_lde: the whole domain, as on one device)
-    const int cP = full_lde ? 0 : logP;
-    const uint64_t cg = full_lde ? 0 : (uint64_t)rank;
-    const uint64_t M_ = N >> cP;
-    const uint64_t rho = hgl_mul(hgl_mul(3, hgl_inv(z)), hgl_pow(hgl_root_2exp((uint32_t)logN), cg));
-    const uint64_t rhoM = hgl_pow(rho, M_);
-    uint64_t G = 0, pw = 1;
-    for (int t = 0; t < (1 << cP); t++) {
-      G = hgl_add(G, pw);
-      pw = hgl_mul(pw, rhoM);
-    }
-    K2 = hgl_mul(K2, G);
-    h_chal->z = z;
-    h_chal->zn = zn;
-    h_chal->K1 = K1;
-    h_chal->K2 = K2;
-    h_chal->rho = rho;
-    h_chal->rho4096 = hgl_pow(rho, 4096);
-    h_chal->K3 = hgl_mul(hgl_mul(zn, hgl_inv(z)), hgl_inv(n % GL_P_HOST));  // z^(n-1) / n: kappa = K3 S
-  }
-  // alphas, masks and the DEEP constants for the kernels below
-  HIP_OR_THROW(hipMemcpyAsync(d_chal, h_chal, offsetof(DevChal, beta), hipMemcpyHostToDevice, st));
-  const uint64_t dq_per = dq_rows_per_part(row_hi - row_lo);  // base rows per partial sum (k_inv_base WG)
-  if (dq) {
-    // the composition's combine (alphas, mask) fused with the DEEP quotient:
-    // D_j = C_j / (w^j - z) and the partial sums of f(z) (DeepPoly); the
-    // INTT runs on D, f(z) is needed by the tables only
-    ok(launch_inv_base(st, Tm, d_base, d_dq_part, logn, d_chal, tw, row_lo, row_hi - row_lo, dq_per), "inv_base");
-  } else {
-    ok(launch_compose_combine(st, Tm, d_chal, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
-    if (sharded && !dist_intt)
-      coll("base_values", P1 * (row_hi - row_lo) * 8,
-           [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
-  }
-  rec(4);
-  // sharded: this rank's partial sums of f(z) travel with the INTT exchange
-  // that gathers every rank's values (one collective)
-  auto gather_fz = [&](uint64_t nrows) {
-    if (dq) comm->allgather(d_dq_part + row_lo / dq_per, d_dq_part, (size_t)(nrows / dq_per) * 8, st);
-  };
-  if (dist_intt) {
-    const uint64_t m = n >> logP, Q = m >> logP;
-    if (row_lo != (uint64_t)rank * m || row_hi - row_lo != m) throw Err{SEZKP_E_INVALID, "sharded INTT: row split"};
-    uint64_t* blk = d_base + row_lo;
-    // d_lde: r[g Q + t] = x[g m + rank Q + t]
-    coll("intt_alltoall1", P1 * Q * 8, [&] { comm->alltoall(blk, d_lde, Q * 8, st); });
-    ok(bintt_dft_twiddle(st, d_lde, world, Q, (uint32_t)rank, logn, tw), "intt_dft");
-    coll("intt_alltoall2", P1 * Q * 8, [&] { comm->alltoall(d_lde, blk, Q * 8, st); });  // blk[j] = y_rank[j]
-    ok(ntt_dif(st, blk, logn - logP, true, tw), "intt_local");  // slot p: n a_(rank + P bitrev(p))
-    coll("intt_coeffs", P1 * (m * 8 + (dq ? m / dq_per * 8 : 0)), [&] {
-      comm->group_start();
-      comm->allgather(blk, d_base, m * 8, st);
-      gather_fz(m);
-      comm->group_end();
-    });
-  } else {
-    if (sharded && dq) {
-      const uint64_t nrows = row_hi - row_lo;
-      coll("d_values", P1 * (nrows * 8 + nrows / dq_per * 8), [&] {
+  std::vector<uint8_t> roots((size_t)(k + 1) * 32);
+  uint64_t rows[NUM_QUERIES], frows[NUM_QUERIES];
+  std::vector<uint64_t> pos((size_t)NUM_QUERIES * (k + 1));
+  size_t nf = 0, no = 0;
+
+  // ---- the proof as four device phases and three host phases (the
+  // Fiat-Shamir round trips). Each enqueue_* issues one phase's work on the
+  // streams; each host_* reads what the previous phase copied back, runs the
+  // transcript and fills what the next phase copies in. (Round 6 measured
+  // the phases enqueued ahead behind stream wait-value gates that the host
+  // opened: a P = 8 rank's device stages took 0.94 against 0.90 ms, the
+  // kernels after each gate running slower; the round trips stay
+  // synchronous.)
+  auto enqueue_A = [&]() {
+    rec(0);
+    // ---- column commitments (openings.rs:306-398): this rank's chunks, then
+    // every rank gathers all chunk roots and builds the outer trees
+    ok(launch_expand(st, T, blk_lo, blk_cnt, d_err), "expand");
+    rec(1);
+    // piecewise / table / dense columns on the side stream, concurrent with the
+    // (VALU-bound) dictionary columns; disjoint outer-tree leaves. (Starting
+    // them later, beside part of the dictionary chain only, or on a CU-masked
+    // stream, measured even or slower in round 3.)
+    HIP_OR_THROW(hipEventRecord(ev_expand, st));
+    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_expand, 0));
+    ok(launch_col_tables(st2, T, d_tmpl, d_tab_cols, n_tab_cols, tab_units, d_tabs, blk_lo, blk_cnt), "col_tables");
+    ok(launch_col_commit(st2, T, d_tmpl, d_work, n_work, d_tabs, d_outer, outer_stride), "col_commit");
+    ok(launch_col_commit_pw(st2, T, d_tmpl, d_pw_cols, n_pw_cols, d_pw_chunks, n_pw_chunks, d_tabs, d_outer,
+                            outer_stride, d_err), "col_commit_pw");
+    // the composition's transcript-independent half (the row sums), also
+    // beside the dictionary commitments: only its combine with the alphas is
+    // left after the transcript's first round trip
+    ok(launch_compose_terms(st2, T, Tm, row_lo, row_hi - row_lo), "compose_terms");
+    HIP_OR_THROW(hipEventRecord(ev_cols, st2));
+    ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
+                          row_hi - row_lo, d_dlev),
+       "col_commit_dict");
+    HIP_OR_THROW(hipStreamWaitEvent(st, ev_cols, 0));
+    // test hook: SEZKP_DEBUG_TRIP_GUARD=<rank> sets that rank's guard word, to
+    // check that the failure is collective (tests/test_gpu_sharded.py)
+    static const char* trip = getenv("SEZKP_DEBUG_TRIP_GUARD");
+    if (trip && atoi(trip) == rank) HIP_OR_THROW(hipMemsetAsync(d_err, 0x7f, 1, st));
+    if (sharded) {
+      // the chunk roots of every column and every rank's guard word in one
+      // group: sharded ranks see all guard words, so a trip on any rank makes
+      // ALL ranks fail at the first check, before the next collective (no rank
+      // is left blocked in an RCCL call its peers never reach)
+      const size_t bytes = (size_t)(ch_hi - ch_lo) * 32;
+      coll("col_chunk_roots", P1 * (bytes * ncols + 4), [&] {
         comm->group_start();
-        comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st);
-        gather_fz(nrows);
+        for (int c = 0; c < ncols; c++) {
+          uint32_t* lvl0 = d_outer + (size_t)c * outer_stride * 8;
+          comm->allgather(lvl0 + ch_lo * 8, lvl0, bytes, st);
+        }
+        comm->allgather(d_err, d_err + 8, 4, st);
         comm->group_end();
       });
     }
-    ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
-  }
-  if (dq)
-    ok(launch_q_tables(st, d_dq_part, logn, full_lde ? logN : logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk, dq_per),
-       "q_tables");
-  rec(5);
-  // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on
-  // 3 w_N^g <w_M> (M = N/P), no communication
-  const uint64_t inv_n = hgl_inv(n % GL_P_HOST);
-  uint64_t* lde_out = sharded ? d_cyc : d_lde;
-  // the evaluated coset: 3 w_N^g <w_M> (rank g of P), or the whole domain
-  const int eP = full_lde ? 0 : logP;
-  const uint32_t eg = full_lde ? 0u : (uint32_t)rank;
-  const int logE = logN - eP;
-  const uint64_t coset_e = sharded && !full_lde ? ((uint64_t)rank << (tw.K - logN)) : 0;
-  const DeepFuse dfuse{z, logN, eP, eg};
-  bool deep_fused = dq;
-  const int src_logP = dist_intt ? logP : 0;
-  if (dq)
-    ok(ntt_dit(st, lde_out, logE, false, tw, d_base, logn, inv_n, coset_e, nullptr, nullptr, &dpoly, src_logP),
-       "lde_ntt");
-  else
-    ok(ntt_dit(st, lde_out, logE, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused, nullptr, src_logP),
-       "lde_ntt");
-  rec(6);
-  if (!deep_fused) ok(launch_deep(st, lde_out, logN, z, tw, eP, eg), "deep");
-  if (full_lde) {  // this rank's runs of 4096 out of the whole LDE
-    ok(launch_runs_extract(st, d_cyc, d_lde, M, logP, (uint32_t)rank), "runs_extract");
-  } else if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI
-    ok(launch_cyc_pack(st, d_cyc, d_xbuf, M, logP), "cyc_pack");
-    coll("lde_alltoall", P1 * (M >> logP) * 8, [&] { comm->alltoall(d_xbuf, d_cyc, (size_t)(M >> logP) * 8, st); });
-    ok(launch_cyc_unpack(st, d_cyc, d_lde, M, logP), "cyc_unpack");
-  }
-  rec(7);
-  // ---- layer-0 tree: local runs, then the cap from allgathered run roots
-  if (rR >= 0) {
-    ok(launch_layer16(st, d_lde, nullptr, ltrees[0].logLen, 0, 0, ltrees[0], wg_stop(), nullptr, tree_wg_log),
-       "layer0_tree");
-    rec(ST_L0TREE + 1);
-    for (auto& p : jobsL0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_runroots");
-    if (sharded) {
-      const uint64_t nrun = M >> L16_LOG;
-      const uint32_t* lv12 = ltrees[0].nodes + 8 * tree_level_off(ltrees[0].logLen, LSTORE_FRI, L16_LOG);
-      coll("layer0_run_roots", P1 * nrun * 32, [&] { comm->allgather(lv12, rr_gather[0], (size_t)nrun * 32, st); });
-      ok(launch_runroots_scatter(st, rr_gather[0], caps[0], nrun, logP), "runroots0");
-    }
-    for (auto& p : jobs0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_upper");
-  } else {
-    ok(launch_leaf_subtree(st, d_lde, nullptr, logN, 0, 0, ltrees[0]), "layer0_tree");
-    rec(ST_L0TREE + 1);
-  }
-  rec(ST_L0UP + 1);
-  // ---- layer-0 root -> all betas at once (prover.rs:184-198)
-  std::vector<uint8_t> roots((size_t)(k + 1) * 32);
-  HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
-  sync();
-  mark("sync2");
-  memcpy(roots.data(), h_small, 32);
-  tr.absorb("fri_layer_root", roots.data(), 32);
-  auto bb = tr.challenge("fri_betas", 8 * (size_t)k);
-  for (int r = 0; r < k; r++) h_chal->beta[r] = rd64(bb.data() + 8 * r) % GL_P_HOST;
-  HIP_OR_THROW(hipMemcpyAsync(d_chal->beta, h_chal->beta, 8 * (size_t)k, hipMemcpyHostToDevice, st));
+    rec(2);
+    TreeDev outer0{d_outer, d_colroots, logChunks, 0};
+    ok(launch_tree_upper(st, &outer0, ncols, outer_stride, 8, 0), "col_outer");
+    rec(3);
+    // one copy: the column roots and the guard words stored right behind them
+    // (d_err = d_colroots + 8 ncols; sharded, every rank's word at d_err + 8)
+    HIP_OR_THROW(hipMemcpyAsync(h_small, d_colroots, (size_t)ncols * 32 + 4 * (gofs + nguard), hipMemcpyDeviceToHost,
+                                st));
+  };
+  auto host_1 = [&]() {
+    const uint32_t* colroots_h = h_small;
+    check_guards(h_small + 8 * ncols + gofs, nguard);
+    std::vector<uint8_t> colroots((const uint8_t*)colroots_h, (const uint8_t*)colroots_h + (size_t)ncols * 32);
+    for (int c = 0; c < ncols; c++) memcpy(h_proof + root_pos[c], colroots.data() + 32 * c, 32);
 
-  // ---- FRI folds + layer trees (prover.rs:192-239). Folds of run layers are
-  // rank-local (i and i + len/2 share i mod 4096P). The kernels read the
-  // betas from the challenge record: beta r folds layer r into layer r + 1.
-  const uint64_t* dbeta = d_chal->beta;
-  // layers of <= 2^11 leaves: one launch on the side stream, overlapping the
-  // forest / upper levels (its source is the last fold-chain output)
-  auto tail_args = [&](const uint64_t* src_vals) {
-    TailArgs ta{};
-    ta.src = src_vals;
-    ta.Ls = k - tail_first;
-    ta.beta = dbeta + (tail_first - 1);
-    for (int j = 0; j <= ta.Ls; j++) {
-      ta.vals[j] = lvals[tail_first + j];
-      ta.tree[j] = ltrees[tail_first + j];
+    // ---- transcript prelude + column roots (prover.rs:67-81); every rank
+    // replays the same transcript, so challenges need no broadcast
+    tr.absorb("manifest_root", mroot, 32);
+    tr.absorb_u64("n", n);
+    tr.absorb_u64("tau", tau);
+    tr.absorb_u64("n_cols", (uint64_t)ncols);
+    for (int c = 0; c < ncols; c++) tr.absorb("col_root", colroots.data() + 32 * c, 32);
+    // alphas (params.rs:82-92) with the reuse of prover.rs:86-98
+    mark("tr_roots");
+    auto ab = tr.challenge("alphas", 64);
+    uint64_t a[8];
+    for (int i = 0; i < 8; i++) a[i] = rd64(ab.data() + 8 * i) % GL_P_HOST;
+    // masks (masking.rs:56-79): one cubic
+    tr.absorb("masks", "masks", 5);
+    tr.absorb_u64("n_masks", 1);
+    tr.absorb_u64("deg", 4);
+    uint64_t mask[4];
+    for (int j = 0; j < 4; j++) mask[j] = rd64(tr.challenge("mask_coeff", 8).data()) % GL_P_HOST;
+    // OOD point + coset nudge (prover.rs:119-135)
+    z = rd64(tr.challenge("ood_point", 8).data()) % GL_P_HOST;
+    for (;;) {
+      uint64_t t = hgl_mul(z, shift_inv);
+      for (int i = 0; i < k; i++) t = hgl_mul(t, t);
+      if (t != 1) break;
+      z = hgl_add(z, 1);
     }
-    return ta;
+    for (int i = 0; i < 8; i++) h_chal->alpha[i] = a[i];
+    for (int j = 0; j < 4; j++) h_chal->mask[j] = mask[j];
+    zn = hgl_pow(z, n);
+    // ---- composition (this rank's rows), DEEP quotient, INTT
+    mark("z_done");
+    // single device: DEEP as the LDE of H = q + c S (DeepPoly); the base
+    // evaluations become q(w^j) before the INTT. Not when z^n = 1 (z on the
+    // base domain) or z = 0, nor below 16 rows: the per-point DEEP below.
+    mark("compose_issued");
+    dq = logn >= 4 && z != 0 && zn != 1 && !no_deep_poly;
+    if (dq) {
+      const uint64_t K1 = hgl_mul(hgl_sub(1, zn), hgl_inv(n % GL_P_HOST));             // f(z) = K1 S
+      const uint64_t zN = hgl_pow(zn, N / n);
+      uint64_t K2 = hgl_mul(hgl_pow(z, N - 1), hgl_inv(hgl_sub(hgl_pow(3, N), zN)));  // c' = f(z) K2
+      // rank g evaluates the coset 3 w_N^g <w_M>: H's N coefficients fold to M
+      // (M >= n): h'_k = [k < n] q_k (3 w_N^g)^k + c' G rho^k, rho = (3/z) w_N^g,
+      // G = sum_{t<P} rho^(tM); single device: rho = 3/z, G = 1
+      // (full_lde: the whole domain, as on one device)
+      const int cP = full_lde ? 0 : logP;
+      const uint64_t cg = full_lde ? 0 : (uint64_t)rank;
+      const uint64_t M_ = N >> cP;
+      const uint64_t rho = hgl_mul(hgl_mul(3, hgl_inv(z)), hgl_pow(hgl_root_2exp((uint32_t)logN), cg));
+      const uint64_t rhoM = hgl_pow(rho, M_);
+      uint64_t G = 0, pw = 1;
+      for (int t = 0; t < (1 << cP); t++) {
+        G = hgl_add(G, pw);
+        pw = hgl_mul(pw, rhoM);
+      }
+      K2 = hgl_mul(K2, G);
+      h_chal->z = z;
+      h_chal->zn = zn;
+      h_chal->K1 = K1;
+      h_chal->K2 = K2;
+      h_chal->rho = rho;
+      h_chal->rho4096 = hgl_pow(rho, 4096);
+      h_chal->K3 = hgl_mul(hgl_mul(zn, hgl_inv(z)), hgl_inv(n % GL_P_HOST));  // z^(n-1) / n: kappa = K3 S
+    }
   };
-  auto launch_tail = [&](const uint64_t* src_vals) {
-    if (tail_first > k) return;
-    const TailArgs ta = tail_args(src_vals);
-    HIP_OR_THROW(hipEventRecord(ev_fold, st));
-    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
-    ok(launch_fri_tail(st2, ta), "fri_tail");
-    HIP_OR_THROW(hipEventRecord(ev_tail, st2));
-  };
-  mark("folds");
-  const bool tail_merged = !sharded && tail_first <= k && n_forest > 0 && d_tailbuf;
-  // fold chain, up to FOLD_MAX layers per pass (2 measured even); the forest
-  // follows the whole chain (hashing the first pass's layers beside the later
-  // folds measured slower in round 3: the forest starves the folds)
-  for (int r = 0; r < rR;) {
-    const int F = std::min(FOLD_MAX, rR - r);
-    if (F >= 2) {
-      FoldOuts fo{};
-      fo.beta = dbeta + r;
-      for (int m = 1; m <= F; m++) fo.out[m - 1] = lvals[r + m];
-      ok(launch_foldm(st, lvals[r], fo, F, ltrees[r + F].logLen), "fri_foldm");
-      r += F;
+  auto enqueue_B = [&]() {
+    // alphas, masks and the DEEP constants for the kernels below
+    HIP_OR_THROW(hipMemcpyAsync(d_chal, h_chal, offsetof(DevChal, beta), hipMemcpyHostToDevice, st));
+    const uint64_t dq_per = dq_rows_per_part(row_hi - row_lo);  // base rows per partial sum (k_inv_base WG)
+    if (dq) {
+      // the composition's combine (alphas, mask) fused with the DEEP quotient:
+      // D_j = C_j / (w^j - z) and the partial sums of f(z) (DeepPoly); the
+      // INTT runs on D, f(z) is needed by the tables only
+      ok(launch_inv_base(st, Tm, d_base, d_dq_part, logn, d_chal, tw, row_lo, row_hi - row_lo, dq_per), "inv_base");
     } else {
-      ok(launch_fold(st, lvals[r], lvals[r + 1], ltrees[r + 1].logLen, 0, dbeta + r), "fri_fold");
-      r += 1;
+      ok(launch_compose_combine(st, Tm, d_chal, tw, logn, d_base, row_lo, row_hi - row_lo), "compose");
+      if (sharded && !dist_intt)
+        coll("base_values", P1 * (row_hi - row_lo) * 8,
+             [&] { comm->allgather(d_base + row_lo, d_base, (size_t)(row_hi - row_lo) * 8, st); });
     }
-  }
-  const uint64_t* rep_src = rR >= 0 ? lvals[rR] : d_lde;  // full values of the layer above the replicated ones
-  // single device: the small layers ride in the forest launch's first
-  // workgroups (sharded: their own kernel on the side stream)
-  if (tail_merged) {
-    const TailArgs ta = tail_args(rep_src);
-    krec(false);
-    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf, 0, tree_wg_log), "fri_forest");
-    krec(true);
-  } else if (!sharded) {
-    launch_tail(rep_src);
-    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, nullptr, nullptr, 0, tree_wg_log), "fri_forest");
-  } else {
-    // the whole of layer rR, then the replicated layers folded from it in one
-    // pass, the tail (side stream) and one forest of run + replicated layers
-    coll("fri_rep_values", P1 * S * 8, [&] { comm->allgather(lvals[rR], d_rep, (size_t)S * 8, st); });
-    rep_src = d_rep;
-    const int last = rR + (int)rep16.size();
-    for (int r = rR; r < last;) {
-      const int F = std::min(FOLD_MAX, last - r);
-      const uint64_t* src = r == rR ? d_rep : lvals[r];
+    rec(4);
+    // sharded: this rank's partial sums of f(z) travel with the INTT exchange
+    // that gathers every rank's values (one collective)
+    auto gather_fz = [&](uint64_t nrows) {
+      if (dq) comm->allgather(d_dq_part + row_lo / dq_per, d_dq_part, (size_t)(nrows / dq_per) * 8, st);
+    };
+    if (dist_intt) {
+      const uint64_t m = n >> logP, Q = m >> logP;
+      if (row_lo != (uint64_t)rank * m || row_hi - row_lo != m) throw Err{SEZKP_E_INVALID, "sharded INTT: row split"};
+      uint64_t* blk = d_base + row_lo;
+      // d_lde: r[g Q + t] = x[g m + rank Q + t]
+      coll("intt_alltoall1", P1 * Q * 8, [&] { comm->alltoall(blk, d_lde, Q * 8, st); });
+      ok(bintt_dft_twiddle(st, d_lde, world, Q, (uint32_t)rank, logn, tw), "intt_dft");
+      coll("intt_alltoall2", P1 * Q * 8, [&] { comm->alltoall(d_lde, blk, Q * 8, st); });  // blk[j] = y_rank[j]
+      ok(ntt_dif(st, blk, logn - logP, true, tw), "intt_local");  // slot p: n a_(rank + P bitrev(p))
+      coll("intt_coeffs", P1 * (m * 8 + (dq ? m / dq_per * 8 : 0)), [&] {
+        comm->group_start();
+        comm->allgather(blk, d_base, m * 8, st);
+        gather_fz(m);
+        comm->group_end();
+      });
+    } else {
+      if (sharded && dq) {
+        const uint64_t nrows = row_hi - row_lo;
+        coll("d_values", P1 * (nrows * 8 + nrows / dq_per * 8), [&] {
+          comm->group_start();
+          comm->allgather(d_base + row_lo, d_base, (size_t)nrows * 8, st);
+          gather_fz(nrows);
+          comm->group_end();
+        });
+      }
+      // the DEEP tables (f(z) from the partial sums, the r^t / c' r^(4096t) /
+      // kappa r^(4096t) power tables: a latency-bound ~10 us) on the side
+      // stream beside the INTT, which does not read them
+      if (dq) {
+        HIP_OR_THROW(hipEventRecord(ev_qin, st));
+        HIP_OR_THROW(hipStreamWaitEvent(st2, ev_qin, 0));
+        ok(launch_q_tables(st2, d_dq_part, logn, full_lde ? logN : logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk, dq_per),
+           "q_tables");
+        HIP_OR_THROW(hipEventRecord(ev_qout, st2));
+      }
+      ok(ntt_dif(st, d_base, logn, true, tw), "intt");  // -> n * coeffs, bit-reversed
+      if (dq) HIP_OR_THROW(hipStreamWaitEvent(st, ev_qout, 0));
+    }
+    if (dq && dist_intt)
+      ok(launch_q_tables(st, d_dq_part, logn, full_lde ? logN : logM, d_chal, d_dq_rlo, d_dq_rhi, d_dq_rhk, dq_per),
+         "q_tables");
+    rec(5);
+    // ---- coset LDE (prover.rs:137-189, lde.rs:42-97): rank g evaluates on
+    // 3 w_N^g <w_M> (M = N/P), no communication
+    const uint64_t inv_n = hgl_inv(n % GL_P_HOST);
+    uint64_t* lde_out = sharded ? d_cyc : d_lde;
+    // the evaluated coset: 3 w_N^g <w_M> (rank g of P), or the whole domain
+    const int eP = full_lde ? 0 : logP;
+    const uint32_t eg = full_lde ? 0u : (uint32_t)rank;
+    const int logE = logN - eP;
+    const uint64_t coset_e = sharded && !full_lde ? ((uint64_t)rank << (tw.K - logN)) : 0;
+    const DeepFuse dfuse{z, logN, eP, eg};
+    bool deep_fused = dq;
+    const int src_logP = dist_intt ? logP : 0;
+    if (dq)
+      ok(ntt_dit(st, lde_out, logE, false, tw, d_base, logn, inv_n, coset_e, nullptr, nullptr, &dpoly, src_logP),
+         "lde_ntt");
+    else
+      ok(ntt_dit(st, lde_out, logE, false, tw, d_base, logn, inv_n, coset_e, &dfuse, &deep_fused, nullptr, src_logP),
+         "lde_ntt");
+    rec(6);
+    if (!deep_fused) ok(launch_deep(st, lde_out, logN, z, tw, eP, eg), "deep");
+    if (full_lde) {  // this rank's runs of 4096 out of the whole LDE
+      ok(launch_runs_extract(st, d_cyc, d_lde, M, logP, (uint32_t)rank), "runs_extract");
+    } else if (sharded) {  // cyclic coset -> runs of 4096: one all-to-all over xGMI
+      ok(launch_cyc_pack(st, d_cyc, d_xbuf, M, logP), "cyc_pack");
+      coll("lde_alltoall", P1 * (M >> logP) * 8, [&] { comm->alltoall(d_xbuf, d_cyc, (size_t)(M >> logP) * 8, st); });
+      ok(launch_cyc_unpack(st, d_cyc, d_lde, M, logP), "cyc_unpack");
+    }
+    rec(7);
+    // ---- layer-0 tree: local runs, then the cap from allgathered run roots
+    if (rR >= 0) {
+      ok(launch_layer16(st, d_lde, nullptr, ltrees[0].logLen, 0, 0, ltrees[0], wg_stop(), nullptr, tree_wg_log),
+         "layer0_tree");
+      rec(ST_L0TREE + 1);
+      for (auto& p : jobsL0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_runroots");
+      if (sharded) {
+        const uint64_t nrun = M >> L16_LOG;
+        const uint32_t* lv12 = ltrees[0].nodes + 8 * tree_level_off(ltrees[0].logLen, LSTORE_FRI, L16_LOG);
+        coll("layer0_run_roots", P1 * nrun * 32, [&] { comm->allgather(lv12, rr_gather[0], (size_t)nrun * 32, st); });
+      }
+      for (auto& p : jobs0) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "layer0_upper");
+    } else {
+      ok(launch_leaf_subtree(st, d_lde, nullptr, logN, 0, 0, ltrees[0]), "layer0_tree");
+      rec(ST_L0TREE + 1);
+    }
+    rec(ST_L0UP + 1);
+    // ---- layer-0 root -> all betas at once (prover.rs:184-198)
+    HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, 32, hipMemcpyDeviceToHost, st));
+  };
+  auto host_2 = [&]() {
+    memcpy(roots.data(), h_small, 32);
+    tr.absorb("fri_layer_root", roots.data(), 32);
+    auto bb = tr.challenge("fri_betas", 8 * (size_t)k);
+    for (int r = 0; r < k; r++) h_chal->beta[r] = rd64(bb.data() + 8 * r) % GL_P_HOST;
+  };
+  auto enqueue_C = [&]() {
+    HIP_OR_THROW(hipMemcpyAsync(d_chal->beta, h_chal->beta, 8 * (size_t)k, hipMemcpyHostToDevice, st));
+
+    // ---- FRI folds + layer trees (prover.rs:192-239). Folds of run layers are
+    // rank-local (i and i + len/2 share i mod 4096P). The kernels read the
+    // betas from the challenge record: beta r folds layer r into layer r + 1.
+    const uint64_t* dbeta = d_chal->beta;
+    // layers of <= 2^11 leaves: one launch on the side stream, overlapping the
+    // forest / upper levels (its source is the last fold-chain output)
+    auto tail_args = [&](const uint64_t* src_vals) {
+      TailArgs ta{};
+      ta.src = src_vals;
+      ta.Ls = k - tail_first;
+      ta.beta = dbeta + (tail_first - 1);
+      for (int j = 0; j <= ta.Ls; j++) {
+        ta.vals[j] = lvals[tail_first + j];
+        ta.tree[j] = ltrees[tail_first + j];
+      }
+      return ta;
+    };
+    auto launch_tail = [&](const uint64_t* src_vals) {
+      if (tail_first > k) return;
+      const TailArgs ta = tail_args(src_vals);
+      HIP_OR_THROW(hipEventRecord(ev_fold, st));
+      HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+      ok(launch_fri_tail(st2, ta), "fri_tail");
+      HIP_OR_THROW(hipEventRecord(ev_tail, st2));
+    };
+    mark("folds");
+    const bool tail_merged = !sharded && tail_first <= k && n_forest > 0 && d_tailbuf;
+    // fold chain, up to FOLD_MAX layers per pass (2 measured even); the forest
+    // follows the whole chain (hashing the first pass's layers beside the later
+    // folds measured slower in round 3: the forest starves the folds)
+    for (int r = 0; r < rR;) {
+      const int F = std::min(FOLD_MAX, rR - r);
       if (F >= 2) {
         FoldOuts fo{};
         fo.beta = dbeta + r;
         for (int m = 1; m <= F; m++) fo.out[m - 1] = lvals[r + m];
-        ok(launch_foldm(st, src, fo, F, ltrees[r + F].logLen), "fri_rep_folds");
+        ok(launch_foldm(st, lvals[r], fo, F, ltrees[r + F].logLen), "fri_foldm");
+        r += F;
       } else {
-        ok(launch_fold(st, src, lvals[r + 1], ltrees[r + 1].logLen, 0, dbeta + r), "fri_rep_fold");
+        ok(launch_fold(st, lvals[r], lvals[r + 1], ltrees[r + 1].logLen, 0, dbeta + r), "fri_fold");
+        r += 1;
       }
-      r += F;
     }
-    if (!rep16.empty()) rep_src = lvals[rep16.back()];
-    launch_tail(rep_src);
-    ok(launch_forest16(st, d_forest, n_forest, forest_wgs, nullptr, nullptr, 0, tree_wg_log), "fri_forest");
-    for (auto& p : jobsLR) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_runroots");
-    uint64_t wire = 0;
-    for (int r = 1; r <= rR; r++) wire += P1 * ((N >> r) >> (L16_LOG + logP)) * 32;
-    coll("fri_run_roots", wire, [&] {
-      comm->group_start();
-      for (int r = 1; r <= rR; r++) {
-        const uint64_t nrun = (N >> r) >> (L16_LOG + logP);
-        const uint32_t* lv12 = ltrees[r].nodes + 8 * tree_level_off(ltrees[r].logLen, LSTORE_FRI, L16_LOG);
-        comm->allgather(lv12, rr_gather[r], (size_t)nrun * 32, st);
+    const uint64_t* rep_src = rR >= 0 ? lvals[rR] : d_lde;  // full values of the layer above the replicated ones
+    // single device: the small layers ride in the forest launch's first
+    // workgroups (sharded: their own kernel on the side stream)
+    if (tail_merged) {
+      const TailArgs ta = tail_args(rep_src);
+      krec(false);
+      ok(launch_forest16(st, d_forest, n_forest, forest_wgs, &ta, d_tailbuf, 0, tree_wg_log), "fri_forest");
+      krec(true);
+    } else if (!sharded) {
+      launch_tail(rep_src);
+      ok(launch_forest16(st, d_forest, n_forest, forest_wgs, nullptr, nullptr, 0, tree_wg_log), "fri_forest");
+    } else {
+      // the whole of layer rR, then the replicated layers folded from it in one
+      // pass, the tail (side stream) and one forest of run + replicated layers
+      coll("fri_rep_values", P1 * S * 8, [&] { comm->allgather(lvals[rR], d_rep, (size_t)S * 8, st); });
+      rep_src = d_rep;
+      const int last = rR + (int)rep16.size();
+      for (int r = rR; r < last;) {
+        const int F = std::min(FOLD_MAX, last - r);
+        const uint64_t* src = r == rR ? d_rep : lvals[r];
+        if (F >= 2) {
+          FoldOuts fo{};
+          fo.beta = dbeta + r;
+          for (int m = 1; m <= F; m++) fo.out[m - 1] = lvals[r + m];
+          ok(launch_foldm(st, src, fo, F, ltrees[r + F].logLen), "fri_rep_folds");
+        } else {
+          ok(launch_fold(st, src, lvals[r + 1], ltrees[r + 1].logLen, 0, dbeta + r), "fri_rep_fold");
+        }
+        r += F;
       }
-      comm->group_end();
-    });
-    for (int r0 = 1; r0 <= rR; r0 += RR_BATCH_MAX) {  // one launch for all run layers (rR <= 32)
-      RunRootsBatch B{};
-      B.logP = logP;
-      for (int r = r0; r <= rR && B.n < RR_BATCH_MAX; r++, B.n++) {
-        B.gathered[B.n] = rr_gather[r];
-        B.cap[B.n] = caps[r];
-        B.nrun[B.n] = (N >> r) >> (L16_LOG + logP);
-      }
-      ok(launch_runroots_scatter_multi(st, B), "runroots");
+      if (!rep16.empty()) rep_src = lvals[rep16.back()];
+      launch_tail(rep_src);
+      ok(launch_forest16(st, d_forest, n_forest, forest_wgs, nullptr, nullptr, 0, tree_wg_log), "fri_forest");
+      for (auto& p : jobsLR) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_runroots");
+      uint64_t wire = 0;
+      for (int r = 1; r <= rR; r++) wire += P1 * ((N >> r) >> (L16_LOG + logP)) * 32;
+      coll("fri_run_roots", wire, [&] {
+        comm->group_start();
+        for (int r = 1; r <= rR; r++) {
+          const uint64_t nrun = (N >> r) >> (L16_LOG + logP);
+          const uint32_t* lv12 = ltrees[r].nodes + 8 * tree_level_off(ltrees[r].logLen, LSTORE_FRI, L16_LOG);
+          comm->allgather(lv12, rr_gather[r], (size_t)nrun * 32, st);
+        }
+        comm->group_end();
+      });
+      // (the caps' first upper-level pass reads the gathered roots in place)
     }
-  }
-  for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
-  if (tail_first <= k && !tail_merged) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
-  rec(ST_FRI + 1);
-  // ---- FRI roots -> query rows mod n and mod N (prover.rs:248, 297), the
-  // path / opening requests each rank owns and (device mode) the body fields
-  uint64_t rows[NUM_QUERIES], frows[NUM_QUERIES];
-  std::vector<uint64_t> pos((size_t)NUM_QUERIES * (k + 1));
-  size_t nf = 0, no = 0;
-  if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
-  HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
+    for (auto& p : jobsF) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_upper");
+    if (tail_first <= k && !tail_merged) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
+    rec(ST_FRI + 1);
+    // ---- FRI roots -> query rows mod n and mod N (prover.rs:248, 297), the
+    // path / opening requests each rank owns and (device mode) the body fields
+    if (sharded) HIP_OR_THROW(hipMemsetAsync(PL.base, 0, PL.total, st));  // one writer per byte
+    HIP_OR_THROW(hipMemcpyAsync(h_small, d_roots, (size_t)(k + 1) * 32, hipMemcpyDeviceToHost, st));
+  };
+  auto host_3 = [&]() {
+    memcpy(roots.data(), h_small, (size_t)(k + 1) * 32);
+    for (int r = 1; r <= k; r++) tr.absorb("fri_layer_root", roots.data() + 32 * r, 32);
+
+    // ---- queries (prover.rs:248, 297)
+    mark("tr_fri");
+    auto qb = tr.challenge("row_queries", 8 * NUM_QUERIES);
+    for (int i = 0; i < NUM_QUERIES; i++) rows[i] = rd64(qb.data() + 8 * i) % n;
+    auto fb = tr.challenge("row_queries", 8 * NUM_QUERIES);
+    for (int i = 0; i < NUM_QUERIES; i++) frows[i] = rd64(fb.data() + 8 * i) % N;
+
+    mark("queries");
+    // FRI path requests (layer, index, ordinal) for the records this rank owns:
+    // run layers by run owner, replicated layers on rank 0
+    for (int q = 0; q < NUM_QUERIES; q++) {
+      uint64_t* p = &pos[(size_t)q * (k + 1)];
+      p[0] = frows[q];
+      uint64_t len = N;
+      for (int r = 0; r < k; r++) {
+        const uint64_t half = len / 2;
+        for (int side = 0; side < 2; side++) {
+          const uint64_t idx = side ? (p[r] ^ half) : p[r];
+          const int owner = (sharded && r <= rR) ? (int)((idx >> L16_LOG) & (uint64_t)(world - 1)) : 0;
+          if (owner != rank) continue;
+          h_req[3 * nf] = (uint32_t)r;
+          h_req[3 * nf + 1] = (uint32_t)idx;
+          h_req[3 * nf + 2] = (uint32_t)(q * 2 * k + 2 * r + side);
+          nf++;
+        }
+        p[r + 1] = p[r] % half;
+        len = half;
+      }
+    }
+    // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66),
+    // each by the rank owning the row's chunk
+    uint32_t* oreq = h_req + 3 * max_fri_req;
+    size_t ord = 0;
+    auto push_open = [&](int c, uint64_t row) {
+      const uint64_t ch = n >= 1024 ? row >> COL_CHUNK_LOG2 : 0;
+      if (ch >= ch_lo && ch < ch_hi) {
+        uint32_t* rq = oreq + (size_t)OPEN_REQ_WORDS * no;
+        rq[0] = (uint32_t)c;
+        rq[1] = (uint32_t)row;
+        rq[2] = (uint32_t)(row >> 32);
+        rq[3] = (uint32_t)ord;
+        rq[4] = dict_of[c];
+        no++;
+      }
+      ord++;
+    };
+    for (int q = 0; q < NUM_QUERIES; q++) {
+      const uint64_t row = rows[q], ip1 = row + 1 < n ? row + 1 : 0;  // next_wrap
+      for (uint32_t r = 0; r < tau; r++) {
+        push_open(3 + 0 * tau + r, row);   // mv
+        push_open(3 + 0 * tau + r, ip1);   // next_mv
+        push_open(3 + 1 * tau + r, row);   // write_flag
+        push_open(3 + 2 * tau + r, row);   // write_sym
+        push_open(3 + 3 * tau + r, row);   // head
+        push_open(3 + 3 * tau + r, ip1);   // next_head
+        push_open(3 + 4 * tau + r, row);   // win_len
+        push_open(3 + 5 * tau + r, row);   // in_off
+        push_open(3 + 6 * tau + r, row);   // out_off
+      }
+      push_open(1, row);  // is_first
+      push_open(2, row);  // is_last
+      push_open(0, row);  // input_mv
+    }
+  };
+  auto enqueue_D = [&](size_t nf_grid, size_t no_grid, const uint32_t* cnt_f, const uint32_t* cnt_o) {
+    mark("req_copy");
+    const uint32_t* req = d_req;
+    // the openings and the FRI paths write disjoint sections of the proof image
+    // and are both latency-bound small grids: the openings run on the side
+    // stream beside the path kernel, and (single device) their section (~70% of
+    // the proof) goes back over PCIe from there while the paths still run
+    mark("col_open");
+    HIP_OR_THROW(hipEventRecord(ev_fold, st));
+    HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
+    if (stage_ev) HIP_OR_THROW(hipEventRecord(oev[0], st2));
+    ok(launch_col_open(st2, T, d_tmpl, d_outer, outer_stride, logChunks, req + 3 * max_fri_req, (int)no_grid, PL,
+                       d_tabs, d_dlev, d_dplans, d_dtabs, d_dcols, cnt_o),
+       "col_open");
+    if (stage_ev) HIP_OR_THROW(hipEventRecord(oev[1], st2));
+    rec(ST_OPEN + 1);
+    mark("col_open_issued");
+    if (!sharded) HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.fr_off, hipMemcpyDeviceToHost, st2));
+    HIP_OR_THROW(hipEventRecord(ev_tail, st2));
+    mark("open_d2h_issued");
+    ok(launch_fri_paths(st, d_layers, req, (int)nf_grid, PL, cnt_f), "fri_paths");
+    mark("fri_paths_issued");
+    if (sharded) {
+      HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));  // the openings are part of the byte-sum
+      coll("proof_allreduce", 2 * P1 * PL.total / (uint64_t)world, [&] { comm->allreduce_sum_u8(PL.base, PL.total, st); });
+    }
+    rec(ST_PATHS + 1);
+    const uint64_t d2h_from = sharded ? 0 : PL.fr_off;
+    HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes + d2h_from, (const uint8_t*)PL.base + d2h_from,
+                                PL.total - d2h_from, hipMemcpyDeviceToHost, st));
+    mark("proof_d2h_issued");
+    HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), lvals[k], 8, hipMemcpyDeviceToHost, st));
+    if (!sharded) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
+    mark("issued");
+  };
+
+  enqueue_A();
+  sync();
+  mark("sync1");
+  host_1();
+  enqueue_B();
+  sync();
+  mark("sync2");
+  host_2();
+  enqueue_C();
   sync();
   mark("sync3");
-  memcpy(roots.data(), h_small, (size_t)(k + 1) * 32);
-  for (int r = 1; r <= k; r++) tr.absorb("fri_layer_root", roots.data() + 32 * r, 32);
-
-  // ---- queries (prover.rs:248, 297)
-  mark("tr_fri");
-  auto qb = tr.challenge("row_queries", 8 * NUM_QUERIES);
-  for (int i = 0; i < NUM_QUERIES; i++) rows[i] = rd64(qb.data() + 8 * i) % n;
-  auto fb = tr.challenge("row_queries", 8 * NUM_QUERIES);
-  for (int i = 0; i < NUM_QUERIES; i++) frows[i] = rd64(fb.data() + 8 * i) % N;
-
-  mark("queries");
-  // FRI path requests (layer, index, ordinal) for the records this rank owns:
-  // run layers by run owner, replicated layers on rank 0
-  for (int q = 0; q < NUM_QUERIES; q++) {
-    uint64_t* p = &pos[(size_t)q * (k + 1)];
-    p[0] = frows[q];
-    uint64_t len = N;
-    for (int r = 0; r < k; r++) {
-      const uint64_t half = len / 2;
-      for (int side = 0; side < 2; side++) {
-        const uint64_t idx = side ? (p[r] ^ half) : p[r];
-        const int owner = (sharded && r <= rR) ? (int)((idx >> L16_LOG) & (uint64_t)(world - 1)) : 0;
-        if (owner != rank) continue;
-        h_req[3 * nf] = (uint32_t)r;
-        h_req[3 * nf + 1] = (uint32_t)idx;
-        h_req[3 * nf + 2] = (uint32_t)(q * 2 * k + 2 * r + side);
-        nf++;
-      }
-      p[r + 1] = p[r] % half;
-      len = half;
-    }
-  }
-  // column opening requests in proof order (prover.rs:252-292, proof.rs:44-66),
-  // each by the rank owning the row's chunk
-  uint32_t* oreq = h_req + 3 * max_fri_req;
-  size_t ord = 0;
-  auto push_open = [&](int c, uint64_t row) {
-    const uint64_t ch = n >= 1024 ? row >> COL_CHUNK_LOG2 : 0;
-    if (ch >= ch_lo && ch < ch_hi) {
-      uint32_t* rq = oreq + (size_t)OPEN_REQ_WORDS * no;
-      rq[0] = (uint32_t)c;
-      rq[1] = (uint32_t)row;
-      rq[2] = (uint32_t)(row >> 32);
-      rq[3] = (uint32_t)ord;
-      rq[4] = dict_of[c];
-      no++;
-    }
-    ord++;
-  };
-  for (int q = 0; q < NUM_QUERIES; q++) {
-    const uint64_t row = rows[q], ip1 = row + 1 < n ? row + 1 : 0;  // next_wrap
-    for (uint32_t r = 0; r < tau; r++) {
-      push_open(3 + 0 * tau + r, row);   // mv
-      push_open(3 + 0 * tau + r, ip1);   // next_mv
-      push_open(3 + 1 * tau + r, row);   // write_flag
-      push_open(3 + 2 * tau + r, row);   // write_sym
-      push_open(3 + 3 * tau + r, row);   // head
-      push_open(3 + 3 * tau + r, ip1);   // next_head
-      push_open(3 + 4 * tau + r, row);   // win_len
-      push_open(3 + 5 * tau + r, row);   // in_off
-      push_open(3 + 6 * tau + r, row);   // out_off
-    }
-    push_open(1, row);  // is_first
-    push_open(2, row);  // is_last
-    push_open(0, row);  // input_mv
-  }
-  mark("req_copy");
-  const uint32_t* req = d_req;
-  // the openings and the FRI paths write disjoint sections of the proof image
-  // and are both latency-bound small grids: the openings run on the side
-  // stream beside the path kernel, and (single device) their section (~70% of
-  // the proof) goes back over PCIe from there while the paths still run
-  mark("col_open");
-  HIP_OR_THROW(hipEventRecord(ev_fold, st));
-  HIP_OR_THROW(hipStreamWaitEvent(st2, ev_fold, 0));
-  if (stage_ev) HIP_OR_THROW(hipEventRecord(oev[0], st2));
-  ok(launch_col_open(st2, T, d_tmpl, d_outer, outer_stride, logChunks, req + 3 * max_fri_req, (int)no, PL, d_tabs,
-                     d_dlev, d_dplans, d_dtabs, d_dcols, nullptr),
-     "col_open");
-  if (stage_ev) HIP_OR_THROW(hipEventRecord(oev[1], st2));
-  rec(ST_OPEN + 1);
-  mark("col_open_issued");
-  if (!sharded) HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes, PL.base, PL.fr_off, hipMemcpyDeviceToHost, st2));
-  HIP_OR_THROW(hipEventRecord(ev_tail, st2));
-  mark("open_d2h_issued");
-  ok(launch_fri_paths(st, d_layers, req, (int)nf, PL, nullptr), "fri_paths");
-  mark("fri_paths_issued");
-  if (sharded) {
-    HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));  // the openings are part of the byte-sum
-    coll("proof_allreduce", 2 * P1 * PL.total / (uint64_t)world, [&] { comm->allreduce_sum_u8(PL.base, PL.total, st); });
-  }
-  rec(ST_PATHS + 1);
-  const uint64_t d2h_from = sharded ? 0 : PL.fr_off;
-  HIP_OR_THROW(hipMemcpyAsync(h_proof + hdr_bytes + d2h_from, (const uint8_t*)PL.base + d2h_from,
-                              PL.total - d2h_from, hipMemcpyDeviceToHost, st));
-  mark("proof_d2h_issued");
-  HIP_OR_THROW(hipMemcpyAsync(h_small + 8 * (k + 1), lvals[k], 8, hipMemcpyDeviceToHost, st));
-  if (!sharded) HIP_OR_THROW(hipStreamWaitEvent(st, ev_tail, 0));
-  mark("issued");
+  host_3();
+  enqueue_D(nf, no, nullptr, nullptr);
   sync();
   mark("sync4");
   if (htrace) {
@@ -1821,6 +1863,8 @@ static sezkp_ctx* ctx_create(int32_t device, int32_t rank, int32_t world, const 
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_expand, hipEventDisableTiming));
     HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_cols, hipEventDisableTiming));
+    HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_qin, hipEventDisableTiming));
+    HIP_OR_THROW(hipEventCreateWithFlags(&c->ev_qout, hipEventDisableTiming));
     c->tw = tables_for_device(device);
     // SEZKP_FORCE_SHARDED=1 runs the sharded algorithm (and its RCCL calls)
     // with a one-rank communicator: tests it on a single GPU

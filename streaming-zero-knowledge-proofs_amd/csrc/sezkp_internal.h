@@ -355,8 +355,16 @@ struct UpperJob {
   uint32_t wg;
   int to;  // last level to build (0: up to the root)
   uint32_t pad;
+  // sharded cap of a run layer: level `from` (12) comes from the allgathered
+  // run roots (rank-major: rank d's nrun roots at [d nrun, (d + 1) nrun)),
+  // cap node g = root g >> logP of rank g & (P - 1); the job stores it too
+  const uint32_t* gath = nullptr;
+  uint64_t nrun = 0;
+  int logP = 0;
+  int pad2 = 0;
 };
-void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes, int to = 0);
+void plan_upper_jobs(const TreeDev& T, int from, std::vector<std::vector<UpperJob>>& passes, int to = 0,
+                     const uint32_t* gath = nullptr, uint64_t nrun = 0, int logP = 0);
 hipError_t launch_upper_jobs(hipStream_t st, const UpperJob* d_jobs, int njobs);
 
 constexpr int L16_LOG = 12;  // leaves per WG of the 16-leaves-per-lane layer kernel

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Static instruction histogram of one kernel in a gfx950 .s dump
 (hipcc --cuda-device-only -S). Usage: isa_hist.py file.s symbol-substring.
-Weights: measured issue cost per wave64 instruction (tools/valu_rates.hip,
+Weights: measured issue cost per wave64 instruction (tools/micro/valu_rates.hip,
 profiles/r02_valu_rates.txt): full-rate ~1.37, half-rate ~2.37, carry ops
 and v_mad_u64_u32 ~2.58 cycles per SIMD."""
 import re

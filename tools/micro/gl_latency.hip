@@ -5,7 +5,7 @@
 //   sub   a - (p - b): p - b in two VALU ops, then gl_sub's borrow select (no SALU)
 //   sel2  two selects in turn, c2 ? t : s then c1 ? t : r  (no SALU)
 // Also checks the variants bit-identical to gl_add on random canonical inputs.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gl_latency.hip -o tools/gl_latency
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/micro/gl_latency.hip -o tools/micro/gl_latency
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

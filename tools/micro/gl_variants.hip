@@ -1,6 +1,6 @@
 // Throughput + correctness microbenchmark of Goldilocks primitive variants on
 // gfx950 (dev_common.h's canonical ops vs carry-chain / weakly reduced forms).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gl_variants.hip -o tools/gl_variants
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/micro/gl_variants.hip -o tools/micro/gl_variants
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

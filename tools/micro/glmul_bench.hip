@@ -1,5 +1,5 @@
 // Throughput microbenchmark: Goldilocks mul / add and v_mad_u64_u32 on gfx950.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/glmul_bench.hip -o tools/glmul_bench
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/micro/glmul_bench.hip -o tools/micro/glmul_bench
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include "../streaming-zero-knowledge-proofs_amd/csrc/dev_common.h"

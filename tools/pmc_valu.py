@@ -7,7 +7,7 @@ valu_ms = SQ_INSTS_VALU * 2 cycles / (1024 SIMDs * 2.4 GHz): the time the
 kernel's VALU instructions need if every SIMD issued one wave64 instruction
 per 2 cycles (MI355X_MICROARCH.md: 32 lanes/cycle, 2.4 GHz max clock);
 valu_frac = valu_ms / kernel duration. Half-rate instructions (v_alignbit,
-v_add3, v_mad_u64_u32, carry ops: tools/valu_rates.hip) keep a saturated
+v_add3, v_mad_u64_u32, carry ops: tools/micro/valu_rates.hip) keep a saturated
 kernel below 1.0.
 """
 import csv
