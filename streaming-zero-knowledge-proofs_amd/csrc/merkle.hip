@@ -624,14 +624,28 @@ __global__ void __launch_bounds__(256) k_cyc_pack(const uint64_t* __restrict__ c
   const uint64_t k1 = r >> lsp, t = r & ((1ULL << lsp) - 1);
   send[o] = cyc[(k1 << L16_LOG) + (d << lsp) + t];
 }
+// One workgroup per run k1 (S = 4096 values): they arrive as P segments of
+// S/P, one per source rank g, at recv[g M/P + k1 S/P + t], and go to
+// local[k1 S + t P + g]: both sides contiguous through an LDS transpose
+// (segments padded by 32/P words: the transposed reads take distinct banks).
+// Round 5's one-thread-per-value form wrote 8-byte words P apart (~16 us for
+// a P = 8 rank's 2^21 values).
 __global__ void __launch_bounds__(256) k_cyc_unpack(const uint64_t* __restrict__ recv, uint64_t* __restrict__ local,
                                                     uint64_t M, int logP) {
-  const uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // recv index
-  if (o >= M) return;
-  const int lsp = L16_LOG - logP;
-  const uint64_t g = o / (M >> logP), r = o % (M >> logP);
-  const uint64_t k1 = r >> lsp, t = r & ((1ULL << lsp) - 1);
-  local[(k1 << L16_LOG) + (t << logP) + g] = recv[o];
+  __shared__ uint64_t sh[L16_TILE + 32 * 8];
+  const uint64_t k1 = blockIdx.x;
+  const int lsp = L16_LOG - logP, tid = threadIdx.x;
+  const int seg = 1 << lsp, row = seg + (32 >> logP);
+  const uint64_t MP = M >> logP;
+  for (int i = tid; i < (int)L16_TILE; i += 256) {
+    const int g = i >> lsp, t = i & (seg - 1);
+    sh[g * row + t] = recv[(uint64_t)g * MP + k1 * (uint64_t)seg + t];
+  }
+  __syncthreads();
+  for (int j = tid; j < (int)L16_TILE; j += 256) {
+    const int g = j & ((1 << logP) - 1), t = j >> logP;
+    local[(k1 << L16_LOG) + j] = sh[g * row + t];
+  }
 }
 // rank g's runs out of the whole LDE (P = 2, full_lde): local[k1 S + t] =
 // full[(k1 P + g) S + t], two values per lane
@@ -781,7 +795,8 @@ hipError_t launch_cyc_pack(hipStream_t st, const uint64_t* cyc, uint64_t* send, 
 }
 hipError_t launch_cyc_unpack(hipStream_t st, const uint64_t* recv, uint64_t* local, uint64_t M, int logP) {
   if (M % L16_TILE || (1 << logP) > (int)L16_TILE) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_cyc_unpack, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, recv, local, M, logP);
+  if (logP > 3) return hipErrorInvalidValue;  // the LDS padding assumes P <= 8
+  hipLaunchKernelGGL(k_cyc_unpack, dim3((unsigned)(M >> L16_LOG)), dim3(256), 0, st, recv, local, M, logP);
   return hipGetLastError();
 }
 hipError_t launch_runs_extract(hipStream_t st, const uint64_t* full, uint64_t* local, uint64_t M, int logP,
