@@ -453,8 +453,9 @@ def _sliced_worker(rank, world, port, path, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,tau", [(2, 3), (4, 3), (8, 3), (2, 8), (8, 8)])
-def test_sharded_sliced_upload_matches_full(gpu_ok, product, oracle, tmp_path, world, tau):
+@pytest.mark.parametrize("world,tau,zero", [(2, 3, False), (4, 3, False), (8, 3, False), (2, 8, False), (8, 8, False),
+                                            (4, 3, True)])
+def test_sharded_sliced_upload_matches_full(gpu_ok, product, oracle, tmp_path, world, tau, zero):
     """each rank ingests only its slice of a JSONL file (the
     metadata of 1/P of the lines, then the lines over its own rows plus the
     halo) and uploads it with sezkp_ctx_upload_rows. Ragged 333-step blocks
@@ -462,9 +463,12 @@ def test_sharded_sliced_upload_matches_full(gpu_ok, product, oracle, tmp_path, w
     the whole trace (bound to the file's Frontier root), and no rank holds
     the whole trace (row slices of about n / P). tau = 8 takes the 8-tape
     transposition kernel with slice starts that are not multiples of 8
-    (ADVICE r04)."""
+    (ADVICE r04). zero: zero-step blocks (step_hi = step_lo - 1) in the
+    file, some where the ranks' byte slices and row slices begin."""
     T, b, seed = 1 << 15, 333, 17
     blocks = product.synthetic_blocks(T, b, tau, seed)
+    if zero:
+        blocks = insert_zero_step_blocks(blocks, [0, 25, 25, 49, 50, 74, blocks.n_blocks])
     path = tmp_path / "b.jsonl"
     path.write_bytes(blocks.to_jsonl())
     root = blocks.manifest_frontier_root()

@@ -249,3 +249,6 @@ def test_zero_step_blocks_host_side(product, oracle):
     rt = product.BlockSoA.from_cbor(zb.to_cbor())
     assert rt.manifest_root() == zb.manifest_root()
     assert (rt.step_hi == zb.step_hi).all() and (rt.step_start == zb.step_start).all()
+    jl = product.BlockSoA.from_jsonl(zb.to_jsonl())
+    assert (jl.step_hi == zb.step_hi).all() and (jl.step_start == zb.step_start).all()
+    assert jl.manifest_frontier_root() == zb.manifest_frontier_root()
