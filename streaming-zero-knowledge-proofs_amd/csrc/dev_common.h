@@ -255,18 +255,51 @@ __device__ __forceinline__ void b3_parent_quad(const uint32_t (&mw)[7][4], int q
 }
 
 // Parent pq of the LDS image's nodes 2 pq, 2 pq + 1 on the quad of lanes
-// q = lane & 3 (b3_parent_quad): words q and 4 + q in lo / hi.
-template <int W>
+// q = lane & 3 (b3_parent_quad's rounds): words q and 4 + q in lo / hi.
+// AHEAD: the 28 message words read up front (latency-bound chains); else the
+// lane's 4 words of a round read at that round (a compiler barrier per round
+// keeps the reads and their addresses there: 4 live message words, not 28,
+// so the throughput-bound tree kernels keep their occupancy).
+template <int W, bool AHEAD = true>
 __device__ __forceinline__ void lds_parent_quad(uint32_t (*lds)[W], int pq, int q, uint32_t& lo, uint32_t& hi) {
-  uint32_t mw[7][4];
+  if constexpr (AHEAD) {  // latency-bound chains: all 28 words read up front
+    uint32_t mw[7][4];
 #pragma unroll
-  for (int R = 0; R < 7; R++)
+    for (int R = 0; R < 7; R++)
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int j = b3_quad_word(R, k, q);  // message word j: word j & 7 of child j >> 3
-      mw[R][k] = lds[j & 7][2 * pq + (j >> 3)];
-    }
-  b3_parent_quad(mw, q, lo, hi);
+      for (int k = 0; k < 4; k++) {
+        const int j = b3_quad_word(R, k, q);
+        mw[R][k] = lds[j & 7][2 * pq + (j >> 3)];
+      }
+    b3_parent_quad(mw, q, lo, hi);
+    return;
+  }
+  // qv / pv: copies of q / pq the compiler must treat as new each round, so
+  // the 28 word addresses are not all computed (and held) up front
+  int qv = q, pv = pq;
+  auto word = [&](int R, int k) -> uint32_t {
+    const int j = b3_quad_word(R, k, qv);  // message word j: word j & 7 of child j >> 3
+    return lds[j & 7][2 * pv + (j >> 3)];
+  };
+  const uint32_t iv_a = q == 0 ? B3_IV0 : q == 1 ? B3_IV1 : q == 2 ? B3_IV2 : B3_IV3;
+  const uint32_t iv_b = q == 0 ? B3_IV4 : q == 1 ? B3_IV5 : q == 2 ? B3_IV6 : B3_IV7;
+  uint32_t a = iv_a, b = iv_b, c = iv_a, d = q == 2 ? 64u : q == 3 ? B3_ROOT_FLAGS : 0u;
+#pragma unroll
+  for (int R = 0; R < 7; R++) {
+    const uint32_t m0 = word(R, 0), m1 = word(R, 1);
+    const uint32_t m2 = word(R, 2), m3 = word(R, 3);
+    b3_g1(a, b, c, d, m0, m1);
+    b = quad_rot<DPP_QROT1>(b);
+    c = quad_rot<DPP_QROT2>(c);
+    d = quad_rot<DPP_QROT3>(d);
+    b3_g1(a, b, c, d, m2, m3);
+    b = quad_rot<DPP_QROT3>(b);
+    c = quad_rot<DPP_QROT2>(c);
+    d = quad_rot<DPP_QROT1>(d);
+    asm volatile("" : "+v"(qv), "+v"(pv) : : "memory");  // the next round's reads stay after this round
+  }
+  lo = a ^ c;
+  hi = b ^ d;
 }
 
 // ------------------------------------------------------------ node helpers

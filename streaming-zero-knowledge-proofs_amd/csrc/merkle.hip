@@ -60,20 +60,24 @@ __device__ __forceinline__ void store_level_quad(const TreeDev& T, int l, uint64
 // global index wg * (cnt_at_l) + i. A level of at most W / 4 parents runs one
 // parent per quad of lanes (b3_parent_quad): the chain of the last levels is
 // latency-bound, and a quad's compression is a quarter of the instructions
-// per lane of a one-lane compression (round 6). QUAD = false keeps one lane
-// per parent (the throughput-bound tree kernels, whose occupancy is set by
-// their VGPRs: the quad form's 28 message words would cost them waves).
-template <int W, bool QUAD = false>
+// per lane of a one-lane compression (round 6). QMAX: the largest level (in
+// parents) that goes to quads: W / 4 in the latency-bound chains; 32 in the
+// throughput-bound tree kernels, where a level of 64 parents is one full wave
+// step of one-lane compressions but four of quad ones, while 32 or fewer
+// parents leave most of a wave idle in the one-lane form (and when a small
+// launch runs as a single round of workgroups in the same phase, the idle
+// waves are not covered by other workgroups).
+template <int W, int QMAX = 0>
 __device__ __forceinline__ void wg_reduce(uint32_t (*lds)[W], int cnt, int lvl, uint64_t wg, const TreeDev& T,
                                           int stop = 64) {
   const int tid = threadIdx.x;
   while (cnt > 1 && lvl < stop) {
     const int half = cnt >> 1;
-    if (QUAD && 4 * half <= W) {
+    if (half <= QMAX && 4 * half <= W) {
       const int pq = tid >> 2, q = tid & 3;
       const bool act = pq < half;  // whole quads
       uint32_t lo = 0, hi = 0;
-      if (act) lds_parent_quad(lds, pq, q, lo, hi);
+      if (act) lds_parent_quad<W, (QMAX == W / 4)>(lds, pq, q, lo, hi);
       __syncthreads();
       lvl++;
       cnt = half;
@@ -314,7 +318,7 @@ __device__ __forceinline__ void upper_wg(const TreeDev& T, int from, uint64_t wg
     lds_put(lds, tid, h);
   }
   __syncthreads();
-  wg_reduce<MK_THREADS, true>(lds, nact, from + logper, wg, T);
+  wg_reduce<MK_THREADS, MK_THREADS / 4>(lds, nact, from + logper, wg, T);
 }
 
 // grid.y indexes trees of identical shape spaced tree_stride nodes apart.
@@ -392,7 +396,12 @@ __device__ __forceinline__ void layer16_wg(const uint64_t* __restrict__ in, uint
   subtree_regs<LPL, 0>(v, i0, T, h);
   lds_put(lds, tid, h);
   __syncthreads();
-  wg_reduce(lds, MK_THREADS, LPL, wg, T, stop);
+  // quads for the levels of <= 32 parents only in the 1024-leaf form, which
+  // small per-device LDEs (a sharded rank's, <= 2^21 points) launch as one
+  // round of workgroups in the same phase (a P = 8 rank's layer-0 tree 0.099
+  // -> 0.090 ms); with several rounds (the headline's 4096 / 2048-leaf forms,
+  // three proofs in flight) the one-lane form measured 3-5% faster in flight
+  wg_reduce<MK_THREADS, (LPL == L16S_LOG - 8 ? 32 : 0)>(lds, MK_THREADS, LPL, wg, T, stop);
 }
 
 template <int LPL>
@@ -516,7 +525,7 @@ __global__ void __launch_bounds__(TAIL_THREADS) k_fri_tail(TailArgs A) {
     lds_put(lds, tid, h);
   }
   __syncthreads();
-  wg_reduce<TAIL_THREADS, true>(lds, nact, lp, 0, T);
+  wg_reduce<TAIL_THREADS, TAIL_THREADS / 4>(lds, nact, lp, 0, T);
 }
 
 // The same small-layer job as k_fri_tail, run by the first workgroups of the
@@ -591,14 +600,19 @@ __device__ __forceinline__ void fri_tail_wg(const TailArgs& A, int j, uint64_t* 
 // `ntail` workgroups build the layers of <= 2048 leaves (fri_tail_wg).
 // A launch may cover a sub-range of the layers: `layers` then points at its
 // first one and wg_base is that layer's wg_start (wg_start values are global).
-template <int LPL>
+template <int LPL, bool TAIL>
 __global__ void __launch_bounds__(MK_THREADS) k_forest16(const ForestLayer* __restrict__ layers, int nlayers,
                                                          TailArgs A, int ntail, uint64_t* __restrict__ tailbuf,
                                                          uint32_t wg_base) {
   __shared__ uint32_t lds[8][MK_THREADS];
-  if ((int)blockIdx.x < ntail) {
-    fri_tail_wg(A, (int)blockIdx.x, tailbuf, lds);
-    return;
+  // TAIL = false (the sharded launches, whose small layers run in k_fri_tail):
+  // without the tail's fold replay the kernel needs fewer VGPRs, so a small
+  // launch that runs as one round of workgroups fits more of them per SIMD
+  if constexpr (TAIL) {
+    if ((int)blockIdx.x < ntail) {
+      fri_tail_wg(A, (int)blockIdx.x, tailbuf, lds);
+      return;
+    }
   }
   const uint32_t b = blockIdx.x - (uint32_t)ntail + wg_base;
   int l = 0;
@@ -890,17 +904,20 @@ hipError_t launch_forest16(hipStream_t st, const ForestLayer* d_layers, int nlay
   if (tail && (tail->Ls < 0 || tail->Ls >= TAIL_MAX || !tailbuf)) return hipErrorInvalidValue;
   const int ntail = tail ? tail->Ls + 1 : 0;
   const TailArgs none{};
-  if (wg_log == L16_LOG)
-    hipLaunchKernelGGL(k_forest16<4>, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
-                       tail ? *tail : none, ntail, tailbuf, wg_base);
-  else if (wg_log == L16M_LOG)
-    hipLaunchKernelGGL(k_forest16<3>, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
-                       tail ? *tail : none, ntail, tailbuf, wg_base);
-  else if (wg_log == L16S_LOG)
-    hipLaunchKernelGGL(k_forest16<2>, dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st, d_layers, nlayers,
-                       tail ? *tail : none, ntail, tailbuf, wg_base);
-  else
-    return hipErrorInvalidValue;
+#define SEZKP_FOREST(LPL)                                                                                      \
+  do {                                                                                                         \
+    if (tail)                                                                                                  \
+      hipLaunchKernelGGL((k_forest16<LPL, true>), dim3(total_wgs + (uint32_t)ntail), dim3(MK_THREADS), 0, st,   \
+                         d_layers, nlayers, *tail, ntail, tailbuf, wg_base);                                   \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_forest16<LPL, false>), dim3(total_wgs), dim3(MK_THREADS), 0, st, d_layers, nlayers, \
+                         none, 0, tailbuf, wg_base);                                                           \
+  } while (0)
+  if (wg_log == L16_LOG) SEZKP_FOREST(4);
+  else if (wg_log == L16M_LOG) SEZKP_FOREST(3);
+  else if (wg_log == L16S_LOG) SEZKP_FOREST(2);
+  else return hipErrorInvalidValue;
+#undef SEZKP_FOREST
   return hipGetLastError();
 }
 
