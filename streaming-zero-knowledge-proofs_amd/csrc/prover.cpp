@@ -1236,6 +1236,12 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
   const uint64_t row_lo = n >= 1024 ? ch_lo << COL_CHUNK_LOG2 : 0;
   const uint64_t row_hi = n >= 1024 ? ch_hi << COL_CHUNK_LOG2 : n;
   const bool no_deep_poly = getenv("SEZKP_NO_DEEP_POLY") != nullptr;
+  // largest dictionary table above level 0 (entries; SEZKP_DICT_TAB_CAP, for A/Bs)
+  uint32_t dict_tab_cap = DICT_CAP;
+  if (const char* cap = getenv("SEZKP_DICT_TAB_CAP")) {
+    const long v = atol(cap);
+    if (v >= 1 && v <= (long)DICT_CAP) dict_tab_cap = (uint32_t)v;
+  }
   const int nguard = sharded ? comm->world : 1;
   auto check_guards = [&](const uint32_t* g_h, int ng) {
     for (int r = 0; r < ng; r++) {
@@ -1322,7 +1328,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     ok(launch_compose_terms(st2, T, Tm, row_lo, row_hi - row_lo), "compose_terms");
     HIP_OR_THROW(hipEventRecord(ev_cols, st2));
     ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
-                          row_hi - row_lo, d_dlev),
+                          row_hi - row_lo, d_dlev, dict_tab_cap),
        "col_commit_dict");
     HIP_OR_THROW(hipStreamWaitEvent(st, ev_cols, 0));
     // test hook: SEZKP_DEBUG_TRIP_GUARD=<rank> sets that rank's guard word, to

@@ -282,7 +282,8 @@ hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplat
 // rows [row0, row0 + nrows) of every dictionary column (row0, nrows multiples of 4096 or the whole trace)
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev);
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev,
+                              uint32_t tab_cap = DICT_CAP);
 hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);

@@ -1241,7 +1241,7 @@ __device__ __forceinline__ void reduce_parts(const int64_t* pp, uint32_t nparts,
 // lower levels cost more than the misses save. (lo, hi): the column's range;
 // (mlo, mhi): its tape's move range (head columns, has_mv), for the delta plan.
 __device__ __forceinline__ DictPlan make_plan(int64_t lo, int64_t hi, bool has_mv, int64_t mlo, int64_t mhi,
-                                              uint64_t n, uint64_t nrows) {
+                                              uint64_t n, uint64_t nrows, uint32_t tab_cap) {
   DictPlan P{};
   P.min = lo;
   P.K = -1;
@@ -1256,7 +1256,7 @@ __device__ __forceinline__ DictPlan make_plan(int64_t lo, int64_t hi, bool has_m
     // it in scratch memory, and the kernel took ~23 us for 33 tiny workgroups)
 #pragma unroll
     for (int k = 0; k < DICT_LEVELS; k++) {
-      open = open && (1ULL << k) <= n && sz <= DICT_CAP;
+      open = open && (1ULL << k) <= n && sz <= (k ? tab_cap : DICT_CAP);
       if (open) {
         P.pw[k] = (uint32_t)sz;
         tabcost += sz;
@@ -1270,7 +1270,7 @@ __device__ __forceinline__ DictPlan make_plan(int64_t lo, int64_t hi, bool has_m
       if (k > P.K) P.pw[k] = 0;
     // head delta plan (see DictPlan): 4-row groups from (head, 3 moves)
     const uint64_t dR = mhi >= mlo ? (uint64_t)mhi - (uint64_t)mlo + 1 : 0;
-    if (has_mv && P.K <= 1 && n >= 4 && dR && R * R <= DICT_CAP && dR <= 256 && R * dR * dR * dR <= DICT_CAP) {
+    if (has_mv && P.K <= 1 && n >= 4 && dR && R * R <= tab_cap && dR <= 256 && R * dR * dR * dR <= tab_cap) {
       P.K = 2;
       P.delta = 1;
       P.dmin = mlo;
@@ -1363,13 +1363,13 @@ __global__ void __launch_bounds__(TR_THREADS) k_dict_range(TraceDev T, const Col
 // maintenance of ~2000 workgroups disturbs the L2s the commit then gathers from.)
 __global__ void __launch_bounds__(TR_THREADS) k_dict_plan(const int64_t* __restrict__ part, uint32_t nparts,
                                                           uint64_t n, uint64_t nrows, const DictCol* __restrict__ dcols,
-                                                          DictPlan* __restrict__ plans) {
+                                                          DictPlan* __restrict__ plans, uint32_t tab_cap) {
   __shared__ int64_t slo[TR_THREADS / 64], shi[TR_THREADS / 64];
   int64_t lo, hi, mlo = 0, mhi = -1;
   reduce_parts(part + 2 * (uint64_t)blockIdx.x * nparts, nparts, lo, hi, slo, shi);
   const uint32_t mvc = dcols[blockIdx.x].mv;
   if (mvc != NO_DICT) reduce_parts(part + 2 * (uint64_t)mvc * nparts, nparts, mlo, mhi, slo, shi);
-  if (threadIdx.x == 0) plans[blockIdx.x] = make_plan(lo, hi, mvc != NO_DICT, mlo, mhi, n, nrows);
+  if (threadIdx.x == 0) plans[blockIdx.x] = make_plan(lo, hi, mvc != NO_DICT, mlo, mhi, n, nrows, tab_cap);
 }
 
 // entry e of table level `lvl` of one dictionary column
@@ -1605,8 +1605,10 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
 }
 hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev) {
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev,
+                              uint32_t tab_cap) {
   if (ndict == 0) return hipSuccess;
+  if (tab_cap == 0 || tab_cap > DICT_CAP) return hipErrorInvalidValue;
   if (T.n < (1ULL << COL_CHUNK_LOG2)) return hipErrorInvalidValue;
   if (row0 + nrows > T.n || (nrows != T.n && (row0 % DICT_WG_ROWS || nrows % DICT_WG_ROWS))) return hipErrorInvalidValue;
   // parts of 1..8 sweeps: ~64 per column (the partial buffer holds n / 4096)
@@ -1617,7 +1619,8 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
                      row0, row0 + nrows, sweeps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, nrows, d_dcols, d_plans);
+  hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, nrows, d_dcols, d_plans,
+                     tab_cap);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   for (int l = 0; l < DICT_LEVELS; l++) {
     // one flat launch per level (and per DICT_FLAT_MAX columns): all WGs

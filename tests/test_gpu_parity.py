@@ -226,6 +226,11 @@ def test_prove_dictionary_branches_bit_exact(gpu_ok, product, oracle, monkeypatc
     mroot = blocks.manifest_root()
     want = oracle.prove_v1(blocks, mroot)
     assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
+    # smaller tables above level 0 (lower K per column; the A/B switch)
+    for cap in ("16", "4096"):
+        monkeypatch.setenv("SEZKP_DICT_TAB_CAP", cap)
+        assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
+    monkeypatch.delenv("SEZKP_DICT_TAB_CAP")
     monkeypatch.setenv("SEZKP_NO_DICT", "1")
     assert product.StarkV1.prove(blocks, mroot).proof_bytes == want
 
