@@ -67,6 +67,36 @@ def test_ntt_large_matches_openmp_oracle(gpu_ok, product, oracle, log_n):
     np.testing.assert_array_equal(_host(d), x)
 
 
+@pytest.mark.parametrize("log_n", [4, 11, 12, 16, 20, 21, 24])
+def test_ntt_edge_values_match_oracle(gpu_ok, product, oracle, log_n):
+    """Canonical values at the carry / borrow boundaries of the 32-bit-lane
+    Goldilocks arithmetic (0, 1, p - 1, p - 2, eps = 2^32 - 1, 2^32, 2^63,
+    p - eps, ...), drawn at random and as constant runs of p - 1, through
+    every pass form (plain, X16, the 2^20 radix-8 passes, the natural-order
+    DIT, the headline 2^24): forward values against the oracle, then the
+    inverse round trip."""
+    torch = gpu_ok
+    if log_n > 20:
+        oracle.use_mt(int(os.environ.get("OMP_NUM_THREADS", "8")))
+    n = 1 << log_n
+    eps = (1 << 32) - 1
+    edge = np.array([0, 1, 2, P - 1, P - 2, eps, eps + 1, eps - 1, 1 << 32, (1 << 32) + 1, 1 << 63, (1 << 63) - 1,
+                     P - eps, P - eps - 1, P - (1 << 32), (1 << 64) - (1 << 33), P >> 1, (P >> 1) + 1], dtype=np.uint64)
+    rng = np.random.default_rng(log_n)
+    x = edge[rng.integers(0, len(edge), n)]
+    x[: n // 4] = P - 1
+    d = _dev(torch, x)
+    scratch = torch.empty_like(d)
+    assert product.lib.sezkp_gl_ntt(d.data_ptr(), scratch.data_ptr(), log_n, 1, None) == 0
+    torch.cuda.synchronize()
+    got = _host(d)
+    assert (got < P).all()
+    np.testing.assert_array_equal(got, oracle.ntt_forward(x))
+    assert product.lib.sezkp_gl_ntt(d.data_ptr(), scratch.data_ptr(), log_n, -1, None) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d), x)
+
+
 @pytest.mark.parametrize("vec", ["zeros", "delta", "ap"])
 def test_ntt_special_vectors(gpu_ok, product, oracle, vec):
     torch = gpu_ok
@@ -89,6 +119,25 @@ def test_coset_lde_deep_matches_oracle(gpu_ok, product, oracle, log_n):
     n = 1 << log_n
     base = oracle.det_vec(n, 7 + log_n)
     z = 0x1234567890ABCDEF % P
+    want = oracle.lde_deep(base, 3, z)
+    d_in = _dev(torch, base)
+    d_out = torch.empty(8 * n, dtype=torch.int64, device="cuda")
+    assert product.lib.sezkp_gl_coset_lde_deep(d_in.data_ptr(), log_n, 3, 3, z, d_out.data_ptr(), None, None) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d_out), want)
+
+
+@pytest.mark.parametrize("log_n", [5, 13, 18])
+def test_coset_lde_deep_edge_values(gpu_ok, product, oracle, log_n):
+    """The LDE + DEEP path on trace values at the carry / borrow boundaries
+    (p - 1 runs, eps, 2^63, ...) and z = p - 1: every output against the oracle."""
+    torch = gpu_ok
+    n = 1 << log_n
+    eps = (1 << 32) - 1
+    edge = np.array([0, 1, P - 1, P - 2, eps, 1 << 32, 1 << 63, P - eps, (1 << 64) - (1 << 33)], dtype=np.uint64)
+    base = edge[np.random.default_rng(log_n).integers(0, len(edge), n)]
+    base[: n // 2] = P - 1
+    z = P - 1
     want = oracle.lde_deep(base, 3, z)
     d_in = _dev(torch, base)
     d_out = torch.empty(8 * n, dtype=torch.int64, device="cuda")
