@@ -1327,6 +1327,8 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
     // left after the transcript's first round trip
     ok(launch_compose_terms(st2, T, Tm, row_lo, row_hi - row_lo), "compose_terms");
     HIP_OR_THROW(hipEventRecord(ev_cols, st2));
+    // (the commit of the K <= 2 columns on a third stream beside table levels
+    // 3..4 measured slower, round 6: profiles/r06/ab/dict_split_streams_ab.txt)
     ok(launch_dict_commit(st, T, d_tmpl, d_dcols, n_dict, d_dpart, d_dplans, d_dtabs, d_outer, outer_stride, row_lo,
                           row_hi - row_lo, d_dlev, dict_tab_cap),
        "col_commit_dict");
@@ -1624,6 +1626,7 @@ size_t sezkp_ctx::prove_body(const uint8_t mroot[32]) {
         r += F;
       }
       if (!rep16.empty()) rep_src = lvals[rep16.back()];
+      // (the tail launched after the forest instead measured even, round 6)
       launch_tail(rep_src);
       ok(launch_forest16(st, d_forest, n_forest, forest_wgs, nullptr, nullptr, 0, tree_wg_log), "fri_forest");
       for (auto& p : jobsLR) ok(launch_upper_jobs(st, d_jobs + p.first, p.second), "fri_runroots");

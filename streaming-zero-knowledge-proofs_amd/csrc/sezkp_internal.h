@@ -284,6 +284,18 @@ hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTempla
                               int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
                               uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev,
                               uint32_t tab_cap = DICT_CAP);
+// the same in three steps, so the commit of the columns whose table level K
+// is built early can run beside the later levels: ranges + plans, table
+// levels [lvl_lo, lvl_hi), and the commit of the columns with kmin <= K <= kmax
+hipError_t launch_dict_prepare(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
+                               int ndict, int64_t* d_part, DictPlan* d_plans, uint64_t row0, uint64_t nrows,
+                               uint32_t tab_cap = DICT_CAP);
+hipError_t launch_dict_levels(hipStream_t st, const ColTemplate* d_tmpl, const DictCol* d_dcols, int ndict,
+                              const DictPlan* d_plans, uint32_t* d_dtabs, int lvl_lo, int lvl_hi);
+hipError_t launch_dict_commit_cols(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl,
+                                   const DictCol* d_dcols, int ndict, const DictPlan* d_plans,
+                                   const uint32_t* d_dtabs, uint32_t* outer_nodes, uint64_t outer_stride_nodes,
+                                   uint64_t row0, uint64_t nrows, uint32_t* d_dlev, int kmin, int kmax);
 hipError_t launch_col_commit_pw(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_pw_cols,
                                 int n_pw_cols, const uint32_t* d_chunks, int nchunks, const uint32_t* tabs,
                                 uint32_t* outer_nodes, uint64_t outer_stride_nodes, uint32_t* d_err);

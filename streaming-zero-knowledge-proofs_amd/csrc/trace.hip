@@ -1491,7 +1491,7 @@ __global__ void __launch_bounds__(DICT_WG_LANES) k_col_commit_dict(TraceDev T, c
                                                                    const uint32_t* __restrict__ tabs,
                                                                    uint32_t* __restrict__ outer, uint64_t outer_stride,
                                                                    uint64_t row0, uint64_t row_end,
-                                                                   uint32_t* __restrict__ dlev) {
+                                                                   uint32_t* __restrict__ dlev, int kmin, int kmax) {
   __shared__ uint32_t lds[2][8][DICT_WG_LANES];
   // (XCD-interleaved column orders, so that one XCD's workgroups gather
   // from one column's tables at a time, measured slower in rounds 1 and 3)
@@ -1500,6 +1500,7 @@ __global__ void __launch_bounds__(DICT_WG_LANES) k_col_commit_dict(TraceDev T, c
   const ColTemplate* ctp = tmpl + dc.col;
   const ColTemplate ct = *ctp;
   const DictPlan P = plans[by];
+  if (P.K < kmin || P.K > kmax) return;  // the other launch's column (uniform per WG)
   const uint32_t* tab = tabs + 8 * dc.tab;
   const int lane = threadIdx.x;
   // high-K columns give each lane more rows (fewer LDS levels per row)
@@ -1603,40 +1604,68 @@ hipError_t launch_col_tables(hipStream_t st, const TraceDev& T, const ColTemplat
                      blk_cnt);
   return hipGetLastError();
 }
-hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
-                              int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
-                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev,
-                              uint32_t tab_cap) {
-  if (ndict == 0) return hipSuccess;
-  if (tab_cap == 0 || tab_cap > DICT_CAP) return hipErrorInvalidValue;
+static hipError_t dict_shape_ok(const TraceDev& T, uint64_t row0, uint64_t nrows) {
   if (T.n < (1ULL << COL_CHUNK_LOG2)) return hipErrorInvalidValue;
   if (row0 + nrows > T.n || (nrows != T.n && (row0 % DICT_WG_ROWS || nrows % DICT_WG_ROWS))) return hipErrorInvalidValue;
+  return hipSuccess;
+}
+hipError_t launch_dict_prepare(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
+                               int ndict, int64_t* d_part, DictPlan* d_plans, uint64_t row0, uint64_t nrows,
+                               uint32_t tab_cap) {
+  if (ndict == 0) return hipSuccess;
+  hipError_t e = dict_shape_ok(T, row0, nrows);
+  if (e != hipSuccess) return e;
+  if (tab_cap == 0 || tab_cap > DICT_CAP) return hipErrorInvalidValue;
   // parts of 1..8 sweeps: ~64 per column (the partial buffer holds n / 4096)
   const int sweeps = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, nrows / (64ull * DICT_RANGE_STEP)));
   const uint64_t prow = (uint64_t)sweeps * DICT_RANGE_STEP;
   const uint32_t nparts = (uint32_t)((nrows + prow - 1) / prow);
   hipLaunchKernelGGL(k_dict_range, dim3(nparts, ndict), dim3(TR_THREADS), 0, st, T, d_tmpl, d_dcols, d_part, nparts,
                      row0, row0 + nrows, sweeps);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_dict_plan, dim3(ndict), dim3(TR_THREADS), 0, st, d_part, nparts, T.n, nrows, d_dcols, d_plans,
                      tab_cap);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  for (int l = 0; l < DICT_LEVELS; l++) {
+  return hipGetLastError();
+}
+hipError_t launch_dict_levels(hipStream_t st, const ColTemplate* d_tmpl, const DictCol* d_dcols, int ndict,
+                              const DictPlan* d_plans, uint32_t* d_dtabs, int lvl_lo, int lvl_hi) {
+  if (lvl_lo < 0 || lvl_hi > DICT_LEVELS) return hipErrorInvalidValue;
+  for (int l = lvl_lo; l < lvl_hi; l++) {
     // one flat launch per level (and per DICT_FLAT_MAX columns): all WGs
     // share every column's entries
     for (int c0 = 0; c0 < ndict; c0 += DICT_FLAT_MAX) {
       const int nc = ndict - c0 < DICT_FLAT_MAX ? ndict - c0 : DICT_FLAT_MAX;
       hipLaunchKernelGGL(k_dict_level, dim3(DICT_FLAT_WGS), dim3(TR_THREADS), 0, st, d_tmpl, d_dcols + c0,
                          d_plans + c0, d_dtabs, nc, l);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
     }
   }
+  return hipSuccess;
+}
+hipError_t launch_dict_commit_cols(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl,
+                                   const DictCol* d_dcols, int ndict, const DictPlan* d_plans,
+                                   const uint32_t* d_dtabs, uint32_t* outer_nodes, uint64_t outer_stride_nodes,
+                                   uint64_t row0, uint64_t nrows, uint32_t* d_dlev, int kmin, int kmax) {
+  if (ndict == 0) return hipSuccess;
+  hipError_t e = dict_shape_ok(T, row0, nrows);
+  if (e != hipSuccess) return e;
   const uint64_t wg_rows = (uint64_t)DICT_WG_LANES << DICT_LANE_LOG;  // rows of a WG at a = 0
   const unsigned gx = (unsigned)((nrows + wg_rows - 1) / wg_rows);
   hipLaunchKernelGGL(k_col_commit_dict, dim3(gx, ndict), dim3(DICT_WG_LANES), 0, st, T, d_tmpl, d_dcols, d_plans, d_dtabs,
-                     outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev);
+                     outer_nodes, outer_stride_nodes, row0, row0 + nrows, d_dlev, kmin, kmax);
   return hipGetLastError();
+}
+hipError_t launch_dict_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const DictCol* d_dcols,
+                              int ndict, int64_t* d_part, DictPlan* d_plans, uint32_t* d_dtabs, uint32_t* outer_nodes,
+                              uint64_t outer_stride_nodes, uint64_t row0, uint64_t nrows, uint32_t* d_dlev,
+                              uint32_t tab_cap) {
+  hipError_t e = launch_dict_prepare(st, T, d_tmpl, d_dcols, ndict, d_part, d_plans, row0, nrows, tab_cap);
+  if (e == hipSuccess && ndict) e = launch_dict_levels(st, d_tmpl, d_dcols, ndict, d_plans, d_dtabs, 0, DICT_LEVELS);
+  if (e == hipSuccess)
+    e = launch_dict_commit_cols(st, T, d_tmpl, d_dcols, ndict, d_plans, d_dtabs, outer_nodes, outer_stride_nodes, row0,
+                                nrows, d_dlev, -1, DICT_LEVELS);
+  return e;
 }
 
 hipError_t launch_col_commit(hipStream_t st, const TraceDev& T, const ColTemplate* d_tmpl, const uint32_t* d_work,
