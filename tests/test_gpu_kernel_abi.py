@@ -112,6 +112,25 @@ def test_fri_fold_matches_oracle(gpu_ok, product, oracle, log_out):
     np.testing.assert_array_equal(_host(d_out), want)
 
 
+@pytest.mark.parametrize("beta", [0, 1, P - 1, (1 << 32) - 1, 1 << 63, P - (1 << 32)])
+def test_fri_fold_edge_values(gpu_ok, product, beta):
+    """fri.rs fold (lo + beta * hi) on values at the carry / borrow boundaries
+    of the 32-bit-lane arithmetic, with boundary betas: exact against Python
+    integers."""
+    torch = gpu_ok
+    n = 1 << 12
+    eps = (1 << 32) - 1
+    edge = np.array([0, 1, P - 1, P - 2, eps, eps + 1, 1 << 63, P - eps, (1 << 64) - (1 << 33)], dtype=np.uint64)
+    vals = edge[np.random.default_rng(beta % 1000).integers(0, len(edge), 2 * n)]
+    vals[: n // 2] = P - 1
+    vals[n: n + n // 2] = P - 1
+    want = np.array([(int(vals[i]) + beta * int(vals[i + n])) % P for i in range(n)], dtype=np.uint64)
+    d_in = _dev(torch, vals)
+    d_out = torch.empty(n, dtype=torch.int64, device="cuda")
+    assert product.lib.sezkp_fri_fold(d_in.data_ptr(), n, beta, d_out.data_ptr(), None) == 0
+    np.testing.assert_array_equal(_host(d_out), want)
+
+
 @pytest.mark.parametrize("log_n,log_blowup,shift", [(0, 3, 3), (4, 3, 7), (5, 0, 5), (6, 1, 3), (8, 2, 11),
                                                     (10, 3, 2 ** 40 + 1), (13, 3, P - 1), (16, 3, 7)])
 def test_coset_lde_deep_shift_and_leaves(gpu_ok, product, oracle, log_n, log_blowup, shift):
