@@ -1095,12 +1095,15 @@ def measure_configs(args, torch):
         assert lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, -1, None) == 0
     torch.cuda.synchronize()
     ok = bool(torch.equal(d, x))
-    reps = 50
+    # on torch's current stream (the one its events record on), 200 round
+    # trips as tools/c2_probe.py: 50 read ~3 us higher (the first ones)
+    stream = torch.cuda.current_stream().cuda_stream
+    reps = 200
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, 1, None)
-        lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, -1, None)
+        lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, 1, stream)
+        lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), 20, -1, stream)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
@@ -1116,15 +1119,15 @@ def measure_configs(args, torch):
         x = torch.randint(0, 0xFFFFFFFF00000001 >> 1, (m,), dtype=torch.int64, device="cuda", generator=g)
         d, s = x.clone(), torch.empty_like(x)
         for _ in range(10 if lg < 26 else 5):
-            lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, 1, None)
-            lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, -1, None)
+            lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, 1, stream)
+            lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, -1, stream)
         torch.cuda.synchronize()
         ok = bool(torch.equal(d, x))
         reps = 50 if lg < 26 else 20
         e0.record()
         for _ in range(reps):
-            lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, 1, None)
-            lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, -1, None)
+            lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, 1, stream)
+            lib.sezkp_gl_ntt(d.data_ptr(), s.data_ptr(), lg, -1, stream)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / (2 * reps)
