@@ -1484,6 +1484,8 @@ __device__ __forceinline__ void dict_lane(const Key* p, const DictPlan& P, const
 // the column's outer tree. Requires n >= 1024; rows [row0, row_end) may end
 // inside a workgroup (small sharded slices): lanes and parents past row_end
 // are skipped (their LDS slots hold garbage that feeds only skipped parents).
+// (__launch_bounds__(256, 5) for 5 waves per SIMD: 96 VGPRs with 97 spilled to
+// scratch, 291-293 vs 280-284 us per launch, round 6: not kept)
 constexpr int DICT_WG_LANES = 256;
 __global__ void __launch_bounds__(DICT_WG_LANES) k_col_commit_dict(TraceDev T, const ColTemplate* __restrict__ tmpl,
                                                                    const DictCol* __restrict__ dcols,
